@@ -1,0 +1,211 @@
+// ato_capi.hip -- the C ABI of libato.so (include/ato.h): handle lifetime, sparsity, bounds,
+// and dispatch of ato_eval to the per-model launchers (ato_inst.hip).
+#include <hip/hip_runtime.h>
+#include <string>
+#include <new>
+#include "ato_kernels.hpp"
+
+struct ato_handle {
+    ato::Layout L;
+    int device = 0;
+    ato::ProbD pd{};            // device-pointer copy of L.p
+    double* d_geom = nullptr;
+    double* d_node_s = nullptr;
+    double* d_interval_s = nullptr;
+    double* d_spheres = nullptr;
+    ato_gate* d_gates = nullptr;
+    int32_t* d_seg = nullptr;
+    int32_t* d_tail = nullptr;
+    void* d_fpart = nullptr;    // [N][reserved] doubles (reused for float)
+    int32_t reserved = 0;
+    std::vector<hipEvent_t> events;   // 3 per timed call
+    int32_t timed_calls = 0;
+};
+
+static thread_local std::string g_last_error;
+
+static int fail(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+
+#define ATO_HIP(call)                                                                        \
+    do {                                                                                     \
+        hipError_t e_ = (call);                                                              \
+        if (e_ != hipSuccess) return fail(ATO_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+template <class V>
+static int upload(const std::vector<V>& host, V** dev) {
+    *dev = nullptr;
+    if (host.empty()) return ATO_OK;
+    ATO_HIP(hipMalloc((void**)dev, host.size() * sizeof(V)));
+    ATO_HIP(hipMemcpy(*dev, host.data(), host.size() * sizeof(V), hipMemcpyHostToDevice));
+    return ATO_OK;
+}
+
+static void release(ato_handle* h) {
+    if (!h) return;
+    (void)hipFree(h->d_geom);
+    (void)hipFree(h->d_node_s);
+    (void)hipFree(h->d_interval_s);
+    (void)hipFree(h->d_spheres);
+    (void)hipFree(h->d_gates);
+    (void)hipFree(h->d_seg);
+    (void)hipFree(h->d_tail);
+    (void)hipFree(h->d_fpart);
+    for (hipEvent_t e : h->events) (void)hipEventDestroy(e);
+    h->events.clear();
+}
+
+extern "C" {
+
+const char* ato_last_error(void) { return g_last_error.c_str(); }
+
+const char* ato_version(void) { return "ato 1 gfx950"; }
+
+int ato_create(const ato_problem_desc* desc, ato_handle** out) {
+    if (!desc || !out) return fail(ATO_ERR_ARG, "null argument");
+    *out = nullptr;
+    ato_handle* h = new (std::nothrow) ato_handle();
+    if (!h) return fail(ATO_ERR_ARG, "out of host memory");
+    std::string err = h->L.build(*desc);
+    if (!err.empty()) {
+        delete h;
+        return fail(err.find("not supported") != std::string::npos ? ATO_ERR_UNSUPPORTED : ATO_ERR_ARG, err);
+    }
+    int rc;
+    if (hipGetDevice(&h->device) != hipSuccess) {
+        delete h;
+        return fail(ATO_ERR_HIP, "no HIP device");
+    }
+    if ((rc = upload(h->L.geom, &h->d_geom)) || (rc = upload(h->L.node_s, &h->d_node_s)) ||
+        (rc = upload(h->L.interval_s, &h->d_interval_s)) || (rc = upload(h->L.spheres, &h->d_spheres)) ||
+        (rc = upload(h->L.gates, &h->d_gates)) || (rc = upload(h->L.seg, &h->d_seg)) ||
+        (rc = upload(h->L.tail, &h->d_tail))) {
+        release(h);
+        delete h;
+        return rc;
+    }
+    h->pd = h->L.p;
+    h->pd.geom = h->d_geom;
+    h->pd.node_s = h->d_node_s;
+    h->pd.interval_s = h->d_interval_s;
+    h->pd.spheres = h->d_spheres;
+    h->pd.gates = h->d_gates;
+    h->pd.seg = h->d_seg;
+    h->pd.tail = h->d_tail;
+    *out = h;
+    return ATO_OK;
+}
+
+int ato_destroy(ato_handle* h) {
+    if (!h) return ATO_OK;
+    release(h);
+    delete h;
+    return ATO_OK;
+}
+
+int ato_sizes(const ato_handle* h, int32_t* nw, int32_t* ng, int32_t* nnz) {
+    if (!h) return fail(ATO_ERR_ARG, "null handle");
+    if (nw) *nw = h->L.p.nw;
+    if (ng) *ng = h->L.p.ng;
+    if (nnz) *nnz = h->L.p.nnz;
+    return ATO_OK;
+}
+
+int ato_sparsity(const ato_handle* h, const int32_t** row_ptr, const int32_t** col) {
+    if (!h) return fail(ATO_ERR_ARG, "null handle");
+    if (row_ptr) *row_ptr = h->L.row_ptr.data();
+    if (col) *col = h->L.col.data();
+    return ATO_OK;
+}
+
+int ato_bounds(const ato_handle* h, double* lbg, double* ubg) {
+    if (!h) return fail(ATO_ERR_ARG, "null handle");
+    for (size_t i = 0; i < h->L.lbg.size(); ++i) {
+        if (lbg) lbg[i] = h->L.lbg[i];
+        if (ubg) ubg[i] = h->L.ubg[i];
+    }
+    return ATO_OK;
+}
+
+int ato_reserve(ato_handle* h, int32_t max_batch) {
+    if (!h || max_batch < 1) return fail(ATO_ERR_ARG, "bad reserve arguments");
+    if (max_batch <= h->reserved) return ATO_OK;
+    if (h->d_fpart) ATO_HIP(hipFree(h->d_fpart));
+    h->d_fpart = nullptr;
+    h->reserved = 0;
+    ATO_HIP(hipMalloc(&h->d_fpart, (size_t)h->L.p.N * max_batch * sizeof(double)));
+    h->reserved = max_batch;
+    return ATO_OK;
+}
+
+}  // extern "C"
+
+template <class T>
+static int eval_impl(ato_handle* h, int32_t batch, int32_t layout, const T* w, T* g, T* jac, T* f,
+                     T* grad_f, void* stream) {
+    if (!h) return fail(ATO_ERR_ARG, "null handle");
+    if (batch < 1) return fail(ATO_ERR_ARG, "batch must be >= 1");
+    if (layout != ATO_LAYOUT_INTERLEAVED && layout != ATO_LAYOUT_INSTANCE_MAJOR)
+        return fail(ATO_ERR_ARG, "unknown layout");
+    if (!w) return fail(ATO_ERR_ARG, "w is null");
+    const bool wf = f || grad_f;
+    if (wf && !(f && grad_f)) return fail(ATO_ERR_ARG, "f and grad_f must be requested together");
+    if (wf && batch > h->reserved) {
+        int rc = ato_reserve(h, batch);
+        if (rc) return rc;
+    }
+    const ato::ProbD& p = h->pd;
+    hipError_t e = hipSuccess;
+    ato::with_model(p, [&]<class M>() {
+        hipEvent_t* ev = nullptr;
+        if ((size_t)(h->timed_calls + 1) * 3 <= h->events.size()) ev = &h->events[(size_t)h->timed_calls++ * 3];
+        e = ato::launch_eval<M, T>(p, batch, layout, w, g, jac, grad_f, (T*)h->d_fpart, f, (hipStream_t)stream,
+                                   ev);
+    });
+    if (e != hipSuccess) return fail(ATO_ERR_HIP, std::string("kernel launch: ") + hipGetErrorString(e));
+    return ATO_OK;
+}
+
+extern "C" int ato_timing(ato_handle* h, int32_t max_calls) {
+    if (!h || max_calls < 0) return fail(ATO_ERR_ARG, "bad timing arguments");
+    for (hipEvent_t e : h->events) ATO_HIP(hipEventDestroy(e));
+    h->events.clear();
+    h->timed_calls = 0;
+    for (int i = 0; i < 3 * max_calls; ++i) {
+        hipEvent_t e;
+        ATO_HIP(hipEventCreate(&e));
+        h->events.push_back(e);
+    }
+    return ATO_OK;
+}
+
+extern "C" int ato_timing_read(ato_handle* h, double* eval_ms, double* reduce_ms, int32_t* calls) {
+    if (!h) return fail(ATO_ERR_ARG, "null handle");
+    double se = 0.0, sr = 0.0;
+    for (int32_t c = 0; c < h->timed_calls; ++c) {
+        hipEvent_t* ev = &h->events[(size_t)c * 3];
+        ATO_HIP(hipEventSynchronize(ev[2]));
+        float a = 0.f, b = 0.f;
+        ATO_HIP(hipEventElapsedTime(&a, ev[0], ev[1]));
+        ATO_HIP(hipEventElapsedTime(&b, ev[1], ev[2]));
+        se += a;
+        sr += b;
+    }
+    if (eval_ms) *eval_ms = se;
+    if (reduce_ms) *reduce_ms = sr;
+    if (calls) *calls = h->timed_calls;
+    return ATO_OK;
+}
+
+extern "C" int ato_eval(ato_handle* h, int32_t batch, int32_t layout, const double* w, double* g,
+                        double* jac, double* f, double* grad_f, void* stream) {
+    return eval_impl<double>(h, batch, layout, w, g, jac, f, grad_f, stream);
+}
+
+extern "C" int ato_eval_f32(ato_handle* h, int32_t batch, int32_t layout, const float* w, float* g,
+                            float* jac, float* f, float* grad_f, void* stream) {
+    return eval_impl<float>(h, batch, layout, w, g, jac, f, grad_f, stream);
+}

@@ -1,0 +1,292 @@
+// ato_layout.hpp -- host side: problem validation, row order, CSR pattern, bounds.
+//
+// Runs every segment program of ato_program.hpp in pattern mode and lays the segments
+// out in the reference's constraint order:
+//   [equal-h rows (global)]                         base_raceline.py:891-905
+//   per interval n:                                 base_raceline.py:393-396
+//     collocation nodes k = 0..K                    :398-434
+//     regularity rows (masked nodes)                :1114-1130
+//     model stage constraints (point mass)          :436-451
+//     continuity (n >= 1)                           :460-490 / :1132-1163
+//     fixed-s rows (parametric)                     :1165-1181
+//   base loop closure (closed point mass)           :357-358, :492-514, :1183-1227
+//   gates                                           :907-918 / :986-1032
+//   obstacle-tube spheres                           :1293-1310
+//   drone loop closure (closed drone)               drone_raceline.py:150-156
+// Header-only so the HIP library and the CPU test harness share it.
+#pragma once
+#include <string>
+#include <vector>
+#include <cstring>
+#include <cmath>
+#include "ato_program.hpp"
+
+namespace ato {
+
+struct SegPat {
+    std::vector<int32_t> rowlen, cols;
+    std::vector<double> lb, ub;
+};
+
+struct PatSink {
+    SegPat* sp;
+    int last = -1, cur = 0;
+    bool sorted = true;
+    void jac(int col, double) {
+        if (col <= last) sorted = false;
+        last = col;
+        sp->cols.push_back(col);
+        ++cur;
+    }
+    void row(double, double lb, double ub) {
+        sp->rowlen.push_back(cur);
+        sp->lb.push_back(lb);
+        sp->ub.push_back(ub);
+        cur = 0;
+        last = -1;
+    }
+};
+
+struct OnesW {
+    double operator()(int) const { return 1.0; }
+};
+
+// model dispatch: calls f.template operator()<Model>() for the problem's model variant
+template <class F>
+bool with_model(const ProbD& p, F&& f) {
+    if (p.model == ATO_MODEL_DRONE) {
+        if (p.att == ATO_ATT_ESP) {
+            if (p.frame == GLOBAL) { f.template operator()<DroneModel<ESP, GLOBAL>>(); return true; }
+            if (p.frame == PARAM_GR) { f.template operator()<DroneModel<ESP, PARAM_GR>>(); return true; }
+            if (p.frame == PARAM_REL) { f.template operator()<DroneModel<ESP, PARAM_REL>>(); return true; }
+        } else if (p.att == ATO_ATT_YPR) {
+            if (p.frame == GLOBAL) { f.template operator()<DroneModel<YPR, GLOBAL>>(); return true; }
+            if (p.frame == PARAM_GR) { f.template operator()<DroneModel<YPR, PARAM_GR>>(); return true; }
+            if (p.frame == PARAM_REL) { f.template operator()<DroneModel<YPR, PARAM_REL>>(); return true; }
+        }
+    } else if (p.model == ATO_MODEL_POINT) {
+        if (p.frame == GLOBAL) { f.template operator()<PointModel<GLOBAL>>(); return true; }
+        if (p.frame == PARAM_GR) { f.template operator()<PointModel<PARAM_GR>>(); return true; }
+        if (p.frame == PARAM_REL) { f.template operator()<PointModel<PARAM_REL>>(); return true; }
+    }
+    return false;
+}
+
+// Run one segment of the given kind with any sink / accessor.
+template <class M, class T, class W, class S>
+ATO_HD void run_node_seg(const ProbD& p, int kind, int n, int k, const W& w, S& s) {
+    switch (kind) {
+        case SEG_COLLOC: seg_colloc<M, T>(p, n, k, w, s); break;
+        case SEG_REG: seg_reg<M, T>(p, n, k, w, s); break;
+        case SEG_STAGE: seg_stage<M, T>(p, n, k, w, s); break;
+        case SEG_SPHERE: seg_sphere<M, T>(p, n, k, w, s); break;
+        case SEG_CONT: seg_cont<M, T>(p, n, w, s); break;
+        case SEG_SROWS: seg_srows<M, T>(p, n, w, s); break;
+        default: break;
+    }
+}
+
+template <class M, class T, class W, class S>
+ATO_HD void run_tail_seg(const ProbD& p, int kind, int index, const W& w, S& s) {
+    switch (kind) {
+        case TAIL_HEQ: seg_heq<M, T>(p, w, s); break;
+        case TAIL_CLOSURE_BASE: seg_closure_base<M, T>(p, w, s); break;
+        case TAIL_GATE: seg_gate<M, T>(p, index, w, s); break;
+        case TAIL_DRONE_CLOSURE: seg_drone_closure<M, T>(p, w, s); break;
+        default: break;
+    }
+}
+
+struct Layout {
+    ProbD p{};                        // host pointers into the vectors below
+    std::vector<double> geom, node_s, interval_s, spheres;
+    std::vector<ato_gate> gates;
+    std::vector<int32_t> seg, tail;   // segment tables (see ProbD)
+    std::vector<int32_t> row_ptr, col;
+    std::vector<double> lbg, ubg;
+    int nz = 0, nu = 0;
+
+    void rebind() {
+        p.geom = geom.data();
+        p.node_s = node_s.data();
+        p.interval_s = interval_s.data();
+        p.gates = gates.data();
+        p.spheres = spheres.empty() ? nullptr : spheres.data();
+        p.seg = seg.data();
+        p.tail = tail.data();
+    }
+
+    // returns empty string on success
+    std::string build(const ato_problem_desc& d) {
+        if (d.abi_version != ATO_ABI_VERSION) return "abi_version mismatch";
+        if (d.N < 1) return "N must be >= 1";
+        if (d.transcription != ATO_TRANS_COLLOCATION) return "RK4 transcription not supported by this build";
+        if (d.K < 1 || d.K > ATO_KMAX) return "K out of range [1, ATO_KMAX]";
+        if (d.closed && d.N < 2) return "closed problems need N >= 2";
+        if (!d.closed) return "open (non-periodic) racelines are not supported by this build";
+        std::memset(&p, 0, sizeof(p));
+        p.model = d.model;
+        p.att = d.attitude;
+        p.frame = d.frame == ATO_FRAME_GLOBAL ? GLOBAL : (d.global_r ? PARAM_GR : PARAM_REL);
+        p.trans = d.transcription;
+        p.N = d.N;
+        p.K = d.K;
+        p.K1 = d.K + 1;
+        p.P = d.N * (d.K + 1);
+        if (d.model == ATO_MODEL_DRONE) {
+            nz = d.attitude == ATO_ATT_ESP ? 13 : 12;
+            nu = 4;
+        } else if (d.model == ATO_MODEL_POINT) {
+            nz = 6;
+            nu = 3;
+        } else {
+            return "unknown model";
+        }
+        if (d.model == ATO_MODEL_DRONE && d.attitude != ATO_ATT_ESP && d.attitude != ATO_ATT_YPR)
+            return "unknown attitude parameterisation";
+        p.NZ = nz;
+        p.NU = nu;
+        p.NV = nz + 2 * nu;
+        p.nw = p.N + p.P * p.NV;
+        p.closed = d.closed;
+        p.cleanly_closed = d.cleanly_closed;
+        p.quat_flip = d.quat_flip;
+        p.force_reg = d.force_regularity;
+        p.n_gates = d.n_gates;
+        p.phase_len = d.frame == ATO_FRAME_GLOBAL ? d.phase_len : 0;
+        p.has_spheres = d.has_spheres;
+        p.euler_wraps = d.euler_wraps;
+        p.gamma = d.gamma;
+        p.veh.m = d.m;
+        p.veh.g = d.g;
+        for (int i = 0; i < 3; ++i) {
+            p.veh.b[i] = d.b[i];
+            p.veh.I[i] = d.I[i];
+            p.veh.bw[i] = d.bw[i];
+        }
+        p.veh.l = d.l;
+        p.veh.kt = d.kt;
+        p.veh.Tmax = d.T_max;
+        std::memcpy(p.Rc, d.Rcost, sizeof(p.Rc));
+        std::memcpy(p.dRc, d.dRcost, sizeof(p.dRc));
+        std::memcpy(p.tau, d.tau, sizeof(p.tau));
+        std::memcpy(p.Bq, d.Bq, sizeof(p.Bq));
+        // C is stored with row stride K+1
+        for (int j = 0; j < p.K1; ++j)
+            for (int r = 0; r < p.K1; ++r) p.C[j * p.K1 + r] = d.C[j * p.K1 + r];
+        std::memcpy(p.D, d.D, sizeof(p.D));
+        std::memcpy(p.A_skew, d.A_skew, sizeof(p.A_skew));
+
+        const bool param = d.frame == ATO_FRAME_PARAMETRIC;
+        if (param && (!d.node_geom || !d.interval_s)) return "parametric frame needs node_geom and interval_s";
+        if (d.n_gates < 0 || (d.n_gates > 0 && !d.gates)) return "bad gates";
+        if (d.has_spheres && !d.spheres) return "has_spheres without spheres table";
+        if (d.frame == ATO_FRAME_GLOBAL && d.phase_len < 0) return "bad phase_len";
+
+        geom.assign((size_t)p.P * ATO_GEOM_WIDTH, 0.0);
+        if (d.node_geom) std::memcpy(geom.data(), d.node_geom, geom.size() * sizeof(double));
+        node_s.assign(p.P, 0.0);
+        if (d.node_s) std::memcpy(node_s.data(), d.node_s, node_s.size() * sizeof(double));
+        interval_s.assign(p.N + 1, 0.0);
+        if (d.interval_s) std::memcpy(interval_s.data(), d.interval_s, interval_s.size() * sizeof(double));
+        gates.assign(d.gates, d.gates + d.n_gates);
+        for (const ato_gate& g : gates) {
+            if (g.interval < 0 || g.interval >= p.N) return "gate interval out of range";
+            if (g.shape != ATO_GATE_CIRCLE && g.shape != ATO_GATE_SQUARE) return "bad gate shape";
+        }
+        spheres.clear();
+        if (d.has_spheres) spheres.assign(d.spheres, d.spheres + (size_t)p.P * 3);
+        seg.assign((size_t)p.P * NSEG * 2, -1);
+        tail.clear();
+        rebind();
+
+        row_ptr.assign(1, 0);
+        col.clear();
+        lbg.clear();
+        ubg.clear();
+        std::string err;
+        const bool ok = with_model(p, [&]<class M>() { err = this->assemble<M>(d); });
+        if (!ok) return "unsupported model / frame combination";
+        if (!err.empty()) return err;
+        p.ng = (int32_t)lbg.size();
+        p.nnz = (int32_t)col.size();
+        p.n_tail = (int32_t)(tail.size() / 4);
+        rebind();
+        return "";
+    }
+
+  private:
+    // append one segment's pattern; returns its (row0, nnz0)
+    std::pair<int, int> append(const SegPat& sp) {
+        const int row0 = (int)lbg.size(), nnz0 = (int)col.size();
+        size_t off = 0;
+        for (size_t r = 0; r < sp.rowlen.size(); ++r) {
+            for (int e = 0; e < sp.rowlen[r]; ++e) col.push_back(sp.cols[off + e]);
+            off += sp.rowlen[r];
+            row_ptr.push_back((int32_t)col.size());
+            lbg.push_back(sp.lb[r]);
+            ubg.push_back(sp.ub[r]);
+        }
+        return {row0, nnz0};
+    }
+
+    template <class M>
+    std::string node_segment(int kind, int n, int k) {
+        SegPat sp;
+        PatSink s{&sp};
+        run_node_seg<M, double>(p, kind, n, k, OnesW{}, s);
+        if (!s.sorted) return "internal: unsorted columns in node segment " + std::to_string(kind);
+        auto [r0, e0] = append(sp);
+        const size_t slot = ((size_t)(n * p.K1 + k) * NSEG + kind) * 2;
+        seg[slot] = r0;
+        seg[slot + 1] = e0;
+        return "";
+    }
+
+    template <class M>
+    std::string tail_segment(int kind, int index) {
+        SegPat sp;
+        PatSink s{&sp};
+        run_tail_seg<M, double>(p, kind, index, OnesW{}, s);
+        if (!s.sorted) return "internal: unsorted columns in tail segment " + std::to_string(kind);
+        auto [r0, e0] = append(sp);
+        tail.push_back(kind);
+        tail.push_back(index);
+        tail.push_back(r0);
+        tail.push_back(e0);
+        return "";
+    }
+
+    template <class M>
+    std::string assemble(const ato_problem_desc& d) {
+        if (M::NZ != nz || M::NU != nu) return "internal: model size mismatch";
+        std::string e;
+#define ATO_TRY(x) do { e = (x); if (!e.empty()) return e; } while (0)
+        if (p.phase_len > 0) ATO_TRY(tail_segment<M>(TAIL_HEQ, 0));
+        const bool param = M::PARAM;
+        for (int n = 0; n < p.N; ++n) {
+            for (int k = 0; k < p.K1; ++k) ATO_TRY(node_segment<M>(SEG_COLLOC, n, k));
+            if (param && p.force_reg)
+                for (int k = 0; k < p.K1; ++k)
+                    if (geom[(size_t)(n * p.K1 + k) * ATO_GEOM_WIDTH + 13] != 0.0)
+                        ATO_TRY(node_segment<M>(SEG_REG, n, k));
+            if (!M::IS_DRONE)
+                for (int k = 0; k < p.K1; ++k) ATO_TRY(node_segment<M>(SEG_STAGE, n, k));
+            if (n >= 1) ATO_TRY(node_segment<M>(SEG_CONT, n, 0));
+            if (param) ATO_TRY(node_segment<M>(SEG_SROWS, n, 0));
+        }
+        if (p.closed && !M::IS_DRONE) ATO_TRY(tail_segment<M>(TAIL_CLOSURE_BASE, 0));
+        for (int g = 0; g < p.n_gates; ++g) ATO_TRY(tail_segment<M>(TAIL_GATE, g));
+        if (p.has_spheres) {
+            if (!param) return "obstacle spheres need the parametric frame";
+            for (int n = 0; n < p.N; ++n)
+                for (int k = 0; k < p.K1; ++k) ATO_TRY(node_segment<M>(SEG_SPHERE, n, k));
+        }
+        if (p.closed && M::IS_DRONE) ATO_TRY(tail_segment<M>(TAIL_DRONE_CLOSURE, 0));
+#undef ATO_TRY
+        (void)d;
+        return "";
+    }
+};
+
+}  // namespace ato

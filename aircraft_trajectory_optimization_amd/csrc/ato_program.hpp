@@ -1,0 +1,482 @@
+// ato_program.hpp -- the NLP transcription as "segment programs".
+//
+// A segment is a run of consecutive constraint rows of g(w) that one thread produces
+// (the rows of one collocation node, the continuity block of one interval, one gate, ...).
+// Each program walks its rows in the reference's order and, per row, calls
+//     sink.jac(col, value)      for every structural Jacobian entry (ascending col)
+//     sink.row(g, lbg, ubg)     to close the row
+// The same code runs
+//   * on the host with a pattern sink  -> CSR sparsity, lbg/ubg, segment offsets
+//   * on the device with a value sink  -> g and J values for one problem instance
+// so the sparsity pattern and the values cannot drift apart.
+//
+// Reference row families (drone3d/raceline/base_raceline.py):
+//   collocation ODE / s-dot / input-rate rows     :398-434
+//   regularity rows                               :1114-1130
+//   model stage constraints (point-mass ball)     :436-451, point_model.py:122-129
+//   continuity (+ quaternion normalisation)       :460-490, :1132-1181, drone_raceline.py:42-45
+//   fixed-s rows                                  :1165-1181
+//   gates                                         :545-595, :907-918, :986-1032
+//   equal-h rows (global frame)                   :891-905
+//   loop closure                                  :492-514, :1183-1227, drone_raceline.py:47-104
+//   obstacle-tube sphere rows                     obstacles/mesh_obstacle.py:219-237
+//   cost                                          :601-623
+#pragma once
+#include "ato_models.hpp"
+#include "../../include/ato.h"
+
+namespace ato {
+
+enum SegKind { SEG_COLLOC = 0, SEG_REG, SEG_STAGE, SEG_SPHERE, SEG_CONT, SEG_SROWS, NSEG };
+enum TailKind { TAIL_HEQ = 0, TAIL_CLOSURE_BASE, TAIL_INITIAL, TAIL_TERMINAL, TAIL_GATE,
+                TAIL_DRONE_CLOSURE };
+
+#ifndef ATO_INF
+#define ATO_INF (__builtin_huge_val())
+#endif
+
+// Problem constants as the kernels see them (passed by value as a kernel argument).
+struct ProbD {
+    int32_t model, att, frame, trans;
+    int32_t N, K, K1, P, NZ, NU, NV, nw, ng, nnz;
+    int32_t closed, cleanly_closed, quat_flip, force_reg, n_gates, phase_len, has_spheres, n_tail;
+    double euler_wraps, gamma;
+    Vehicle veh;
+    double Rc[16], dRc[16];
+    double tau[ATO_KMAX + 1], Bq[ATO_KMAX + 1], C[(ATO_KMAX + 1) * (ATO_KMAX + 1)], D[ATO_KMAX + 1];
+    double A_skew[4];
+    const double* geom;        // [P][ATO_GEOM_WIDTH]
+    const double* node_s;      // [P]
+    const double* interval_s;  // [N+1]
+    const ato_gate* gates;     // [n_gates]
+    const double* spheres;     // [P][3]
+    const int32_t* seg;        // [P][NSEG][2]  (row0, nnz0); -1 = absent
+    const int32_t* tail;       // [n_tail][4]   (kind, index, row0, nnz0)
+};
+
+template <class T>
+ATO_HD NodeGeom<T> load_geom(const ProbD& p, int node) {
+    NodeGeom<T> G;
+    const double* gp = p.geom + (long)node * ATO_GEOM_WIDTH;
+    for (int i = 0; i < 9; ++i) G.Rp[i] = T(gp[i]);
+    G.ks = T(gp[9]);
+    G.ky = T(gp[10]);
+    G.kn = T(gp[11]);
+    G.mag = T(gp[12]);
+    return G;
+}
+
+// column helpers: w = [h_0..h_{N-1}, (Z, U, dU) for every node (n, k)]
+template <class M>
+struct Cols {
+    static constexpr int NZ = M::NZ, NU = M::NU, NV = NZ + 2 * NU;
+    int N, K1;
+    ATO_HD int node(int n, int k) const { return N + (n * K1 + k) * NV; }
+    ATO_HD int z(int n, int k, int i) const { return node(n, k) + i; }
+    ATO_HD int u(int n, int k, int i) const { return node(n, k) + NZ + i; }
+    ATO_HD int du(int n, int k, int i) const { return node(n, k) + NZ + NU + i; }
+};
+
+// -------------------------------------------------------------------------- collocation node
+// Rows of node (n, k): [s-dot poly >= 0 (param)] [ODE defect (k > 0)] [dU defect].
+template <class M, class T, class W, class S>
+ATO_HD void seg_colloc(const ProbD& p, int n, int k, const W& w, S& s) {
+    constexpr int NZ = M::NZ, NU = M::NU;
+    const Cols<M> c{p.N, p.K1};
+    const int K1 = p.K1;
+    const T h = w(n);
+    const T ih = T(1) / h, ih2 = ih * ih;
+    T Pz[NZ], Pu[NU];
+#pragma unroll
+    for (int i = 0; i < NZ; ++i) Pz[i] = T(0);
+#pragma unroll
+    for (int i = 0; i < NU; ++i) Pu[i] = T(0);
+    for (int j = 0; j < K1; ++j) {
+        const T cj = T(p.C[j * K1 + k]);
+#pragma unroll
+        for (int i = 0; i < NZ; ++i) Pz[i] += cj * w(c.z(n, j, i));
+#pragma unroll
+        for (int i = 0; i < NU; ++i) Pu[i] += cj * w(c.u(n, j, i));
+    }
+    if (M::PARAM) {
+        // poly_ode[0] >= 0  (base_raceline.py:422-425)
+        s.jac(n, -Pz[0] * ih2);
+        for (int j = 0; j < K1; ++j) s.jac(c.z(n, j, 0), T(p.C[j * K1 + k]) * ih);
+        s.row(Pz[0] * ih, 0.0, ATO_INF);
+    }
+    if (k > 0) {
+        T z[NZ], u[NU];
+#pragma unroll
+        for (int i = 0; i < NZ; ++i) z[i] = w(c.z(n, k, i));
+#pragma unroll
+        for (int i = 0; i < NU; ++i) u[i] = w(c.u(n, k, i));
+        const NodeGeom<T> G = load_geom<T>(p, n * K1 + k);
+        const T ckk = T(p.C[k * K1 + k]) * ih;
+        // f(Z_k, U_k) - poly_ode = 0  (base_raceline.py:427-430)
+        M::rows(z, u, G, p.veh, [&](int i, T fi, const T* dz, const T* du) {
+            s.jac(n, Pz[i] * ih2);
+            for (int j = 0; j < k; ++j) s.jac(c.z(n, j, i), -T(p.C[j * K1 + k]) * ih);
+#pragma unroll
+            for (int m = 0; m < NZ; ++m)
+                if (M::zmask(i, m) || m == i) s.jac(c.z(n, k, m), m == i ? dz[m] - ckk : dz[m]);
+#pragma unroll
+            for (int m = 0; m < NU; ++m)
+                if (M::umask(i, m)) s.jac(c.u(n, k, m), du[m]);
+            for (int j = k + 1; j < K1; ++j) s.jac(c.z(n, j, i), -T(p.C[j * K1 + k]) * ih);
+            s.row(fi - Pz[i] * ih, 0.0, 0.0);
+        });
+    }
+    // dU - poly_du = 0  (base_raceline.py:432-434)
+#pragma unroll
+    for (int i = 0; i < NU; ++i) {
+        s.jac(n, Pu[i] * ih2);
+        for (int j = 0; j < K1; ++j) {
+            s.jac(c.u(n, j, i), -T(p.C[j * K1 + k]) * ih);
+            if (j == k) s.jac(c.du(n, k, i), T(1));
+        }
+        s.row(w(c.du(n, k, i)) - Pu[i] * ih, 0.0, 0.0);
+    }
+}
+
+// regularity: k_n y - k_y n <= gamma at nodes with k_y^2 + k_n^2 > 0.1 (base_raceline.py:1121-1129)
+template <class M, class T, class W, class S>
+ATO_HD void seg_reg(const ProbD& p, int n, int k, const W& w, S& s) {
+    const Cols<M> c{p.N, p.K1};
+    const double* gp = p.geom + (long)(n * p.K1 + k) * ATO_GEOM_WIDTH;
+    const T ky = T(gp[10]), kn = T(gp[11]);
+    s.jac(c.z(n, k, 1), kn);
+    s.jac(c.z(n, k, 2), -ky);
+    s.row(kn * w(c.z(n, k, 1)) - ky * w(c.z(n, k, 2)), -ATO_INF, p.gamma);
+}
+
+// point-mass thrust ball u.u / T_max^2 <= 1  (point_model.py:122-129)
+template <class M, class T, class W, class S>
+ATO_HD void seg_stage(const ProbD& p, int n, int k, const W& w, S& s) {
+    const Cols<M> c{p.N, p.K1};
+    const T it2 = T(1) / (T(p.veh.Tmax) * T(p.veh.Tmax));
+    T uu = T(0);
+#pragma unroll
+    for (int i = 0; i < M::NU; ++i) {
+        const T ui = w(c.u(n, k, i));
+        uu += ui * ui;
+        s.jac(c.u(n, k, i), T(2) * ui * it2);
+    }
+    s.row(uu / T(p.veh.Tmax) / T(p.veh.Tmax), -ATO_INF, 1.0);
+}
+
+// obstacle tube: (y - dy)^2 + (n - dn)^2 <= r_avail^2  (mesh_obstacle.py:219-237)
+template <class M, class T, class W, class S>
+ATO_HD void seg_sphere(const ProbD& p, int n, int k, const W& w, S& s) {
+    const Cols<M> c{p.N, p.K1};
+    const double* sp = p.spheres + (long)(n * p.K1 + k) * 3;
+    const T ey = w(c.z(n, k, 1)) - T(sp[0]);
+    const T en = w(c.z(n, k, 2)) - T(sp[1]);
+    s.jac(c.z(n, k, 1), T(2) * ey);
+    s.jac(c.z(n, k, 2), T(2) * en);
+    s.row(ey * ey + en * en, -ATO_INF, sp[2] * sp[2]);
+}
+
+// quaternion normalisation op(q) = q / |q| and its Jacobian (drone_raceline.py:42-45)
+template <class T>
+ATO_HD void qnormalize(const T* q, T* qh, T& inv_norm) {
+    const T nq = tsqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+    inv_norm = T(1) / nq;
+    for (int i = 0; i < 4; ++i) qh[i] = q[i] / nq;
+}
+
+// continuity into interval n >= 1 (base_raceline.py:474-490, parametric :1149-1163)
+template <class M, class T, class W, class S>
+ATO_HD void seg_cont(const ProbD& p, int n, const W& w, S& s) {
+    constexpr int NZ = M::NZ, NU = M::NU, IR = M::IR;
+    const Cols<M> c{p.N, p.K1};
+    const int K1 = p.K1;
+    T zb[NZ], ub[NU];
+#pragma unroll
+    for (int i = 0; i < NZ; ++i) zb[i] = T(0);
+#pragma unroll
+    for (int i = 0; i < NU; ++i) ub[i] = T(0);
+    for (int k = 0; k < K1; ++k) {
+        const T dk = T(p.D[k]);
+#pragma unroll
+        for (int i = 0; i < NZ; ++i) zb[i] += w(c.z(n - 1, k, i)) * dk;
+#pragma unroll
+        for (int i = 0; i < NU; ++i) ub[i] += w(c.u(n - 1, k, i)) * dk;
+    }
+    T qh[4] = {T(0), T(0), T(0), T(0)}, iq = T(0);
+    if (M::HAS_QUAT) qnormalize(zb + IR, qh, iq);
+#pragma unroll
+    for (int i = (M::PARAM ? 1 : 0); i < NZ; ++i) {
+        const bool isq = M::HAS_QUAT && i >= IR && i < IR + 4;
+        if (isq) {
+            const int a = i - IR;
+            for (int k = 0; k < K1; ++k) {
+                const T dk = T(p.D[k]);
+#pragma unroll
+                for (int m = 0; m < 4; ++m)
+                    s.jac(c.z(n - 1, k, IR + m), -dk * ((a == m ? T(1) : T(0)) - qh[a] * qh[m]) * iq);
+            }
+            s.jac(c.z(n, 0, i), T(1));
+            s.row(w(c.z(n, 0, i)) - qh[a], 0.0, 0.0);
+        } else {
+            for (int k = 0; k < K1; ++k) s.jac(c.z(n - 1, k, i), -T(p.D[k]));
+            s.jac(c.z(n, 0, i), T(1));
+            s.row(w(c.z(n, 0, i)) - zb[i], 0.0, 0.0);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < NU; ++i) {
+        for (int k = 0; k < K1; ++k) s.jac(c.u(n - 1, k, i), -T(p.D[k]));
+        s.jac(c.u(n, 0, i), T(1));
+        s.row(w(c.u(n, 0, i)) - ub[i], 0.0, 0.0);
+    }
+}
+
+// fixed path length at both ends of interval n (base_raceline.py:1165-1181)
+template <class M, class T, class W, class S>
+ATO_HD void seg_srows(const ProbD& p, int n, const W& w, S& s) {
+    const Cols<M> c{p.N, p.K1};
+    s.jac(c.z(n, 0, 0), T(1));
+    s.row(w(c.z(n, 0, 0)) - T(p.interval_s[n]), 0.0, 0.0);
+    T zN = T(0);
+    for (int k = 0; k < p.K1; ++k) {
+        zN += w(c.z(n, k, 0)) * T(p.D[k]);
+        s.jac(c.z(n, k, 0), T(p.D[k]));
+    }
+    s.row(zN - T(p.interval_s[n + 1]), 0.0, 0.0);
+}
+
+// -------------------------------------------------------------------------- tail segments
+// equal step sizes within each gate phase (base_raceline.py:891-905)
+template <class M, class T, class W, class S>
+ATO_HD void seg_heq(const ProbD& p, const W& w, S& s) {
+    for (int n = 0; n < p.N; n += p.phase_len) {
+        for (int n2 = n + 1; n2 < n + p.phase_len; ++n2) {
+            s.jac(n, T(-1));
+            s.jac(n2, T(1));
+            s.row(w(n2) - w(n), 0.0, 0.0);
+        }
+    }
+}
+
+// gate rows (base_raceline.py:545-595). Gate state x = xoff + E zc, zc = sum_k coef_k Z[n,k][comp]
+//   parametric: comps (y, n), E = [e_y e_n], xoff = x_c(s)   (:1028-1030)
+//   global:     comps (x1, x2, x3), E = I, xoff = 0          (:912)
+template <class M, class T, class W, class S>
+ATO_HD void seg_gate(const ProbD& p, int gi, const W& w, S& s) {
+    const ato_gate& gt = p.gates[gi];
+    const Cols<M> c{p.N, p.K1};
+    const int n = gt.interval;
+    const int nk = gt.single_node ? 1 : p.K1;
+    const int nc = M::PARAM ? 2 : 3;
+    const int comp0 = M::PARAM ? 1 : 0;
+    T E[3][3];
+    for (int a = 0; a < 3; ++a) {
+        if (M::PARAM) {
+            E[a][0] = T(gt.ey[a]);
+            E[a][1] = T(gt.en[a]);
+            E[a][2] = T(0);
+        } else {
+            for (int b = 0; b < 3; ++b) E[a][b] = T(a == b ? 1 : 0);
+        }
+    }
+    T zc[3] = {T(0), T(0), T(0)};
+    for (int k = 0; k < nk; ++k) {
+        const T ck = gt.single_node ? T(1) : T(gt.coef[k]);
+        for (int q = 0; q < nc; ++q) zc[q] += w(c.z(n, k, comp0 + q)) * ck;
+    }
+    T x[3], dx[3];
+    for (int a = 0; a < 3; ++a) {
+        x[a] = M::PARAM ? T(gt.xc[a]) : T(0);
+        for (int q = 0; q < nc; ++q) x[a] += zc[q] * E[a][q];
+        dx[a] = x[a] - T(gt.gate_x[a]);
+    }
+    // emit one row whose value is linear or quadratic in zc:  dval/dzc given
+    auto emit_row = [&](const T* dzc, T val, double lb, double ub) {
+        for (int k = 0; k < nk; ++k) {
+            const T ck = gt.single_node ? T(1) : T(gt.coef[k]);
+            for (int q = 0; q < nc; ++q) s.jac(c.z(n, k, comp0 + q), ck * dzc[q]);
+        }
+        s.row(val, lb, ub);
+    };
+    const double dmax = gt.d_max;
+    if (gt.fix_center) {
+        for (int a = 0; a < 3; ++a) {
+            T d[3];
+            for (int q = 0; q < 3; ++q) d[q] = E[a][q];
+            emit_row(d, dx[a], 0.0, 0.0);
+        }
+        return;
+    }
+    // gate axes e1, e2, e3 = columns of R
+    T e[3][3];
+    for (int a = 0; a < 3; ++a)
+        for (int b = 0; b < 3; ++b) e[b][a] = T(gt.R[a * 3 + b]);
+    if (gt.shape == ATO_GATE_CIRCLE) {
+        const T p2 = dx[0] * e[1][0] + dx[1] * e[1][1] + dx[2] * e[1][2];
+        const T p3 = dx[0] * e[2][0] + dx[1] * e[2][1] + dx[2] * e[2][2];
+        T d[3];
+        for (int q = 0; q < 3; ++q) {
+            const T E2 = E[0][q] * e[1][0] + E[1][q] * e[1][1] + E[2][q] * e[1][2];
+            const T E3 = E[0][q] * e[2][0] + E[1][q] * e[2][1] + E[2][q] * e[2][2];
+            d[q] = T(2) * p2 * E2 + T(2) * p3 * E3;
+        }
+        emit_row(d, p2 * p2 + p3 * p3, -ATO_INF, dmax * dmax);
+        if (gt.axial) {
+            T d1[3];
+            for (int q = 0; q < 3; ++q) d1[q] = E[0][q] * e[0][0] + E[1][q] * e[0][1] + E[2][q] * e[0][2];
+            const T xe = x[0] * e[0][0] + x[1] * e[0][1] + x[2] * e[0][2];
+            const T ge = T(gt.gate_x[0]) * e[0][0] + T(gt.gate_x[1]) * e[0][1] + T(gt.gate_x[2]) * e[0][2];
+            emit_row(d1, xe - ge, 0.0, 0.0);
+        }
+    } else {
+        // delta = R^T (x - gate_x); rows 1,2 (+ row 0 when axial)
+        for (int i = gt.axial ? 0 : 1; i < 3; ++i) {
+            T d[3];
+            for (int q = 0; q < 3; ++q) d[q] = E[0][q] * e[i][0] + E[1][q] * e[i][1] + E[2][q] * e[i][2];
+            const T del = dx[0] * e[i][0] + dx[1] * e[i][1] + dx[2] * e[i][2];
+            if (i == 0) emit_row(d, del, 0.0, 0.0);
+            else emit_row(d, del, -dmax, dmax);
+        }
+    }
+}
+
+// end-of-horizon quantities for collocation: zF = op(sum_k D_k Z[N-1,k]), uF = sum_k D_k U[N-1,k]
+// (base_raceline.py:322-348)
+
+// drone loop closure (drone_raceline.py:47-104), appended after gates
+template <class M, class T, class W, class S>
+ATO_HD void seg_drone_closure(const ProbD& p, const W& w, S& s) {
+    constexpr int NZ = M::NZ, NU = M::NU, IR = M::IR, NR = M::NR;
+    const Cols<M> c{p.N, p.K1};
+    const int K1 = p.K1, nl = p.N - 1;
+    T zb[NZ], ub[NU];
+#pragma unroll
+    for (int i = 0; i < NZ; ++i) zb[i] = T(0);
+#pragma unroll
+    for (int i = 0; i < NU; ++i) ub[i] = T(0);
+    for (int k = 0; k < K1; ++k) {
+        const T dk = T(p.D[k]);
+#pragma unroll
+        for (int i = 0; i < NZ; ++i) zb[i] += w(c.z(nl, k, i)) * dk;
+#pragma unroll
+        for (int i = 0; i < NU; ++i) ub[i] += w(c.u(nl, k, i)) * dk;
+    }
+    T qh[4] = {T(0), T(0), T(0), T(0)}, iq = T(0);
+    if (M::HAS_QUAT) qnormalize(zb + IR, qh, iq);
+    // uF - u0
+#pragma unroll
+    for (int i = 0; i < NU; ++i) {
+        s.jac(c.u(0, 0, i), T(-1));
+        for (int k = 0; k < K1; ++k) s.jac(c.u(nl, k, i), T(p.D[k]));
+        s.row(ub[i] - w(c.u(0, 0, i)), 0.0, 0.0);
+    }
+    auto plain = [&](int i, T offset) {
+        s.jac(c.z(0, 0, i), T(-1));
+        for (int k = 0; k < K1; ++k) s.jac(c.z(nl, k, i), T(p.D[k]));
+        s.row(zb[i] - w(c.z(0, 0, i)) - offset, 0.0, 0.0);
+    };
+    plain(1, T(0));
+    plain(2, T(0));
+    // z_delta[7:] (ESP) or z_delta[4:] (YPR): everything after the first attitude slot(s)
+    const int first_after = M::HAS_QUAT ? IR + 4 : IR + 1;
+    for (int i = first_after; i < NZ; ++i) plain(i, T(0));
+    if (M::HAS_QUAT) {
+        const T sgn = p.quat_flip ? T(1) : T(-1);
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+            s.jac(c.z(0, 0, IR + a), sgn);
+            for (int k = 0; k < K1; ++k) {
+                const T dk = T(p.D[k]);
+#pragma unroll
+                for (int m = 0; m < 4; ++m)
+                    s.jac(c.z(nl, k, IR + m), dk * ((a == m ? T(1) : T(0)) - qh[a] * qh[m]) * iq);
+            }
+            s.row(qh[a] + sgn * w(c.z(0, 0, IR + a)), 0.0, 0.0);
+        }
+    } else {
+        const double two_pi = 6.283185307179586;
+        plain(IR, T(two_pi * p.euler_wraps));
+    }
+    (void)NR;
+    if (!M::PARAM) plain(0, T(0));
+}
+
+// base loop closure used by the point-mass racelines (base_raceline.py:492-514, :1183-1227)
+template <class M, class T, class W, class S>
+ATO_HD void seg_closure_base(const ProbD& p, const W& w, S& s) {
+    constexpr int NZ = M::NZ, NU = M::NU;
+    const Cols<M> c{p.N, p.K1};
+    const int K1 = p.K1, nl = p.N - 1;
+    T zb[NZ], ub[NU];
+#pragma unroll
+    for (int i = 0; i < NZ; ++i) zb[i] = T(0);
+#pragma unroll
+    for (int i = 0; i < NU; ++i) ub[i] = T(0);
+    for (int k = 0; k < K1; ++k) {
+        const T dk = T(p.D[k]);
+#pragma unroll
+        for (int i = 0; i < NZ; ++i) zb[i] += w(c.z(nl, k, i)) * dk;
+#pragma unroll
+        for (int i = 0; i < NU; ++i) ub[i] += w(c.u(nl, k, i)) * dk;
+    }
+#pragma unroll
+    for (int i = 0; i < NU; ++i) {
+        s.jac(c.u(0, 0, i), T(-1));
+        for (int k = 0; k < K1; ++k) s.jac(c.u(nl, k, i), T(p.D[k]));
+        s.row(ub[i] - w(c.u(0, 0, i)), 0.0, 0.0);
+    }
+    if (!M::PARAM || p.cleanly_closed) {
+        for (int i = M::PARAM ? 1 : 0; i < NZ; ++i) {
+            s.jac(c.z(0, 0, i), T(-1));
+            for (int k = 0; k < K1; ++k) s.jac(c.z(nl, k, i), T(p.D[k]));
+            s.row(zb[i] - w(c.z(0, 0, i)), 0.0, 0.0);
+        }
+    } else {
+        // A z0[1:3] - zF[1:3] ; z0[3:] - zF[3:]
+        for (int r = 0; r < 2; ++r) {
+            s.jac(c.z(0, 0, 1), T(p.A_skew[r * 2 + 0]));
+            s.jac(c.z(0, 0, 2), T(p.A_skew[r * 2 + 1]));
+            for (int k = 0; k < K1; ++k) s.jac(c.z(nl, k, 1 + r), -T(p.D[k]));
+            s.row(T(p.A_skew[r * 2]) * w(c.z(0, 0, 1)) + T(p.A_skew[r * 2 + 1]) * w(c.z(0, 0, 2)) - zb[1 + r],
+                  0.0, 0.0);
+        }
+        for (int i = 3; i < NZ; ++i) {
+            s.jac(c.z(0, 0, i), T(1));
+            for (int k = 0; k < K1; ++k) s.jac(c.z(nl, k, i), -T(p.D[k]));
+            s.row(w(c.z(0, 0, i)) - zb[i], 0.0, 0.0);
+        }
+    }
+}
+
+// -------------------------------------------------------------------------- cost
+// J = sum_{n,k} h_n B_k (u'Ru + du'dR du + 1)   (base_raceline.py:601-623)
+// stage cost at node (n, k) and its input / input-rate gradient (without the h_n B_k factor)
+template <class M, class T, class W>
+ATO_HD T stage_cost(const ProbD& p, int n, int k, const W& w, T* gu, T* gdu) {
+    constexpr int NU = M::NU;
+    const Cols<M> c{p.N, p.K1};
+    T u[NU], du[NU];
+#pragma unroll
+    for (int i = 0; i < NU; ++i) {
+        u[i] = w(c.u(n, k, i));
+        du[i] = w(c.du(n, k, i));
+    }
+    T L = T(1);
+#pragma unroll
+    for (int i = 0; i < NU; ++i) {
+        T ru = T(0), rdu = T(0), gui = T(0), gdui = T(0);
+#pragma unroll
+        for (int j = 0; j < NU; ++j) {
+            ru += T(p.Rc[i * NU + j]) * u[j];
+            rdu += T(p.dRc[i * NU + j]) * du[j];
+            gui += (T(p.Rc[i * NU + j]) + T(p.Rc[j * NU + i])) * u[j];
+            gdui += (T(p.dRc[i * NU + j]) + T(p.dRc[j * NU + i])) * du[j];
+        }
+        L += u[i] * ru + du[i] * rdu;
+        if (gu) gu[i] = gui;
+        if (gdu) gdu[i] = gdui;
+    }
+    return L;
+}
+
+}  // namespace ato

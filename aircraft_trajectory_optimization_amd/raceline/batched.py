@@ -1,0 +1,78 @@
+'''
+Batched evaluation of a raceline NLP on one HIP device.
+
+B independent instances share one ProblemSpec (same track, N, K, model). Decision
+vectors, constraints, Jacobian values and gradients live in HBM as torch tensors in the
+library's INTERLEAVED layout ([element][instance]); evaluation is a single libato call
+(ato_eval) on the current torch stream. This is the drop-in for the reference's per-
+iterate nlp_g / nlp_jac_g / nlp_f / nlp_grad_f calls (base_raceline.py:165, via IPOPT).
+'''
+from typing import Optional, Tuple
+
+import numpy as np
+import torch
+
+from aircraft_trajectory_optimization_amd import native
+from aircraft_trajectory_optimization_amd.raceline.problem import ProblemSpec
+
+
+class BatchedNLP:
+    ''' device-resident batch of NLP instances '''
+
+    def __init__(self, spec: ProblemSpec, batch: int, dtype: torch.dtype = torch.float64,
+                 layout: int = native.ATO_LAYOUT_INTERLEAVED, device: Optional[torch.device] = None):
+        if not torch.cuda.is_available():
+            raise RuntimeError('BatchedNLP needs a HIP device (torch.cuda.is_available() is False)')
+        self.device = device or torch.device('cuda', torch.cuda.current_device())
+        with torch.cuda.device(self.device):
+            self.problem = native.NativeProblem(spec.native_spec())
+        self.spec = spec
+        self.batch = int(batch)
+        self.dtype = dtype
+        self.layout = layout
+        self.fp32 = dtype == torch.float32
+        nw, ng, nnz, B = self.problem.nw, self.problem.ng, self.problem.nnz, self.batch
+        shape = (lambda n: (n, B)) if layout == native.ATO_LAYOUT_INTERLEAVED else (lambda n: (B, n))
+        opts = {'device': self.device, 'dtype': dtype}
+        self.w = torch.zeros(shape(nw), **opts)
+        self.g = torch.zeros(shape(ng), **opts)
+        self.jac = torch.zeros(shape(nnz), **opts)
+        self.grad_f = torch.zeros(shape(nw), **opts)
+        self.f = torch.zeros(B, **opts)
+        self.problem.reserve(B)
+        self.row_ptr, self.col = self.problem.sparsity()
+        self.lbg, self.ubg = self.problem.bounds()
+
+    @property
+    def sizes(self) -> Tuple[int, int, int]:
+        ''' nw, ng, nnz '''
+        return self.problem.nw, self.problem.ng, self.problem.nnz
+
+    def set_w(self, W: np.ndarray):
+        ''' W: (B, nw) host array of decision vectors '''
+        W = np.asarray(W, dtype=np.float64).reshape(self.batch, -1)
+        t = torch.as_tensor(W, dtype=self.dtype)
+        if self.layout == native.ATO_LAYOUT_INTERLEAVED:
+            t = t.T.contiguous()
+        self.w.copy_(t.to(self.device))
+
+    def evaluate(self, g: bool = True, jac: bool = True, cost: bool = True, stream=None):
+        ''' launch the evaluation (asynchronous on `stream`, default the current torch stream) '''
+        st = stream if stream is not None else torch.cuda.current_stream(self.device)
+        self.problem.eval_ptrs(
+            self.batch, self.w.data_ptr(),
+            g=self.g.data_ptr() if g else 0,
+            jac=self.jac.data_ptr() if jac else 0,
+            f=self.f.data_ptr() if cost else 0,
+            grad_f=self.grad_f.data_ptr() if cost else 0,
+            layout=self.layout, stream=st.cuda_stream, fp32=self.fp32)
+
+    def _host(self, t: torch.Tensor) -> np.ndarray:
+        a = t.detach().to('cpu', torch.float64).numpy()
+        return a.T.copy() if self.layout == native.ATO_LAYOUT_INTERLEAVED else a
+
+    def results(self):
+        ''' (g (B, ng), jac values (B, nnz), f (B,), grad_f (B, nw)) on the host '''
+        torch.cuda.synchronize(self.device)
+        return self._host(self.g), self._host(self.jac), self.f.detach().cpu().double().numpy(), \
+            self._host(self.grad_f)

@@ -1,0 +1,43 @@
+'''
+Seeded batches of problem instances (build-defined; the reference has no RNG).
+
+SURVEY.md 8(d) config 3: instance b uses numpy.random.default_rng(b):
+    v0 ~ U[0.5, 2.0], h0 ~ U[0.5, 1.5], lateral guesses y, n ~ N(0, 0.3^2) clipped to +-1.5,
+    every other entry of w0 as the reference's cold start (A18).
+The cold-start guess is linear in v0 and h0, so instances are derived from one ProblemSpec
+built with v0 = h0 = 1.
+'''
+from typing import Iterable, Tuple
+
+import numpy as np
+
+from aircraft_trajectory_optimization_amd.raceline.problem import ProblemSpec
+
+
+def seeded_instances(spec: ProblemSpec, seeds: Iterable[int]) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+    ''' (W, LBW, UBW), each (B, nw) '''
+    if spec.config.v0 != 1 or spec.config.h0 != 1:
+        raise ValueError('build the base spec with v0 = h0 = 1')
+    seeds = list(seeds)
+    B = len(seeds)
+    nw, N, P, nv = spec.nw, spec.N, spec.P, spec.nv
+    node = N + np.arange(P) * nv
+    # velocity slots of the guess (scaled by v0): drone z[IV:IV+3], point z[3:6]
+    iv = (7 if spec.nz == 13 else 6) if spec.is_drone else 3
+    W = np.repeat(spec.w0[None], B, axis=0)
+    LBW = np.repeat(spec.lbw[None], B, axis=0)
+    UBW = np.repeat(spec.ubw[None], B, axis=0)
+    for row, b in enumerate(seeds):
+        rng = np.random.default_rng(b)
+        v0 = rng.uniform(0.5, 2.0)
+        h0 = rng.uniform(0.5, 1.5)
+        yn = np.clip(rng.normal(0.0, 0.3, size=(P, 2)), -1.5, 1.5)
+        W[row, :N] = h0
+        LBW[row, :N] = h0 / 100
+        UBW[row, :N] = h0 * 10
+        for c in range(3):
+            W[row, node + iv + c] *= v0
+        if spec.param:
+            W[row, node + 1] = yn[:, 0]
+            W[row, node + 2] = yn[:, 1]
+    return W, LBW, UBW

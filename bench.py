@@ -1,0 +1,172 @@
+#!/usr/bin/env python
+'''
+Benchmark of the hot path: batched evaluation of the collocation NLP's g(w), dg/dw (all
+structural entries), f(w) and grad f(w) -- what IPOPT asks CasADi for on every iterate of
+the reference (base_raceline.py:165, :182-189).
+
+Workload (BASELINE.json configs[2]): racetrack of scripts/race.py, parametric frame,
+quaternion drone (13 states, 4 inputs), global attitude, square gates, closed loop,
+N = 50 intervals, K = 4 Legendre collocation, fp64, B = 512 seeded instances per GPU
+(SURVEY 8(d) config 3 generator). One step = one ato_eval over the whole batch, inputs
+resident in HBM. Multi-GPU: one process per GPU, instances sharded (weak scaling), no
+collective inside the timed region; per-instance summaries are all-gathered over RCCL
+afterwards.
+
+    python bench.py [--gpus N --steps K --warmup W --batch B]
+'''
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = 'SQP iters/sec (batched) + lap-time err vs CasADi, 50×4 collocation'
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=50)
+    ap.add_argument('--warmup', type=int, default=10)
+    ap.add_argument('--batch', type=int, default=512, help='instances per GPU')
+    ap.add_argument('--dtype', choices=['f64', 'f32'], default='f64')
+    ap.add_argument('--layout', choices=['interleaved', 'instance'], default='interleaved')
+    ap.add_argument('--cpu-seconds', type=float, default=15.0, help='budget of the oracle CPU baseline')
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--traffic-json', default=os.path.join(ROOT, 'profiles', 'traffic_latest.json'))
+    return ap.parse_args()
+
+
+def cpu_baseline(spec_kwargs, W, budget_s):
+    ''' the numpy oracle (tests-only code) timed on a bounded sample of the same workload '''
+    from tests.helpers import oracle_nlp
+    nlp = oracle_nlp(**spec_kwargs)
+    t0 = time.perf_counter()
+    n = 0
+    while n < W.shape[0]:
+        w = W[n]
+        nlp.g(w)
+        nlp.jac_dense(w)
+        nlp.f(w)
+        nlp.grad_f(w)
+        n += 1
+        if time.perf_counter() - t0 > budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return {'value': n / dt, 'unit': 'evals/s', 'cores': 1, 'kind': 'port',
+            'sample': f'{n} instances of the same 50x4x13 racetrack workload: oracle g + complex-step '
+                      f'dense J + f + grad f, numpy fp64, single thread, {dt:.1f} s'}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    from aircraft_trajectory_optimization_amd import native
+    from aircraft_trajectory_optimization_amd.raceline.batched import BatchedNLP
+    from aircraft_trajectory_optimization_amd.raceline.instances import seeded_instances
+    from aircraft_trajectory_optimization_amd.tracks import make_spec
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        dist.init_process_group('nccl')
+    torch.cuda.set_device(local)
+    dev = torch.device('cuda', local)
+
+    spec_kwargs = dict(track='race', model='drone', frame='parametric', N=50, K=4, use_quat=True, global_r=True)
+    spec = make_spec(**spec_kwargs)
+    B = args.batch
+    W, _, _ = seeded_instances(spec, range(rank * B, (rank + 1) * B))
+    dtype = torch.float64 if args.dtype == 'f64' else torch.float32
+    layout = native.ATO_LAYOUT_INTERLEAVED if args.layout == 'interleaved' else native.ATO_LAYOUT_INSTANCE_MAJOR
+    bn = BatchedNLP(spec, B, dtype=dtype, layout=layout, device=dev)
+    bn.set_w(W)
+    nw, ng, nnz = bn.sizes
+
+    for _ in range(args.warmup):
+        bn.evaluate()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    bn.problem.timing_start(args.steps)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        bn.evaluate()
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    elapsed = float(elapsed.item())
+    k_ms, r_ms, calls = bn.problem.timing_read()
+    bn.problem.timing_start(0)
+
+    # per-instance summary {lap-time guess sum(h), cost f, max equality residual}, all-gathered (RCCL)
+    g, _, f, _ = bn.results()
+    eq = bn.lbg == bn.ubg
+    summary = np.stack([W[:, :spec.N].sum(axis=1), f, np.abs(g[:, eq]).max(axis=1)], axis=1)
+    summ_t = torch.as_tensor(summary, device=dev)
+    if world > 1:
+        gathered = torch.empty((world * B, 3), dtype=summ_t.dtype, device=dev)
+        dist.all_gather_into_tensor(gathered, summ_t)
+    else:
+        gathered = summ_t
+    assert bool(torch.isfinite(gathered).all()), 'non-finite evaluation results'
+
+    if rank == 0:
+        elem = 8 if args.dtype == 'f64' else 4
+        bytes_per_eval = elem * (nw + ng + nnz + nw + 1)   # read w; write g, J, grad f, f
+        kernel_s = (k_ms / max(calls, 1)) / 1e3
+        achieved = B * bytes_per_eval / kernel_s / 1e9
+        traffic = None
+        if os.path.exists(args.traffic_json):
+            try:
+                tj = json.load(open(args.traffic_json, encoding='utf-8'))
+                if tj.get('batch') == B and tj.get('dtype') == args.dtype and tj.get('layout') == args.layout:
+                    traffic = tj.get('hbm_bytes_per_launch')
+            except (OSError, ValueError):
+                traffic = None
+        value = world * B * args.steps / elapsed
+        out = {
+            'metric': METRIC,
+            'value': value,
+            'unit': 'constraint+Jacobian evals/s (g, dg/dw, f, grad f per instance)',
+            'n_gpus': world,
+            'steps': args.steps,
+            'warmup': args.warmup,
+            'ms_per_step': elapsed / args.steps * 1e3,
+            'higher_is_better': True,
+            'scaling': 'weak',
+            'vs_baseline': None,
+            'dtype': args.dtype,
+            'data': 'synthetic: seeded cold-start instances (SURVEY 8(d) config 3 generator)',
+            'config': {'workload': 'racetrack_parametric_esp_drone_colloc_N50_K4', 'N': 50, 'K': 4, 'nz': 13,
+                       'nu': 4, 'batch_per_gpu': B, 'global_batch': world * B, 'layout': args.layout,
+                       'nw': nw, 'ng': ng, 'nnz': nnz, 'parallelism': f'instances sharded x{world}'},
+            'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                         'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
+                         'kernel': 'k_eval', 'kernel_avg_us': kernel_s * 1e6,
+                         'reduce_avg_us': r_ms / max(calls, 1) * 1e3,
+                         'algorithmic_bytes_per_launch': B * bytes_per_eval},
+            'cpu_baseline': None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out['cpu_baseline'] = cpu_baseline(spec_kwargs, W, args.cpu_seconds)
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -1,0 +1,112 @@
+'''
+Shared test fixtures: tracks, product / oracle problem construction, host-check loader.
+'''
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+from aircraft_trajectory_optimization_amd import native
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+from aircraft_trajectory_optimization_amd.tracks import TRACKS, make_line as product_line, \
+    make_spec as product_spec  # noqa: F401
+
+
+def oracle_line(track):
+    from oracle.ref_geometry import RefCenterline
+    x, shape = TRACKS[track]
+    return RefCenterline(np.array(x, float), True, gate_shape=shape)
+
+
+def oracle_nlp(track='race', model='drone', frame='parametric', N=50, K=4, use_quat=True, global_r=True,
+               fix_gate_center=False, quat_flip=False, spheres=None, v0=1.0, h0=1):
+    from oracle.ref_transcription import RefNLP
+    line = oracle_line(track)
+    veh = {'use_quat': use_quat, 'global_r': global_r} if model == 'drone' else {'global_r': global_r}
+    fixed = line.s[:-1] if frame == 'parametric' else None
+    return RefNLP(line, model, frame, N, K, veh=veh, fix_gate_center=fix_gate_center, fixed_gates=fixed,
+                  quat_flip=quat_flip, spheres=spheres, v0=v0, h0=h0)
+
+
+def random_w(spec_or_nlp, rng, scale=0.05):
+    ''' a seeded point near w0, strictly inside the box, with unit-ish quaternions '''
+    w0 = np.array(spec_or_nlp.w0, float)
+    w = w0 + scale * rng.standard_normal(w0.shape)
+    N = spec_or_nlp.N
+    w[:N] = np.abs(w0[:N]) * (1 + 0.2 * rng.random(N))
+    return w
+
+
+def csr_dense(row_ptr, col, vals, ng, nw):
+    J = np.zeros((ng, nw))
+    for r in range(ng):
+        J[r, col[row_ptr[r]:row_ptr[r + 1]]] = vals[row_ptr[r]:row_ptr[r + 1]]
+    return J
+
+
+# ------------------------------------------------------------------ test-only CPU build of the programs
+HOSTCHECK_SRC = os.path.join(REPO, 'tests', 'native', 'hostcheck.cpp')
+HOSTCHECK_LIB = os.path.join(REPO, 'tests', 'native', 'libato_hostcheck.so')
+
+
+def build_hostcheck(force=False):
+    srcs = [HOSTCHECK_SRC] + [os.path.join(REPO, 'aircraft_trajectory_optimization_amd', 'csrc', f)
+                              for f in ('ato_models.hpp', 'ato_program.hpp', 'ato_layout.hpp')]
+    if not force and os.path.exists(HOSTCHECK_LIB) and \
+            os.path.getmtime(HOSTCHECK_LIB) >= max(os.path.getmtime(s) for s in srcs):
+        return HOSTCHECK_LIB
+    subprocess.check_call(['g++', '-std=c++20', '-O2', '-fPIC', '-shared', '-o', HOSTCHECK_LIB, HOSTCHECK_SRC])
+    return HOSTCHECK_LIB
+
+
+class HostCheck:
+    ''' the segment programs compiled for the CPU (test harness only) '''
+
+    def __init__(self, spec_dict):
+        lib = ctypes.CDLL(build_hostcheck())
+        vp = ctypes.c_void_p
+        lib.atoh_create.argtypes = [ctypes.POINTER(native.AtoProblemDesc), ctypes.POINTER(vp)]
+        lib.atoh_last_error.restype = ctypes.c_char_p
+        lib.atoh_eval.argtypes = [vp, ctypes.c_int, vp, vp, vp, vp, vp]
+        lib.atoh_destroy.argtypes = [vp]
+        lib.atoh_sizes.argtypes = [vp] + [ctypes.POINTER(ctypes.c_int32)] * 3
+        lib.atoh_sparsity.argtypes = [vp, vp, vp]
+        lib.atoh_bounds.argtypes = [vp, vp, vp]
+        self.lib = lib
+        self.holder = native.DescHolder(spec_dict)
+        h = vp()
+        if lib.atoh_create(ctypes.byref(self.holder.desc), ctypes.byref(h)) != 0:
+            raise RuntimeError(lib.atoh_last_error().decode())
+        self.h = h
+        a, b, c = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        lib.atoh_sizes(h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
+        self.nw, self.ng, self.nnz = a.value, b.value, c.value
+        self.row_ptr = np.zeros(self.ng + 1, np.int32)
+        self.col = np.zeros(self.nnz, np.int32)
+        lib.atoh_sparsity(h, self.row_ptr.ctypes.data, self.col.ctypes.data)
+        self.lbg = np.zeros(self.ng)
+        self.ubg = np.zeros(self.ng)
+        lib.atoh_bounds(h, self.lbg.ctypes.data, self.ubg.ctypes.data)
+
+    def eval(self, W):
+        ''' W: (B, nw) -> g (B, ng), J (B, nnz), f (B,), grad_f (B, nw) '''
+        W = np.ascontiguousarray(np.atleast_2d(W), dtype=np.float64)
+        B = W.shape[0]
+        g = np.zeros((B, self.ng))
+        J = np.zeros((B, self.nnz))
+        f = np.zeros(B)
+        gf = np.zeros((B, self.nw))
+        rc = self.lib.atoh_eval(self.h, B, W.ctypes.data, g.ctypes.data, J.ctypes.data, f.ctypes.data,
+                                gf.ctypes.data)
+        if rc != 0:
+            raise RuntimeError(self.lib.atoh_last_error().decode())
+        return g, J, f, gf
+
+    def __del__(self):
+        try:
+            self.lib.atoh_destroy(self.h)
+        except Exception:  # pylint: disable=broad-except
+            pass
