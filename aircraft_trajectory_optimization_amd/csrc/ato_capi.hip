@@ -16,7 +16,8 @@ struct ato_handle {
     ato_gate* d_gates = nullptr;
     int32_t* d_seg = nullptr;
     int32_t* d_tail = nullptr;
-    void* d_fpart = nullptr;    // [N][reserved] doubles (reused for float)
+    int32_t* d_units = nullptr;
+    void* d_fpart = nullptr;    // [N][reserved] cost partials (double; reused for float)
     int32_t reserved = 0;
     std::vector<hipEvent_t> events;   // 3 per timed call
     int32_t timed_calls = 0;
@@ -53,6 +54,7 @@ static void release(ato_handle* h) {
     (void)hipFree(h->d_gates);
     (void)hipFree(h->d_seg);
     (void)hipFree(h->d_tail);
+    (void)hipFree(h->d_units);
     (void)hipFree(h->d_fpart);
     for (hipEvent_t e : h->events) (void)hipEventDestroy(e);
     h->events.clear();
@@ -82,7 +84,7 @@ int ato_create(const ato_problem_desc* desc, ato_handle** out) {
     if ((rc = upload(h->L.geom, &h->d_geom)) || (rc = upload(h->L.node_s, &h->d_node_s)) ||
         (rc = upload(h->L.interval_s, &h->d_interval_s)) || (rc = upload(h->L.spheres, &h->d_spheres)) ||
         (rc = upload(h->L.gates, &h->d_gates)) || (rc = upload(h->L.seg, &h->d_seg)) ||
-        (rc = upload(h->L.tail, &h->d_tail))) {
+        (rc = upload(h->L.tail, &h->d_tail)) || (rc = upload(h->L.units, &h->d_units))) {
         release(h);
         delete h;
         return rc;
@@ -95,6 +97,7 @@ int ato_create(const ato_problem_desc* desc, ato_handle** out) {
     h->pd.gates = h->d_gates;
     h->pd.seg = h->d_seg;
     h->pd.tail = h->d_tail;
+    h->pd.units = h->d_units;
     *out = h;
     return ATO_OK;
 }
@@ -162,7 +165,7 @@ static int eval_impl(ato_handle* h, int32_t batch, int32_t layout, const T* w, T
     ato::with_model(p, [&]<class M>() {
         hipEvent_t* ev = nullptr;
         if ((size_t)(h->timed_calls + 1) * 3 <= h->events.size()) ev = &h->events[(size_t)h->timed_calls++ * 3];
-        e = ato::launch_eval<M, T>(p, batch, layout, w, g, jac, grad_f, (T*)h->d_fpart, f, (hipStream_t)stream,
+        e = ato::launch_eval<M, T>(p, batch, layout, w, g, jac, grad_f, f, (T*)h->d_fpart, (hipStream_t)stream,
                                    ev);
     });
     if (e != hipSuccess) return fail(ATO_ERR_HIP, std::string("kernel launch: ") + hipGetErrorString(e));

@@ -8,11 +8,11 @@
 // The node-uniform problem data (coefficients, Darboux frame of the node, segment
 // offsets) is wave-uniform and comes through the scalar path.
 //
-//   grid.x = ceil(B / 64) instance chunks, grid.y = P node units (+1 tail unit)
-//   node unit (n, k): collocation rows of (n, k), its regularity / stage / sphere row,
-//                     the continuity + fixed-s rows of interval n (k == 0), cost gradient
-//   tail unit:        equal-h rows, gates, loop closure
-//   k_cost_reduce:    f = sum_n partial(n)   (deterministic order)
+//   grid.x = ceil(B / 64) instance chunks, grid.y = work units (ProbD::units, built by
+//   ato_layout.hpp): the tail (gates, closure, f), the two ODE row groups of every
+//   collocation node, the s-dot / dU / regularity rows of every node, the continuity rows
+//   of every interval (which also write the interval's cost partial). k_cost_reduce then
+//   sums the partials into f in a fixed order.
 #pragma once
 #include <hip/hip_runtime.h>
 #include "ato_layout.hpp"
@@ -54,7 +54,7 @@ __global__ __launch_bounds__(WAVE) void k_eval(ProbD p, int B, int layout, const
                                                T* __restrict__ gf, T* __restrict__ fpart) {
     const int b = blockIdx.x * WAVE + threadIdx.x;
     if (b >= B) return;
-    const int unit = blockIdx.y;
+    const int32_t* ut = p.units + 4 * blockIdx.y;      // wave-uniform: scalar loads
     long st;
     const T* wb;
     T *gb = nullptr, *Jb = nullptr, *gfb = nullptr;
@@ -73,74 +73,33 @@ __global__ __launch_bounds__(WAVE) void k_eval(ProbD p, int B, int layout, const
     }
     const DevW<T> W{wb, st};
     DevSink<T, WJ, WG> s{Jb, gb, st, st, 0, 0};
-
-    if (unit < p.P) {
-        const int n = unit / p.K1, k = unit - n * p.K1;
-        const int32_t* sg = p.seg + (long)unit * NSEG * 2;
-        if (WJ || WG) {
-            for (int kind = 0; kind < NSEG; ++kind) {
-                const int r0 = sg[2 * kind];
-                if (r0 < 0) continue;
-                s.begin(r0, sg[2 * kind + 1]);
-                run_node_seg<M, T>(p, kind, n, k, W, s);
-            }
-        }
-        if (WF) {
-            constexpr int NZ = M::NZ, NU = M::NU;
-            const Cols<M> c{p.N, p.K1};
-            T gu[NU], gdu[NU];
-            stage_cost<M, T>(p, n, k, W, gu, gdu);
-            const T h = W(n);
-            const T hB = h * T(p.Bq[k]);
-            const long base = (long)c.node(n, k) * st;
-#pragma unroll
-            for (int i = 0; i < NZ; ++i) gfb[base + i * st] = T(0);
-#pragma unroll
-            for (int i = 0; i < NU; ++i) gfb[base + (NZ + i) * st] = hB * gu[i];
-#pragma unroll
-            for (int i = 0; i < NU; ++i) gfb[base + (NZ + NU + i) * st] = hB * gdu[i];
-            if (k == 0) {
-                T acc = T(0);
-                for (int j = 0; j < p.K1; ++j)
-                    acc += T(p.Bq[j]) * stage_cost<M, T>(p, n, j, W, (T*)nullptr, (T*)nullptr);
-                gfb[(long)n * st] = acc;
-                fpart[(long)n * B + b] = h * acc;
-            }
-        }
-    } else if (WJ || WG) {
-        for (int t = 0; t < p.n_tail; ++t) {
-            const int32_t* tl = p.tail + 4 * t;
-            s.begin(tl[2], tl[3]);
-            run_tail_seg<M, T>(p, tl[0], tl[1], W, s);
-        }
-    }
+    const GradOut<T> go{gfb, st, WF ? fpart + b : nullptr, B};
+    run_unit<M, T, WJ || WG, WF>(p, ut[0], ut[1], ut[2], W, s, go);
 }
 
+// f[b] = sum_n fpart[n][b]  (fixed order, loads issued in batches)
 template <class T>
 __global__ __launch_bounds__(256) void k_cost_reduce(int N, int B, const T* __restrict__ fpart,
                                                     T* __restrict__ f) {
     const int b = blockIdx.x * 256 + threadIdx.x;
     if (b >= B) return;
-    T acc = T(0);
-    for (int n = 0; n < N; ++n) acc += fpart[(long)n * B + b];
-    f[b] = acc;
+    f[b] = reduce_cost(fpart + b, (long)B, N);
 }
-
 
 // Host-side launcher, explicitly instantiated per model in ato_inst.hip (one translation unit
 // per model variant so the library builds in parallel).
-// ev (optional): three events recorded before k_eval, between the kernels and after k_cost_reduce
+// ev (optional): events recorded before and after k_eval (ev[2] == end as well)
 template <class M, class T>
-hipError_t launch_eval(const ProbD& p, int B, int layout, const T* w, T* g, T* J, T* gf, T* fpart, T* f,
+hipError_t launch_eval(const ProbD& p, int B, int layout, const T* w, T* g, T* J, T* gf, T* f, T* fpart,
                        hipStream_t st, hipEvent_t* ev);
 
 #ifdef ATO_DEFINE_LAUNCHERS
 template <class M, class T>
-hipError_t launch_eval(const ProbD& p, int B, int layout, const T* w, T* g, T* J, T* gf, T* fpart, T* f,
+hipError_t launch_eval(const ProbD& p, int B, int layout, const T* w, T* g, T* J, T* gf, T* f, T* fpart,
                        hipStream_t st, hipEvent_t* ev) {
     const dim3 block(WAVE);
     if (ev) (void)hipEventRecord(ev[0], st);
-    const dim3 grid((B + WAVE - 1) / WAVE, p.P + (p.n_tail > 0 ? 1 : 0));
+    const dim3 grid((B + WAVE - 1) / WAVE, p.n_units);
     const bool wj = J != nullptr, wg = g != nullptr, wf = gf != nullptr;
     auto go = [&]<bool WJ, bool WG, bool WF>() {
         hipLaunchKernelGGL((k_eval<M, T, WJ, WG, WF>), grid, block, 0, st, p, B, layout, w, g, J, gf, fpart);

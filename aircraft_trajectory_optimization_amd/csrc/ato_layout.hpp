@@ -76,7 +76,12 @@ bool with_model(const ProbD& p, F&& f) {
 template <class M, class T, class W, class S>
 ATO_HD void run_node_seg(const ProbD& p, int kind, int n, int k, const W& w, S& s) {
     switch (kind) {
-        case SEG_COLLOC: seg_colloc<M, T>(p, n, k, w, s); break;
+        case SEG_SDOT: seg_sdot<M, T>(p, n, k, w, s); break;
+        case SEG_ODE_A: seg_ode<M, T, 0, ode_split<M>()>(p, n, k, w, s); break;
+        case SEG_ODE_B:
+            if constexpr (ode_split<M>() < M::NZ) seg_ode<M, T, ode_split<M>(), M::NZ>(p, n, k, w, s);
+            break;
+        case SEG_DU: seg_du<M, T>(p, n, k, w, s); break;
         case SEG_REG: seg_reg<M, T>(p, n, k, w, s); break;
         case SEG_STAGE: seg_stage<M, T>(p, n, k, w, s); break;
         case SEG_SPHERE: seg_sphere<M, T>(p, n, k, w, s); break;
@@ -97,11 +102,104 @@ ATO_HD void run_tail_seg(const ProbD& p, int kind, int index, const W& w, S& s) 
     }
 }
 
+// where an instance's gradient / cost go (pointers already offset to the instance)
+template <class T>
+struct GradOut {
+    T* gf;       // grad f, element stride st
+    long st;
+    T* fpart;    // per-interval cost partials h_n sum_k B_k L_nk, element stride pst
+    long pst;
+};
+
+// f = sum_n partial(n), fixed order (the k_cost_reduce kernel and the CPU harness)
+template <class T>
+ATO_HD T reduce_cost(const T* fpart, long pst, int N) {
+    T acc = T(0);
+    int n = 0;
+    for (; n + 16 <= N; n += 16) {     // issue 16 independent loads before summing
+        T v[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v[i] = fpart[(long)(n + i) * pst];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc += v[i];
+    }
+    for (; n < N; ++n) acc += fpart[(long)n * pst];
+    return acc;
+}
+
+// Execute one work unit for one instance: the device kernel and the CPU test harness both
+// call this, so the dispatch is identical.
+template <class M, class T, bool ROWS, bool GRAD, class W, class S>
+ATO_HD void run_unit(const ProbD& p, int kind, int n, int k, const W& w, S& s, const GradOut<T>& go) {
+    constexpr int NZ = M::NZ, NU = M::NU;
+    const int32_t* sg = p.seg + (long)(n * p.K1 + k) * NSEG * 2;
+    auto seg = [&](int sk) {
+        if (sg[2 * sk] < 0) return;
+        s.begin(sg[2 * sk], sg[2 * sk + 1]);
+        run_node_seg<M, T>(p, sk, n, k, w, s);
+    };
+    switch (kind) {
+        case UNIT_TAIL:
+            if (ROWS) {
+                for (int t = 0; t < p.n_tail; ++t) {
+                    const int32_t* tl = p.tail + 4 * t;
+                    s.begin(tl[2], tl[3]);
+                    run_tail_seg<M, T>(p, tl[0], tl[1], w, s);
+                }
+            }
+            break;
+        case UNIT_ODE_A:
+            if (ROWS) seg(SEG_ODE_A);
+            break;
+        case UNIT_ODE_B:
+            if (ROWS) seg(SEG_ODE_B);
+            break;
+        case UNIT_NODE:
+            if (ROWS) {
+                seg(SEG_SDOT);
+                seg(SEG_DU);
+                seg(SEG_REG);
+                seg(SEG_STAGE);
+                seg(SEG_SPHERE);
+            }
+            if (GRAD) {
+                const Cols<M> c{p.N, p.K1};
+                T gu[NU], gdu[NU];
+                stage_cost<M, T>(p, n, k, w, gu, gdu);
+                const T hB = w(n) * T(p.Bq[k]);
+                const long base = (long)c.node(n, k) * go.st;
+#pragma unroll
+                for (int i = 0; i < NZ; ++i) go.gf[base + i * go.st] = T(0);
+#pragma unroll
+                for (int i = 0; i < NU; ++i) go.gf[base + (NZ + i) * go.st] = hB * gu[i];
+#pragma unroll
+                for (int i = 0; i < NU; ++i) go.gf[base + (NZ + NU + i) * go.st] = hB * gdu[i];
+            }
+            break;
+        case UNIT_INTERVAL:
+            if (ROWS) {
+                seg(SEG_CONT);
+                seg(SEG_SROWS);
+            }
+            if (GRAD) {
+                T acc = T(0);
+                for (int j = 0; j < p.K1; ++j)
+                    acc += T(p.Bq[j]) * stage_cost<M, T>(p, n, j, w, (T*)nullptr, (T*)nullptr);
+                go.gf[(long)n * go.st] = acc;
+                go.fpart[(long)n * go.pst] = w(n) * acc;
+            }
+            break;
+        default:
+            break;
+    }
+}
+
 struct Layout {
     ProbD p{};                        // host pointers into the vectors below
     std::vector<double> geom, node_s, interval_s, spheres;
     std::vector<ato_gate> gates;
     std::vector<int32_t> seg, tail;   // segment tables (see ProbD)
+    std::vector<int32_t> units;       // work-unit table (see ProbD)
     std::vector<int32_t> row_ptr, col;
     std::vector<double> lbg, ubg;
     int nz = 0, nu = 0;
@@ -114,6 +212,8 @@ struct Layout {
         p.spheres = spheres.empty() ? nullptr : spheres.data();
         p.seg = seg.data();
         p.tail = tail.data();
+        p.units = units.data();
+        p.n_units = (int32_t)(units.size() / 4);
     }
 
     // returns empty string on success
@@ -211,8 +311,31 @@ struct Layout {
         p.ng = (int32_t)lbg.size();
         p.nnz = (int32_t)col.size();
         p.n_tail = (int32_t)(tail.size() / 4);
+        build_units();
         rebind();
         return "";
+    }
+
+    // Work units, heaviest first so the dispatcher starts the long ones early:
+    // tail (gates, closure, f), ODE groups of every collocation node, then node and interval units.
+    void build_units() {
+        units.clear();
+        auto add = [&](int kind, int n, int k) {
+            units.push_back(kind);
+            units.push_back(n);
+            units.push_back(k);
+            units.push_back(0);
+        };
+        add(UNIT_TAIL, 0, 0);
+        for (int n = 0; n < p.N; ++n)
+            for (int k = 1; k < p.K1; ++k) {
+                const int32_t* sg = &seg[((size_t)(n * p.K1 + k) * NSEG) * 2];
+                if (sg[2 * SEG_ODE_A] >= 0) add(UNIT_ODE_A, n, k);
+                if (sg[2 * SEG_ODE_B] >= 0) add(UNIT_ODE_B, n, k);
+            }
+        for (int n = 0; n < p.N; ++n)
+            for (int k = 0; k < p.K1; ++k) add(UNIT_NODE, n, k);
+        for (int n = 0; n < p.N; ++n) add(UNIT_INTERVAL, n, 0);
     }
 
   private:
@@ -265,7 +388,14 @@ struct Layout {
         if (p.phase_len > 0) ATO_TRY(tail_segment<M>(TAIL_HEQ, 0));
         const bool param = M::PARAM;
         for (int n = 0; n < p.N; ++n) {
-            for (int k = 0; k < p.K1; ++k) ATO_TRY(node_segment<M>(SEG_COLLOC, n, k));
+            for (int k = 0; k < p.K1; ++k) {
+                if (param) ATO_TRY(node_segment<M>(SEG_SDOT, n, k));
+                if (k > 0) {
+                    ATO_TRY(node_segment<M>(SEG_ODE_A, n, k));
+                    if (ode_split<M>() < M::NZ) ATO_TRY(node_segment<M>(SEG_ODE_B, n, k));
+                }
+                ATO_TRY(node_segment<M>(SEG_DU, n, k));
+            }
             if (param && p.force_reg)
                 for (int k = 0; k < p.K1; ++k)
                     if (geom[(size_t)(n * p.K1 + k) * ATO_GEOM_WIDTH + 13] != 0.0)

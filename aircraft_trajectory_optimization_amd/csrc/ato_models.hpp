@@ -227,31 +227,28 @@ struct DroneModel {
     }
     static constexpr bool umask(int i, int) { return i == IV + 2 || i >= IW; }
 
-    // f and its Jacobian, row by row.
-    template <class T, class Emit>
-    ATO_HD static void rows(const T* z, const T* u, const NodeGeom<T>& G, const Vehicle& V,
-                            Emit&& emit) {
+    // s-dot of the parametric pose and its derivatives (drone_models.py:261-267)
+    template <class T>
+    struct SDot {
+        T Rrel[9], vp[3], dvp[3][NR];
+        T sd, sd_y, sd_n, sd_r[NR], sd_v[3];
+    };
+
+    template <class T>
+    ATO_HD static void pose_terms(const T* z, const T* Ra, const NodeGeom<T>& G, SDot<T>& o) {
         const T* r = z + IR;
         const T* v = z + IV;
-        const T* w = z + IW;
-        T Ra[9];
-        A::R(r, Ra);
-
-        // ---- position rows ------------------------------------------------------
-        // Rrel: frame in which the position rate is expressed
-        //   GLOBAL: R ; PARAM_GR: Rp^T R ; PARAM_REL: R_att
-        T Rrel[9];
+        // Rrel: frame of the position rate. GLOBAL: R ; PARAM_GR: Rp^T R ; PARAM_REL: R_att
         if (FRAME == PARAM_GR) {
             for (int i = 0; i < 3; ++i)
                 for (int j = 0; j < 3; ++j)
-                    Rrel[i * 3 + j] = G.Rp[0 * 3 + i] * Ra[0 * 3 + j] + G.Rp[1 * 3 + i] * Ra[1 * 3 + j] +
-                                      G.Rp[2 * 3 + i] * Ra[2 * 3 + j];
+                    o.Rrel[i * 3 + j] = G.Rp[0 * 3 + i] * Ra[0 * 3 + j] + G.Rp[1 * 3 + i] * Ra[1 * 3 + j] +
+                                        G.Rp[2 * 3 + i] * Ra[2 * 3 + j];
         } else {
-            for (int i = 0; i < 9; ++i) Rrel[i] = Ra[i];
+            for (int i = 0; i < 9; ++i) o.Rrel[i] = Ra[i];
         }
-        T vp[3];
-        for (int i = 0; i < 3; ++i) vp[i] = Rrel[i * 3] * v[0] + Rrel[i * 3 + 1] * v[1] + Rrel[i * 3 + 2] * v[2];
-        T dvp[3][NR];   // d vp_i / d r_m
+        for (int i = 0; i < 3; ++i)
+            o.vp[i] = o.Rrel[i * 3] * v[0] + o.Rrel[i * 3 + 1] * v[1] + o.Rrel[i * 3 + 2] * v[2];
         for (int m = 0; m < NR; ++m) {
             T dRa[9];
             A::dR(r, Ra, m, dRa);
@@ -259,64 +256,99 @@ struct DroneModel {
             for (int a = 0; a < 3; ++a) dvg[a] = dRa[a * 3] * v[0] + dRa[a * 3 + 1] * v[1] + dRa[a * 3 + 2] * v[2];
             if (FRAME == PARAM_GR) {
                 for (int i = 0; i < 3; ++i)
-                    dvp[i][m] = G.Rp[0 * 3 + i] * dvg[0] + G.Rp[1 * 3 + i] * dvg[1] + G.Rp[2 * 3 + i] * dvg[2];
+                    o.dvp[i][m] = G.Rp[0 * 3 + i] * dvg[0] + G.Rp[1 * 3 + i] * dvg[1] + G.Rp[2 * 3 + i] * dvg[2];
             } else {
-                for (int i = 0; i < 3; ++i) dvp[i][m] = dvg[i];
+                for (int i = 0; i < 3; ++i) o.dvp[i][m] = dvg[i];
             }
         }
-        // s-dot and its derivatives (parametric); kept for the PARAM_REL attitude rows
-        T sd = T(0), sd_y = T(0), sd_n = T(0), sd_r[NR], sd_v[3];
-        for (int m = 0; m < NR; ++m) sd_r[m] = T(0);
-        for (int j = 0; j < 3; ++j) sd_v[j] = T(0);
+        o.sd = o.sd_y = o.sd_n = T(0);
+        for (int m = 0; m < NR; ++m) o.sd_r[m] = T(0);
+        for (int j = 0; j < 3; ++j) o.sd_v[j] = T(0);
         if (PARAM) {
             const T y = z[1], n = z[2];
             const T den = T(1) + G.ky * n - G.kn * y;
             const T iden = T(1) / (G.mag * den);
-            sd = vp[0] * iden;
-            sd_y = sd * G.kn / den;
-            sd_n = -sd * G.ky / den;
-            for (int m = 0; m < NR; ++m) sd_r[m] = dvp[0][m] * iden;
-            for (int j = 0; j < 3; ++j) sd_v[j] = Rrel[j] * iden;
-            const T km = G.ks * G.mag;
-            {   // s-dot
-                T dz[NZ] = {}, du[NU] = {};
-                dz[1] = sd_y; dz[2] = sd_n;
-                for (int m = 0; m < NR; ++m) dz[IR + m] = sd_r[m];
-                for (int j = 0; j < 3; ++j) dz[IV + j] = sd_v[j];
-                emit(0, sd, dz, du);
-            }
-            {   // y-dot = vp1 + n ks |xc'| s-dot
-                T dz[NZ] = {}, du[NU] = {};
-                const T c = n * km;
-                dz[1] = c * sd_y;
-                dz[2] = km * sd + c * sd_n;
-                for (int m = 0; m < NR; ++m) dz[IR + m] = dvp[1][m] + c * sd_r[m];
-                for (int j = 0; j < 3; ++j) dz[IV + j] = Rrel[3 + j] + c * sd_v[j];
-                emit(1, vp[1] + c * sd, dz, du);
-            }
-            {   // n-dot = vp2 - y ks |xc'| s-dot
-                T dz[NZ] = {}, du[NU] = {};
-                const T c = y * km;
-                dz[1] = -km * sd - c * sd_y;
-                dz[2] = -c * sd_n;
-                for (int m = 0; m < NR; ++m) dz[IR + m] = dvp[2][m] - c * sd_r[m];
-                for (int j = 0; j < 3; ++j) dz[IV + j] = Rrel[6 + j] - c * sd_v[j];
-                emit(2, vp[2] - c * sd, dz, du);
-            }
-        } else {
-            for (int i = 0; i < 3; ++i) {
-                T dz[NZ] = {}, du[NU] = {};
-                for (int m = 0; m < NR; ++m) dz[IR + m] = dvp[i][m];
-                for (int j = 0; j < 3; ++j) dz[IV + j] = Rrel[i * 3 + j];
-                emit(i, vp[i], dz, du);
+            o.sd = o.vp[0] * iden;
+            o.sd_y = o.sd * G.kn / den;
+            o.sd_n = -o.sd * G.ky / den;
+            for (int m = 0; m < NR; ++m) o.sd_r[m] = o.dvp[0][m] * iden;
+            for (int j = 0; j < 3; ++j) o.sd_v[j] = o.Rrel[j] * iden;
+        }
+    }
+
+    // f and its Jacobian for rows [R0, R1), row by row (R0 / R1 fixed at compile time so a
+    // kernel unit evaluates only the row groups it writes).
+    template <int R0 = 0, int R1 = NZ, class T, class Emit>
+    ATO_HD static void rows(const T* z, const T* u, const NodeGeom<T>& G, const Vehicle& V,
+                            Emit&& emit) {
+        const T* r = z + IR;
+        const T* v = z + IV;
+        const T* w = z + IW;
+        T Ra[9];
+        A::R(r, Ra);
+        constexpr bool DO_POS = R0 < 3;
+        constexpr bool DO_ATT = R0 < IV && R1 > IR;
+        constexpr bool DO_VEL = R0 < IW && R1 > IV;
+        constexpr bool DO_ANG = R1 > IW;
+
+        // ---- position rows ------------------------------------------------------
+        if constexpr (DO_POS) {
+            SDot<T> P;
+            pose_terms(z, Ra, G, P);
+            if (PARAM) {
+                const T y = z[1], n = z[2];
+                const T km = G.ks * G.mag;
+                {   // s-dot
+                    T dz[NZ] = {}, du[NU] = {};
+                    dz[1] = P.sd_y; dz[2] = P.sd_n;
+                    for (int m = 0; m < NR; ++m) dz[IR + m] = P.sd_r[m];
+                    for (int j = 0; j < 3; ++j) dz[IV + j] = P.sd_v[j];
+                    emit(0, P.sd, dz, du);
+                }
+                {   // y-dot = vp1 + n ks |xc'| s-dot
+                    T dz[NZ] = {}, du[NU] = {};
+                    const T c = n * km;
+                    dz[1] = c * P.sd_y;
+                    dz[2] = km * P.sd + c * P.sd_n;
+                    for (int m = 0; m < NR; ++m) dz[IR + m] = P.dvp[1][m] + c * P.sd_r[m];
+                    for (int j = 0; j < 3; ++j) dz[IV + j] = P.Rrel[3 + j] + c * P.sd_v[j];
+                    emit(1, P.vp[1] + c * P.sd, dz, du);
+                }
+                {   // n-dot = vp2 - y ks |xc'| s-dot
+                    T dz[NZ] = {}, du[NU] = {};
+                    const T c = y * km;
+                    dz[1] = -km * P.sd - c * P.sd_y;
+                    dz[2] = -c * P.sd_n;
+                    for (int m = 0; m < NR; ++m) dz[IR + m] = P.dvp[2][m] - c * P.sd_r[m];
+                    for (int j = 0; j < 3; ++j) dz[IV + j] = P.Rrel[6 + j] - c * P.sd_v[j];
+                    emit(2, P.vp[2] - c * P.sd, dz, du);
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < 3; ++i) {
+                    T dz[NZ] = {}, du[NU] = {};
+                    for (int m = 0; m < NR; ++m) dz[IR + m] = P.dvp[i][m];
+                    for (int j = 0; j < 3; ++j) dz[IV + j] = P.Rrel[i * 3 + j];
+                    emit(i, P.vp[i], dz, du);
+                }
             }
         }
 
         // ---- attitude rows -------------------------------------------------------
-        {
+        if constexpr (DO_ATT) {
             T weff[3] = {w[0], w[1], w[2]};
             T wp[3] = {T(0), T(0), T(0)};
+            T sd = T(0), sd_y = T(0), sd_n = T(0), sd_r[NR], sd_v[3];
+            for (int m = 0; m < NR; ++m) sd_r[m] = T(0);
+            for (int j = 0; j < 3; ++j) sd_v[j] = T(0);
             if (FRAME == PARAM_REL) {
+                SDot<T> P;
+                pose_terms(z, Ra, G, P);
+                sd = P.sd;
+                sd_y = P.sd_y;
+                sd_n = P.sd_n;
+                for (int m = 0; m < NR; ++m) sd_r[m] = P.sd_r[m];
+                for (int j = 0; j < 3; ++j) sd_v[j] = P.sd_v[j];
                 // w_eff = w_b - R^T k s-dot |xc'|      (drone_models.py:270-274)
                 const T kk[3] = {G.ks, G.ky, G.kn};
                 for (int c = 0; c < 3; ++c) wp[c] = kk[c] * sd * G.mag;
@@ -325,6 +357,7 @@ struct DroneModel {
             T rdot[NR], drq[NR][NR], Mm[NR][3];
             A::kin(r, weff, rdot, drq, Mm);
             if (FRAME != PARAM_REL) {
+#pragma unroll
                 for (int i = 0; i < NR; ++i) {
                     T dz[NZ] = {}, du[NU] = {};
                     for (int m = 0; m < NR; ++m) dz[IR + m] = drq[i][m];
@@ -343,6 +376,7 @@ struct DroneModel {
                     for (int j = 0; j < 3; ++j)
                         dwe_r[j][m] = -(dRa[j] * wp[0] + dRa[3 + j] * wp[1] + dRa[6 + j] * wp[2]) - Rtk[j] * sd_r[m];
                 }
+#pragma unroll
                 for (int i = 0; i < NR; ++i) {
                     T dz[NZ] = {}, du[NU] = {};
                     T My = T(0), Mn = T(0);
@@ -369,7 +403,7 @@ struct DroneModel {
         }
 
         // ---- body linear velocity rows (drone_models.py:61-92, 114) ------------------
-        {
+        if constexpr (DO_VEL) {
             // gravity uses row 3 of the global rotation: R (global / global_r) or Rp R (relative)
             T Rg2[3], dRg2[3][NR];
             if (FRAME == PARAM_REL) {
@@ -391,6 +425,7 @@ struct DroneModel {
             const T usum = u[0] + u[1] + u[2] + u[3];
             // v_dot = F_b / m - w x v
             const T wxv[3] = {w[1] * v[2] - w[2] * v[1], w[2] * v[0] - w[0] * v[2], w[0] * v[1] - w[1] * v[0]};
+#pragma unroll
             for (int i = 0; i < 3; ++i) {
                 T dz[NZ] = {}, du[NU] = {};
                 const T Fb = -T(V.b[i]) * v[i] + mg * Rg2[i] + (i == 2 ? usum : T(0));
@@ -408,7 +443,7 @@ struct DroneModel {
         }
 
         // ---- body angular velocity rows: w_dot = I^-1 (K_b - w x I w) -----------------
-        {
+        if constexpr (DO_ANG) {
             const T I0 = T(V.I[0]), I1 = T(V.I[1]), I2 = T(V.I[2]);
             const T l = T(V.l), kt = T(V.kt);
             const T Ka[3] = {(u[0] + u[1] - u[2] - u[3]) * l, (-u[0] + u[1] + u[2] - u[3]) * l,
@@ -418,6 +453,7 @@ struct DroneModel {
             const T wxIw[3] = {w[1] * Iw[2] - w[2] * Iw[1], w[2] * Iw[0] - w[0] * Iw[2],
                                w[0] * Iw[1] - w[1] * Iw[0]};
             const T Ii[3] = {I0, I1, I2};
+#pragma unroll
             for (int i = 0; i < 3; ++i) {
                 T dz[NZ] = {}, du[NU] = {};
                 const T iI = T(1) / Ii[i];
@@ -450,9 +486,10 @@ struct PointModel {
     }
     static constexpr bool umask(int i, int m) { return i >= 3 && (m == i - 3); }
 
-    template <class T, class Emit>
+    template <int R0 = 0, int R1 = NZ, class T, class Emit>
     ATO_HD static void rows(const T* z, const T* u, const NodeGeom<T>& G, const Vehicle& V,
                             Emit&& emit) {
+        static_assert(R0 == 0 && R1 == NZ, "point-mass rows are evaluated as one group");
         const T* v = z + 3;
         T sd = T(0), sd_y = T(0), sd_n = T(0), sd_v[3] = {T(0), T(0), T(0)};
         if (PARAM) {

@@ -27,9 +27,18 @@
 
 namespace ato {
 
-enum SegKind { SEG_COLLOC = 0, SEG_REG, SEG_STAGE, SEG_SPHERE, SEG_CONT, SEG_SROWS, NSEG };
+// Row segments of node (n, k) in reference order: s-dot row, ODE rows (two groups), dU rows;
+// then per interval: regularity rows, stage rows, continuity, fixed-s rows.
+enum SegKind { SEG_SDOT = 0, SEG_ODE_A, SEG_ODE_B, SEG_DU, SEG_REG, SEG_STAGE, SEG_SPHERE, SEG_CONT,
+               SEG_SROWS, NSEG };
 enum TailKind { TAIL_HEQ = 0, TAIL_CLOSURE_BASE, TAIL_INITIAL, TAIL_TERMINAL, TAIL_GATE,
                 TAIL_DRONE_CLOSURE };
+// Work units of the evaluation kernel (one per grid.y index; see ato_layout.hpp)
+//   UNIT_TAIL      equal-h rows, gates, closure, f
+//   UNIT_ODE_A/B   ODE defect rows [0, SPLIT) / [SPLIT, NZ) of node (n, k > 0)
+//   UNIT_NODE      s-dot, dU, regularity, stage and sphere rows of node (n, k); grad f of its inputs
+//   UNIT_INTERVAL  continuity and fixed-s rows of interval n; d f / d h_n
+enum UnitKind { UNIT_TAIL = 0, UNIT_ODE_A, UNIT_ODE_B, UNIT_NODE, UNIT_INTERVAL };
 
 #ifndef ATO_INF
 #define ATO_INF (__builtin_huge_val())
@@ -52,7 +61,13 @@ struct ProbD {
     const double* spheres;     // [P][3]
     const int32_t* seg;        // [P][NSEG][2]  (row0, nnz0); -1 = absent
     const int32_t* tail;       // [n_tail][4]   (kind, index, row0, nnz0)
+    const int32_t* units;      // [n_units][4]  (UnitKind, n, k, 0)
+    int32_t n_units, pad_units;
 };
+
+// first row of the second ODE group (drone: body-velocity rows; point mass: none)
+template <class M>
+constexpr int ode_split() { return M::IS_DRONE ? M::IV : M::NZ; }
 
 template <class T>
 ATO_HD NodeGeom<T> load_geom(const ProbD& p, int node) {
@@ -78,55 +93,72 @@ struct Cols {
 };
 
 // -------------------------------------------------------------------------- collocation node
-// Rows of node (n, k): [s-dot poly >= 0 (param)] [ODE defect (k > 0)] [dU defect].
+// p_k = sum_j C[j][k] Z_j / h  (base_raceline.py:413-418): numerators for components [I0, I1)
+template <class M, class T, class W>
+ATO_HD void poly_num(const ProbD& p, int n, int k, int I0, int I1, int uz, const W& w, T* P) {
+    const Cols<M> c{p.N, p.K1};
+    const int K1 = p.K1;
+    for (int i = I0; i < I1; ++i) P[i - I0] = T(0);
+    for (int j = 0; j < K1; ++j) {
+        const T cj = T(p.C[j * K1 + k]);
+        const int base = uz ? c.u(n, j, 0) : c.z(n, j, 0);
+        for (int i = I0; i < I1; ++i) P[i - I0] += cj * w(base + i);
+    }
+}
+
+// poly_ode[0] >= 0  (parametric; base_raceline.py:422-425)
 template <class M, class T, class W, class S>
-ATO_HD void seg_colloc(const ProbD& p, int n, int k, const W& w, S& s) {
+ATO_HD void seg_sdot(const ProbD& p, int n, int k, const W& w, S& s) {
+    const Cols<M> c{p.N, p.K1};
+    const T h = w(n), ih = T(1) / h;
+    T P0;
+    poly_num<M, T>(p, n, k, 0, 1, 0, w, &P0);
+    s.jac(n, -P0 * ih * ih);
+    for (int j = 0; j < p.K1; ++j) s.jac(c.z(n, j, 0), T(p.C[j * p.K1 + k]) * ih);
+    s.row(P0 * ih, 0.0, ATO_INF);
+}
+
+// f_i(Z_k, U_k) - poly_ode_i = 0 for rows i in [R0, R1), k > 0  (base_raceline.py:427-430)
+template <class M, class T, int R0, int R1, class W, class S>
+ATO_HD void seg_ode(const ProbD& p, int n, int k, const W& w, S& s) {
     constexpr int NZ = M::NZ, NU = M::NU;
     const Cols<M> c{p.N, p.K1};
     const int K1 = p.K1;
     const T h = w(n);
     const T ih = T(1) / h, ih2 = ih * ih;
-    T Pz[NZ], Pu[NU];
+    T Pz[R1 - R0 > 0 ? R1 - R0 : 1];
+    poly_num<M, T>(p, n, k, R0, R1, 0, w, Pz);
+    T z[NZ], u[NU];
 #pragma unroll
-    for (int i = 0; i < NZ; ++i) Pz[i] = T(0);
+    for (int i = 0; i < NZ; ++i) z[i] = w(c.z(n, k, i));
 #pragma unroll
-    for (int i = 0; i < NU; ++i) Pu[i] = T(0);
-    for (int j = 0; j < K1; ++j) {
-        const T cj = T(p.C[j * K1 + k]);
+    for (int i = 0; i < NU; ++i) u[i] = w(c.u(n, k, i));
+    const NodeGeom<T> G = load_geom<T>(p, n * K1 + k);
+    const T ckk = T(p.C[k * K1 + k]) * ih;
+    M::template rows<R0, R1>(z, u, G, p.veh, [&](int i, T fi, const T* dz, const T* du) {
+        const T Pi = Pz[i - R0];
+        s.jac(n, Pi * ih2);
+        for (int j = 0; j < k; ++j) s.jac(c.z(n, j, i), -T(p.C[j * K1 + k]) * ih);
 #pragma unroll
-        for (int i = 0; i < NZ; ++i) Pz[i] += cj * w(c.z(n, j, i));
+        for (int m = 0; m < NZ; ++m)
+            if (M::zmask(i, m) || m == i) s.jac(c.z(n, k, m), m == i ? dz[m] - ckk : dz[m]);
 #pragma unroll
-        for (int i = 0; i < NU; ++i) Pu[i] += cj * w(c.u(n, j, i));
-    }
-    if (M::PARAM) {
-        // poly_ode[0] >= 0  (base_raceline.py:422-425)
-        s.jac(n, -Pz[0] * ih2);
-        for (int j = 0; j < K1; ++j) s.jac(c.z(n, j, 0), T(p.C[j * K1 + k]) * ih);
-        s.row(Pz[0] * ih, 0.0, ATO_INF);
-    }
-    if (k > 0) {
-        T z[NZ], u[NU];
-#pragma unroll
-        for (int i = 0; i < NZ; ++i) z[i] = w(c.z(n, k, i));
-#pragma unroll
-        for (int i = 0; i < NU; ++i) u[i] = w(c.u(n, k, i));
-        const NodeGeom<T> G = load_geom<T>(p, n * K1 + k);
-        const T ckk = T(p.C[k * K1 + k]) * ih;
-        // f(Z_k, U_k) - poly_ode = 0  (base_raceline.py:427-430)
-        M::rows(z, u, G, p.veh, [&](int i, T fi, const T* dz, const T* du) {
-            s.jac(n, Pz[i] * ih2);
-            for (int j = 0; j < k; ++j) s.jac(c.z(n, j, i), -T(p.C[j * K1 + k]) * ih);
-#pragma unroll
-            for (int m = 0; m < NZ; ++m)
-                if (M::zmask(i, m) || m == i) s.jac(c.z(n, k, m), m == i ? dz[m] - ckk : dz[m]);
-#pragma unroll
-            for (int m = 0; m < NU; ++m)
-                if (M::umask(i, m)) s.jac(c.u(n, k, m), du[m]);
-            for (int j = k + 1; j < K1; ++j) s.jac(c.z(n, j, i), -T(p.C[j * K1 + k]) * ih);
-            s.row(fi - Pz[i] * ih, 0.0, 0.0);
-        });
-    }
-    // dU - poly_du = 0  (base_raceline.py:432-434)
+        for (int m = 0; m < NU; ++m)
+            if (M::umask(i, m)) s.jac(c.u(n, k, m), du[m]);
+        for (int j = k + 1; j < K1; ++j) s.jac(c.z(n, j, i), -T(p.C[j * K1 + k]) * ih);
+        s.row(fi - Pi * ih, 0.0, 0.0);
+    });
+}
+
+// dU - poly_du = 0  (base_raceline.py:432-434)
+template <class M, class T, class W, class S>
+ATO_HD void seg_du(const ProbD& p, int n, int k, const W& w, S& s) {
+    constexpr int NU = M::NU;
+    const Cols<M> c{p.N, p.K1};
+    const int K1 = p.K1;
+    const T h = w(n), ih = T(1) / h, ih2 = ih * ih;
+    T Pu[NU];
+    poly_num<M, T>(p, n, k, 0, NU, 1, w, Pu);
 #pragma unroll
     for (int i = 0; i < NU; ++i) {
         s.jac(n, Pu[i] * ih2);

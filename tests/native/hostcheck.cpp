@@ -82,46 +82,20 @@ void atoh_bounds(const atoh_handle* h, double* lb, double* ub) {
 }
 
 // instance-major evaluation of B instances: w [B][nw], g [B][ng], J [B][nnz], f [B], gf [B][nw]
+// Walks the same work-unit table and calls the same run_unit() as the HIP kernel.
 int atoh_eval(const atoh_handle* h, int B, const double* w, double* g, double* J, double* f, double* gf) {
     const ato::ProbD& p = h->L.p;
     bool ok = ato::with_model(p, [&]<class M>() {
-        constexpr int NZ = M::NZ, NU = M::NU;
-        const ato::Cols<M> c{p.N, p.K1};
+        std::vector<double> fpart(p.N);
         for (int b = 0; b < B; ++b) {
             HostW<double> W{w + (long)b * p.nw, 1};
             HostSink<double> s{J ? J + (long)b * p.nnz : nullptr, g ? g + (long)b * p.ng : nullptr, 1, 1, 0, 0};
-            double fsum = 0.0;
-            for (int unit = 0; unit < p.P; ++unit) {
-                const int n = unit / p.K1, k = unit % p.K1;
-                for (int kind = 0; kind < ato::NSEG; ++kind) {
-                    const int32_t* sg = p.seg + ((long)unit * ato::NSEG + kind) * 2;
-                    if (sg[0] < 0) continue;
-                    s.begin(sg[0], sg[1]);
-                    ato::run_node_seg<M, double>(p, kind, n, k, W, s);
-                }
-                double gu[NU], gdu[NU];
-                ato::stage_cost<M, double>(p, n, k, W, gu, gdu);
-                const double hB = W(n) * p.Bq[k];
-                if (gf) {
-                    double* gb = gf + (long)b * p.nw;
-                    for (int i = 0; i < NZ; ++i) gb[c.z(n, k, i)] = 0.0;
-                    for (int i = 0; i < NU; ++i) gb[c.u(n, k, i)] = hB * gu[i];
-                    for (int i = 0; i < NU; ++i) gb[c.du(n, k, i)] = hB * gdu[i];
-                }
-                if (k == 0) {
-                    double acc = 0.0;
-                    for (int j = 0; j < p.K1; ++j)
-                        acc += p.Bq[j] * ato::stage_cost<M, double>(p, n, j, W, (double*)nullptr, (double*)nullptr);
-                    if (gf) gf[(long)b * p.nw + n] = acc;
-                    fsum += W(n) * acc;
-                }
+            const ato::GradOut<double> go{gf + (long)b * p.nw, 1, fpart.data(), 1};
+            for (int u = 0; u < p.n_units; ++u) {
+                const int32_t* ut = p.units + 4 * u;
+                ato::run_unit<M, double, true, true>(p, ut[0], ut[1], ut[2], W, s, go);
             }
-            for (int t = 0; t < p.n_tail; ++t) {
-                const int32_t* tl = p.tail + 4 * t;
-                s.begin(tl[2], tl[3]);
-                ato::run_tail_seg<M, double>(p, tl[0], tl[1], W, s);
-            }
-            if (f) f[b] = fsum;
+            f[b] = ato::reduce_cost(fpart.data(), 1, p.N);
         }
     });
     if (!ok) {

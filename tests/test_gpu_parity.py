@@ -96,15 +96,15 @@ def test_deterministic_and_partial_outputs():
     g1, J1, f1, gf1 = bn.results()
     bn.g.zero_()
     bn.jac.zero_()
-    bn.evaluate(jac=False, cost=False)      # g only
-    g2 = bn.results()[0]
-    np.testing.assert_array_equal(g1, g2)
-    bn.evaluate(g=False, cost=False)        # J only
-    np.testing.assert_array_equal(J1, bn.results()[1])
-    bn.evaluate()
+    bn.evaluate()                           # same launch again: bitwise identical
     r = bn.results()
-    np.testing.assert_array_equal(f1, r[2])
-    np.testing.assert_array_equal(gf1, r[3])
+    for x, y in zip((g1, J1, f1, gf1), r):
+        np.testing.assert_array_equal(x, y)
+    # g-only / J-only launches are other kernel instantiations: equal up to rounding
+    bn.evaluate(jac=False, cost=False)
+    _close(bn.results()[0], g1, 1e-14)
+    bn.evaluate(g=False, cost=False)
+    _close(bn.results()[1], J1, 1e-14)
 
 
 def test_fp32_tracks_fp64():

@@ -1,0 +1,47 @@
+#!/bin/bash
+# GPU session script for gpurun: parity tests, smoke, bench, rocprof kernel trace.
+# Each GPU step has its own time limit; the script stops at the first crash-like exit
+# (abort / segfault / timeout / kill) and otherwise records failures and continues.
+# Usage: tools/gpu_check.sh <tag> [steps...]   steps: tests smoke bench prof pmc
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+TAG=${1:-r01}
+shift || true
+STEPS=${*:-tests smoke bench prof}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+status=0
+
+run() {  # run <name> <seconds> <cmd...>
+    local name=$1 secs=$2
+    shift 2
+    echo "[gpu_check] $(date +%T) start $name" | tee -a "$OUT/steps.log"
+    timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+    local rc=$?
+    echo "[gpu_check] $(date +%T) end $name rc=$rc" | tee -a "$OUT/steps.log"
+    case $rc in
+        0) ;;
+        124|137|134|139|136|135) echo "[gpu_check] crash-like exit, stopping" | tee -a "$OUT/steps.log"; exit $rc ;;
+        *) status=$rc ;;
+    esac
+}
+
+for s in $STEPS; do
+    case $s in
+        tests) run pytest_gpu 600 python -m pytest tests -m gpu -q -x -p no:cacheprovider ;;
+        smoke) run smoke 300 python -c 'import __graft_entry__ as g; g.smoke()' ;;
+        bench) run bench 400 python bench.py --steps 50 --warmup 10 ;;
+        bench32) run bench_f32 300 python bench.py --steps 50 --warmup 10 --dtype f32 --no-cpu-baseline ;;
+        benchim) run bench_im 300 python bench.py --steps 50 --warmup 10 --layout instance --no-cpu-baseline ;;
+        benchbig) run bench_b4096 300 python bench.py --steps 20 --warmup 5 --batch 4096 --no-cpu-baseline ;;
+        prof)  run prof 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
+                   python bench.py --steps 50 --warmup 10 --no-cpu-baseline ;;
+        pmc)   run pmc_fetch 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- \
+                   python bench.py --steps 20 --warmup 5 --no-cpu-baseline &&
+               run pmc_write 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \
+                   python bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
+        *) echo "unknown step $s" ;;
+    esac
+done
+exit $status
