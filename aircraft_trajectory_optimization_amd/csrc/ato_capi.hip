@@ -3,25 +3,11 @@
 #include <hip/hip_runtime.h>
 #include <string>
 #include <new>
+#include <cstdlib>
+#include <cstring>
 #include "ato_kernels.hpp"
 
-struct ato_handle {
-    ato::Layout L;
-    int device = 0;
-    ato::ProbD pd{};            // device-pointer copy of L.p
-    double* d_geom = nullptr;
-    double* d_node_s = nullptr;
-    double* d_interval_s = nullptr;
-    double* d_spheres = nullptr;
-    ato_gate* d_gates = nullptr;
-    int32_t* d_seg = nullptr;
-    int32_t* d_tail = nullptr;
-    int32_t* d_units = nullptr;
-    void* d_fpart = nullptr;    // [N][reserved] cost partials (double; reused for float)
-    int32_t reserved = 0;
-    std::vector<hipEvent_t> events;   // 3 per timed call
-    int32_t timed_calls = 0;
-};
+#include "ato_handle.hpp"
 
 static thread_local std::string g_last_error;
 
@@ -75,6 +61,27 @@ int ato_create(const ato_problem_desc* desc, ato_handle** out) {
     if (!err.empty()) {
         delete h;
         return fail(err.find("not supported") != std::string::npos ? ATO_ERR_UNSUPPORTED : ATO_ERR_ARG, err);
+    }
+    // Debug / profiling aid: ATO_DEBUG_UNITS=<digits> keeps only the listed unit kinds
+    // (0 tail, 1 ODE_A, 2 ODE_B, 3 node, 4 interval). Outputs are then incomplete.
+    if (const char* filt = std::getenv("ATO_DEBUG_UNITS")) {
+        std::vector<int32_t> kept;
+        int cnt[3] = {0, 0, 0};
+        for (int c = 0; c < 3; ++c)   // keep the class ordering of the table
+            for (size_t u = 0; u + 3 < h->L.units.size(); u += 4) {
+                const int kind = h->L.units[u];
+                const int cl = kind == ato::UNIT_TAIL ? 0 : (kind <= ato::UNIT_ODE_B ? 1 : 2);
+                if (cl == c && std::strchr(filt, '0' + kind)) {
+                    kept.insert(kept.end(), &h->L.units[u], &h->L.units[u] + 4);
+                    ++cnt[c];
+                }
+            }
+        h->L.units = kept;
+        h->L.p.cls_off[0] = 0;
+        h->L.p.cls_off[1] = cnt[0];
+        h->L.p.cls_off[2] = cnt[0] + cnt[1];
+        h->L.p.cls_off[3] = cnt[0] + cnt[1] + cnt[2];
+        h->L.rebind();
     }
     int rc;
     if (hipGetDevice(&h->device) != hipSuccess) {

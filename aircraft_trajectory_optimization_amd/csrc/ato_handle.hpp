@@ -1,0 +1,23 @@
+// ato_handle.hpp -- the opaque ato_handle of include/ato.h (library-internal).
+#pragma once
+#include <vector>
+#include <hip/hip_runtime.h>
+#include "ato_kernels.hpp"
+
+struct ato_handle {
+    ato::Layout L;
+    int device = 0;
+    ato::ProbD pd{};            // device-pointer copy of L.p
+    double* d_geom = nullptr;
+    double* d_node_s = nullptr;
+    double* d_interval_s = nullptr;
+    double* d_spheres = nullptr;
+    ato_gate* d_gates = nullptr;
+    int32_t* d_seg = nullptr;
+    int32_t* d_tail = nullptr;
+    int32_t* d_units = nullptr;
+    void* d_fpart = nullptr;    // [N][reserved] cost partials (double; reused for float)
+    int32_t reserved = 0;
+    std::vector<hipEvent_t> events;   // 3 per timed call
+    int32_t timed_calls = 0;
+};

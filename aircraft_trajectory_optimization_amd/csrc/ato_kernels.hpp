@@ -37,6 +37,94 @@ struct DevSink {
         if (WG) g[r] = gv;
         r += ge;
     }
+    __device__ __forceinline__ void finish() {}
+};
+
+// Paired Jacobian writer (interleaved layout, even B). Lane l holds instance
+// 2 (l mod 32) + (l >= 32) of its 64-instance chunk, so lanes l and l + 32 hold adjacent
+// instances. Two consecutive entries (e, e+1) are exchanged with v_permlane32_swap (lanes
+// 32-63 of the first value trade with lanes 0-31 of the second): afterwards lanes 0-31 hold
+// entry e of instances (2l, 2l+1) and lanes 32-63 entry e+1 of the same instance pairs, and
+// one 16-byte store per lane (8 bytes in fp32) writes both entries: half the store
+// instructions of one store per entry, same bytes (cdna_hip_programming.md T21).
+template <class T>
+__device__ __forceinline__ void swap_halves(T& a, T& b);
+
+template <>
+__device__ __forceinline__ void swap_halves<double>(double& a, double& b) {
+    uint2 ua = __builtin_bit_cast(uint2, a), ub = __builtin_bit_cast(uint2, b);
+    auto lo = __builtin_amdgcn_permlane32_swap(ua.x, ub.x, false, false);
+    auto hi = __builtin_amdgcn_permlane32_swap(ua.y, ub.y, false, false);
+    ua.x = lo[0];
+    ub.x = lo[1];
+    ua.y = hi[0];
+    ub.y = hi[1];
+    a = __builtin_bit_cast(double, ua);
+    b = __builtin_bit_cast(double, ub);
+}
+
+template <>
+__device__ __forceinline__ void swap_halves<float>(float& a, float& b) {
+    auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, a), __builtin_bit_cast(unsigned, b),
+                                              false, false);
+    a = __builtin_bit_cast(float, (unsigned)r[0]);
+    b = __builtin_bit_cast(float, (unsigned)r[1]);
+}
+
+template <class T>
+struct Pair2 { T x, y; };
+
+template <class T, bool WJ, bool WG, bool FULL>
+struct DevSinkPaired {
+    const char* Jc;     // (char*) (J + chunk base): uniform
+    const char* gc;     // (char*) (g + chunk base): uniform
+    char* Jr;           // byte address of entry e's 64-instance row: uniform
+    char* gr;           // byte address of row r's 64-instance row: uniform
+    long Bb;            // entry stride in bytes (B * sizeof(T))
+    uint32_t pair_off;  // this lane's byte offset in a pair store: (l >= 32 ? B : 0) + 2 (l mod 32) elements
+    uint32_t self_off;  // this lane's own instance byte offset inside the chunk
+    bool pvalid, svalid;
+    T pend;
+    bool odd;
+    __device__ __forceinline__ void flush() {
+        if (WJ && odd && (FULL || svalid)) *reinterpret_cast<T*>(Jr - Bb + self_off) = pend;
+        odd = false;
+    }
+    __device__ __forceinline__ void begin(int row0, int nnz0) {
+        flush();
+        Jr = const_cast<char*>(Jc) + (long)nnz0 * Bb;
+        gr = const_cast<char*>(gc) + (long)row0 * Bb;
+    }
+    __device__ __forceinline__ void finish() { flush(); }
+    __device__ __forceinline__ void jac(int, T v) {
+        if (WJ) {
+            if (!odd) {
+                pend = v;
+                odd = true;
+            } else {
+                T a = pend, b2 = v;
+                swap_halves(a, b2);
+                if (FULL || pvalid) *reinterpret_cast<Pair2<T>*>(Jr - Bb + pair_off) = Pair2<T>{a, b2};
+                odd = false;
+            }
+        }
+        Jr += Bb;
+    }
+    __device__ __forceinline__ void row(T gv, double, double) {
+        if (WG && (FULL || svalid)) *reinterpret_cast<T*>(gr + self_off) = gv;
+        gr += Bb;
+    }
+};
+
+// decision-vector reads for the paired kernel: uniform row base + 32-bit lane byte offset
+template <class T>
+struct DevWPaired {
+    const char* w0;     // (char*) (w + chunk base)
+    long Bb;
+    uint32_t off;       // this lane's (clamped) instance byte offset
+    __device__ __forceinline__ T operator()(int col) const {
+        return *reinterpret_cast<const T*>(w0 + (long)col * Bb + off);
+    }
 };
 
 template <class T>
@@ -48,7 +136,7 @@ struct DevW {
 
 constexpr int WAVE = 64;
 
-template <class M, class T, bool WJ, bool WG, bool WF>
+template <class M, class T, int KS, bool WJ, bool WG, bool WF>
 __global__ __launch_bounds__(WAVE) void k_eval(ProbD p, int B, int layout, const T* __restrict__ w,
                                                T* __restrict__ g, T* __restrict__ J,
                                                T* __restrict__ gf, T* __restrict__ fpart) {
@@ -74,7 +162,38 @@ __global__ __launch_bounds__(WAVE) void k_eval(ProbD p, int B, int layout, const
     const DevW<T> W{wb, st};
     DevSink<T, WJ, WG> s{Jb, gb, st, st, 0, 0};
     const GradOut<T> go{gfb, st, WF ? fpart + b : nullptr, B};
-    run_unit<M, T, WJ || WG, WF>(p, ut[0], ut[1], ut[2], W, s, go);
+    run_unit<M, T, KS, WJ || WG, WF>(p, ut[0], ut[1], ut[2], W, s, go);
+}
+
+// Interleaved layout, even B: every lane stays active (permlane swaps need the whole wave);
+// lanes past the end of the batch compute on the last instance and store nothing.
+template <class M, class T, int KS, bool WJ, bool WG, bool WF, bool FULL, int UMASK>
+__global__ __launch_bounds__(WAVE) void k_eval_paired(ProbD p, int B, int unit0, const T* __restrict__ w,
+                                                      T* __restrict__ g, T* __restrict__ J,
+                                                      T* __restrict__ gf, T* __restrict__ fpart) {
+    const int l = threadIdx.x;
+    const int chunk = blockIdx.x * WAVE;
+    const int own = 2 * (l & 31) + (l >> 5);        // instance of this lane inside the chunk
+    const int b = chunk + own;
+    const int bl = (FULL || b < B) ? b : B - 1;     // clamped instance for loads
+    const int32_t* ut = p.units + 4 * (unit0 + blockIdx.y);   // wave-uniform: scalar loads
+    const long Bb = (long)B * sizeof(T);
+    const DevWPaired<T> W{reinterpret_cast<const char*>(w + chunk), Bb, (uint32_t)((bl - chunk) * sizeof(T))};
+    DevSinkPaired<T, WJ, WG, FULL> s;
+    s.Jc = reinterpret_cast<const char*>(J + chunk);
+    s.gc = reinterpret_cast<const char*>(g + chunk);
+    s.Jr = nullptr;
+    s.gr = nullptr;
+    s.Bb = Bb;
+    s.pair_off = (uint32_t)(((l >= 32 ? (long)B : 0L) + 2 * (l & 31)) * sizeof(T));
+    s.self_off = (uint32_t)(own * sizeof(T));
+    s.pvalid = chunk + 2 * (l & 31) < B;
+    s.svalid = b < B;
+    s.pend = T(0);
+    s.odd = false;
+    const GradOut<T> go{WF ? gf + bl : nullptr, (long)B, WF ? fpart + bl : nullptr, B};
+    if (WJ || WG) run_unit<M, T, KS, true, false, UMASK>(p, ut[0], ut[1], ut[2], W, s, go);   // whole wave
+    if (WF && (FULL || b < B)) run_unit<M, T, KS, false, true, UMASK>(p, ut[0], ut[1], ut[2], W, s, go);
 }
 
 // f[b] = sum_n fpart[n][b]  (fixed order, loads issued in batches)
@@ -88,7 +207,7 @@ __global__ __launch_bounds__(256) void k_cost_reduce(int N, int B, const T* __re
 
 // Host-side launcher, explicitly instantiated per model in ato_inst.hip (one translation unit
 // per model variant so the library builds in parallel).
-// ev (optional): events recorded before and after k_eval (ev[2] == end as well)
+// ev (optional): events recorded before / after the g, J kernels and after the cost reduction
 template <class M, class T>
 hipError_t launch_eval(const ProbD& p, int B, int layout, const T* w, T* g, T* J, T* gf, T* f, T* fpart,
                        hipStream_t st, hipEvent_t* ev);
@@ -98,19 +217,38 @@ template <class M, class T>
 hipError_t launch_eval(const ProbD& p, int B, int layout, const T* w, T* g, T* J, T* gf, T* f, T* fpart,
                        hipStream_t st, hipEvent_t* ev) {
     const dim3 block(WAVE);
-    if (ev) (void)hipEventRecord(ev[0], st);
-    const dim3 grid((B + WAVE - 1) / WAVE, p.n_units);
+    const int chunks = (B + WAVE - 1) / WAVE;
     const bool wj = J != nullptr, wg = g != nullptr, wf = gf != nullptr;
-    auto go = [&]<bool WJ, bool WG, bool WF>() {
-        hipLaunchKernelGGL((k_eval<M, T, WJ, WG, WF>), grid, block, 0, st, p, B, layout, w, g, J, gf, fpart);
-    };
-    if (wj && wg && wf) go.template operator()<true, true, true>();
-    else if (wj && wg) go.template operator()<true, true, false>();
-    else if (wg && wf) go.template operator()<false, true, true>();
-    else if (wg) go.template operator()<false, true, false>();
-    else if (wj && wf) go.template operator()<true, false, true>();
-    else if (wj) go.template operator()<true, false, false>();
-    else if (wf) go.template operator()<false, false, true>();
+    // Paired 16-byte stores need the interleaved layout and whole 64-instance chunks.
+    // (Measured and rejected: separate kernels per unit class on fork / join side streams --
+    // the cross-stream waits cost more than the per-class register allocation gained at
+    // B = 512, and nothing at B = 4096; compile-time K everywhere -- the hoisted loads cut
+    // occupancy to one wave per SIMD.)
+    const bool paired = layout == ATO_LAYOUT_INTERLEAVED && (B % WAVE) == 0 && wg;
+    if (ev) (void)hipEventRecord(ev[0], st);
+    if (paired) {
+        const dim3 grid(chunks, p.n_units);
+        if (wj && wg && wf)
+            hipLaunchKernelGGL((k_eval_paired<M, T, 0, true, true, true, true, UMASK_ALL>), grid, block, 0, st, p, B, 0, w, g, J, gf, fpart);
+        else if (wj && wg)
+            hipLaunchKernelGGL((k_eval_paired<M, T, 0, true, true, false, true, UMASK_ALL>), grid, block, 0, st, p, B, 0, w, g, J, gf, fpart);
+        else if (wg && wf)
+            hipLaunchKernelGGL((k_eval_paired<M, T, 0, false, true, true, true, UMASK_ALL>), grid, block, 0, st, p, B, 0, w, g, J, gf, fpart);
+        else
+            hipLaunchKernelGGL((k_eval_paired<M, T, 0, false, true, false, true, UMASK_ALL>), grid, block, 0, st, p, B, 0, w, g, J, gf, fpart);
+    } else {
+        const dim3 grid(chunks, p.n_units);
+        auto go = [&]<bool WJ, bool WG, bool WF>() {
+            hipLaunchKernelGGL((k_eval<M, T, 0, WJ, WG, WF>), grid, block, 0, st, p, B, layout, w, g, J, gf, fpart);
+        };
+        if (wj && wg && wf) go.template operator()<true, true, true>();
+        else if (wj && wg) go.template operator()<true, true, false>();
+        else if (wg && wf) go.template operator()<false, true, true>();
+        else if (wg) go.template operator()<false, true, false>();
+        else if (wj && wf) go.template operator()<true, false, true>();
+        else if (wj) go.template operator()<true, false, false>();
+        else if (wf) go.template operator()<false, false, true>();
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (ev) (void)hipEventRecord(ev[1], st);

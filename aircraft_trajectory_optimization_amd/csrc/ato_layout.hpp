@@ -45,6 +45,7 @@ struct PatSink {
         cur = 0;
         last = -1;
     }
+    void finish() {}
 };
 
 struct OnesW {
@@ -73,31 +74,31 @@ bool with_model(const ProbD& p, F&& f) {
 }
 
 // Run one segment of the given kind with any sink / accessor.
-template <class M, class T, class W, class S>
+template <class M, class T, int KS, class W, class S>
 ATO_HD void run_node_seg(const ProbD& p, int kind, int n, int k, const W& w, S& s) {
     switch (kind) {
-        case SEG_SDOT: seg_sdot<M, T>(p, n, k, w, s); break;
-        case SEG_ODE_A: seg_ode<M, T, 0, ode_split<M>()>(p, n, k, w, s); break;
+        case SEG_SDOT: seg_sdot<M, T, KS>(p, n, k, w, s); break;
+        case SEG_ODE_A: seg_ode<M, T, KS, 0, ode_split<M>()>(p, n, k, w, s); break;
         case SEG_ODE_B:
-            if constexpr (ode_split<M>() < M::NZ) seg_ode<M, T, ode_split<M>(), M::NZ>(p, n, k, w, s);
+            if constexpr (ode_split<M>() < M::NZ) seg_ode<M, T, KS, ode_split<M>(), M::NZ>(p, n, k, w, s);
             break;
-        case SEG_DU: seg_du<M, T>(p, n, k, w, s); break;
-        case SEG_REG: seg_reg<M, T>(p, n, k, w, s); break;
-        case SEG_STAGE: seg_stage<M, T>(p, n, k, w, s); break;
-        case SEG_SPHERE: seg_sphere<M, T>(p, n, k, w, s); break;
-        case SEG_CONT: seg_cont<M, T>(p, n, w, s); break;
-        case SEG_SROWS: seg_srows<M, T>(p, n, w, s); break;
+        case SEG_DU: seg_du<M, T, KS>(p, n, k, w, s); break;
+        case SEG_REG: seg_reg<M, T, KS>(p, n, k, w, s); break;
+        case SEG_STAGE: seg_stage<M, T, KS>(p, n, k, w, s); break;
+        case SEG_SPHERE: seg_sphere<M, T, KS>(p, n, k, w, s); break;
+        case SEG_CONT: seg_cont<M, T, KS>(p, n, w, s); break;
+        case SEG_SROWS: seg_srows<M, T, KS>(p, n, w, s); break;
         default: break;
     }
 }
 
-template <class M, class T, class W, class S>
+template <class M, class T, int KS, class W, class S>
 ATO_HD void run_tail_seg(const ProbD& p, int kind, int index, const W& w, S& s) {
     switch (kind) {
-        case TAIL_HEQ: seg_heq<M, T>(p, w, s); break;
-        case TAIL_CLOSURE_BASE: seg_closure_base<M, T>(p, w, s); break;
-        case TAIL_GATE: seg_gate<M, T>(p, index, w, s); break;
-        case TAIL_DRONE_CLOSURE: seg_drone_closure<M, T>(p, w, s); break;
+        case TAIL_HEQ: seg_heq<M, T, KS>(p, w, s); break;
+        case TAIL_CLOSURE_BASE: seg_closure_base<M, T, KS>(p, w, s); break;
+        case TAIL_GATE: seg_gate<M, T, KS>(p, index, w, s); break;
+        case TAIL_DRONE_CLOSURE: seg_drone_closure<M, T, KS>(p, w, s); break;
         default: break;
     }
 }
@@ -129,32 +130,42 @@ ATO_HD T reduce_cost(const T* fpart, long pst, int N) {
 
 // Execute one work unit for one instance: the device kernel and the CPU test harness both
 // call this, so the dispatch is identical.
-template <class M, class T, bool ROWS, bool GRAD, class W, class S>
+// UMASK: unit kinds compiled into this instantiation (bit = 1 << UnitKind), so a kernel that
+// only runs light units is not register-allocated for the heavy ones.
+constexpr int UMASK_ALL = 0x1f;
+constexpr int UMASK_TAIL = 1 << UNIT_TAIL;
+constexpr int UMASK_ODE = (1 << UNIT_ODE_A) | (1 << UNIT_ODE_B);
+constexpr int UMASK_LIN = (1 << UNIT_NODE) | (1 << UNIT_INTERVAL);
+
+template <class M, class T, int KS, bool ROWS, bool GRAD, int UMASK = UMASK_ALL, class W, class S>
 ATO_HD void run_unit(const ProbD& p, int kind, int n, int k, const W& w, S& s, const GradOut<T>& go) {
     constexpr int NZ = M::NZ, NU = M::NU;
-    const int32_t* sg = p.seg + (long)(n * p.K1 + k) * NSEG * 2;
+    const int32_t* sg = p.seg + (long)(n * K1S(p) + k) * NSEG * 2;
     auto seg = [&](int sk) {
         if (sg[2 * sk] < 0) return;
         s.begin(sg[2 * sk], sg[2 * sk + 1]);
-        run_node_seg<M, T>(p, sk, n, k, w, s);
+        run_node_seg<M, T, KS>(p, sk, n, k, w, s);
     };
     switch (kind) {
-        case UNIT_TAIL:
-            if (ROWS) {
-                for (int t = 0; t < p.n_tail; ++t) {
-                    const int32_t* tl = p.tail + 4 * t;
+        case UNIT_TAIL:   // one tail segment: n = its index in p.tail
+            if constexpr ((UMASK & UMASK_TAIL) != 0) {
+                if (ROWS) {
+                    const int32_t* tl = p.tail + 4 * n;
                     s.begin(tl[2], tl[3]);
-                    run_tail_seg<M, T>(p, tl[0], tl[1], w, s);
+                    run_tail_seg<M, T, KS>(p, tl[0], tl[1], w, s);
                 }
             }
             break;
         case UNIT_ODE_A:
-            if (ROWS) seg(SEG_ODE_A);
+            if constexpr ((UMASK & (1 << UNIT_ODE_A)) != 0)
+                if (ROWS) seg(SEG_ODE_A);
             break;
         case UNIT_ODE_B:
-            if (ROWS) seg(SEG_ODE_B);
+            if constexpr ((UMASK & (1 << UNIT_ODE_B)) != 0)
+                if (ROWS) seg(SEG_ODE_B);
             break;
         case UNIT_NODE:
+            if constexpr ((UMASK & (1 << UNIT_NODE)) == 0) break;
             if (ROWS) {
                 seg(SEG_SDOT);
                 seg(SEG_DU);
@@ -163,9 +174,9 @@ ATO_HD void run_unit(const ProbD& p, int kind, int n, int k, const W& w, S& s, c
                 seg(SEG_SPHERE);
             }
             if (GRAD) {
-                const Cols<M> c{p.N, p.K1};
+                const Cols<M> c{p.N, K1S(p)};
                 T gu[NU], gdu[NU];
-                stage_cost<M, T>(p, n, k, w, gu, gdu);
+                stage_cost<M, T, KS>(p, n, k, w, gu, gdu);
                 const T hB = w(n) * T(p.Bq[k]);
                 const long base = (long)c.node(n, k) * go.st;
 #pragma unroll
@@ -177,14 +188,15 @@ ATO_HD void run_unit(const ProbD& p, int kind, int n, int k, const W& w, S& s, c
             }
             break;
         case UNIT_INTERVAL:
+            if constexpr ((UMASK & (1 << UNIT_INTERVAL)) == 0) break;
             if (ROWS) {
                 seg(SEG_CONT);
                 seg(SEG_SROWS);
             }
             if (GRAD) {
                 T acc = T(0);
-                for (int j = 0; j < p.K1; ++j)
-                    acc += T(p.Bq[j]) * stage_cost<M, T>(p, n, j, w, (T*)nullptr, (T*)nullptr);
+                for (int j = 0; j < K1S(p); ++j)
+                    acc += T(p.Bq[j]) * stage_cost<M, T, KS>(p, n, j, w, (T*)nullptr, (T*)nullptr);
                 go.gf[(long)n * go.st] = acc;
                 go.fpart[(long)n * go.pst] = w(n) * acc;
             }
@@ -192,6 +204,7 @@ ATO_HD void run_unit(const ProbD& p, int kind, int n, int k, const W& w, S& s, c
         default:
             break;
     }
+    if (ROWS) s.finish();
 }
 
 struct Layout {
@@ -316,8 +329,11 @@ struct Layout {
         return "";
     }
 
-    // Work units, heaviest first so the dispatcher starts the long ones early:
-    // tail (gates, closure, f), ODE groups of every collocation node, then node and interval units.
+    // Work units in three classes (each a contiguous range; see ProbD::cls_off / cls_cnt):
+    //   0: tail segments (equal-h rows, gates, closure), one unit each
+    //   1: the ODE row groups of every collocation node (register-heavy)
+    //   2: node units (s-dot, dU, regularity, stage, sphere rows, input gradients) and
+    //      interval units (continuity, fixed-s rows, h gradient, cost partial)
     void build_units() {
         units.clear();
         auto add = [&](int kind, int n, int k) {
@@ -326,16 +342,21 @@ struct Layout {
             units.push_back(k);
             units.push_back(0);
         };
-        add(UNIT_TAIL, 0, 0);
+        p.cls_off[0] = 0;
+        for (int t = 0; t < (int)(tail.size() / 4); ++t) add(UNIT_TAIL, t, 0);
+        p.cls_off[1] = (int32_t)(units.size() / 4);
         for (int n = 0; n < p.N; ++n)
             for (int k = 1; k < p.K1; ++k) {
                 const int32_t* sg = &seg[((size_t)(n * p.K1 + k) * NSEG) * 2];
                 if (sg[2 * SEG_ODE_A] >= 0) add(UNIT_ODE_A, n, k);
                 if (sg[2 * SEG_ODE_B] >= 0) add(UNIT_ODE_B, n, k);
             }
-        for (int n = 0; n < p.N; ++n)
+        p.cls_off[2] = (int32_t)(units.size() / 4);
+        for (int n = 0; n < p.N; ++n) {
+            add(UNIT_INTERVAL, n, 0);
             for (int k = 0; k < p.K1; ++k) add(UNIT_NODE, n, k);
-        for (int n = 0; n < p.N; ++n) add(UNIT_INTERVAL, n, 0);
+        }
+        p.cls_off[3] = (int32_t)(units.size() / 4);
     }
 
   private:
@@ -357,7 +378,7 @@ struct Layout {
     std::string node_segment(int kind, int n, int k) {
         SegPat sp;
         PatSink s{&sp};
-        run_node_seg<M, double>(p, kind, n, k, OnesW{}, s);
+        run_node_seg<M, double, 0>(p, kind, n, k, OnesW{}, s);
         if (!s.sorted) return "internal: unsorted columns in node segment " + std::to_string(kind);
         auto [r0, e0] = append(sp);
         const size_t slot = ((size_t)(n * p.K1 + k) * NSEG + kind) * 2;
@@ -370,7 +391,7 @@ struct Layout {
     std::string tail_segment(int kind, int index) {
         SegPat sp;
         PatSink s{&sp};
-        run_tail_seg<M, double>(p, kind, index, OnesW{}, s);
+        run_tail_seg<M, double, 0>(p, kind, index, OnesW{}, s);
         if (!s.sorted) return "internal: unsorted columns in tail segment " + std::to_string(kind);
         auto [r0, e0] = append(sp);
         tail.push_back(kind);

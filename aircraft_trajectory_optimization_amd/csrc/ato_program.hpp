@@ -63,7 +63,11 @@ struct ProbD {
     const int32_t* tail;       // [n_tail][4]   (kind, index, row0, nnz0)
     const int32_t* units;      // [n_units][4]  (UnitKind, n, k, 0)
     int32_t n_units, pad_units;
+    int32_t cls_off[4];        // unit classes [cls_off[c], cls_off[c+1]): tail, ODE, node/interval
 };
+
+// nodes per interval: compile-time KS (specialised kernels for common K) or runtime p.K1
+#define K1S(p) (KS ? KS : (p).K1)
 
 // first row of the second ODE group (drone: body-velocity rows; point mass: none)
 template <class M>
@@ -94,11 +98,12 @@ struct Cols {
 
 // -------------------------------------------------------------------------- collocation node
 // p_k = sum_j C[j][k] Z_j / h  (base_raceline.py:413-418): numerators for components [I0, I1)
-template <class M, class T, class W>
+template <class M, class T, int KS, class W>
 ATO_HD void poly_num(const ProbD& p, int n, int k, int I0, int I1, int uz, const W& w, T* P) {
-    const Cols<M> c{p.N, p.K1};
-    const int K1 = p.K1;
+    const Cols<M> c{p.N, K1S(p)};
+    const int K1 = K1S(p);
     for (int i = I0; i < I1; ++i) P[i - I0] = T(0);
+#pragma unroll
     for (int j = 0; j < K1; ++j) {
         const T cj = T(p.C[j * K1 + k]);
         const int base = uz ? c.u(n, j, 0) : c.z(n, j, 0);
@@ -107,27 +112,27 @@ ATO_HD void poly_num(const ProbD& p, int n, int k, int I0, int I1, int uz, const
 }
 
 // poly_ode[0] >= 0  (parametric; base_raceline.py:422-425)
-template <class M, class T, class W, class S>
+template <class M, class T, int KS, class W, class S>
 ATO_HD void seg_sdot(const ProbD& p, int n, int k, const W& w, S& s) {
-    const Cols<M> c{p.N, p.K1};
+    const Cols<M> c{p.N, K1S(p)};
     const T h = w(n), ih = T(1) / h;
     T P0;
-    poly_num<M, T>(p, n, k, 0, 1, 0, w, &P0);
+    poly_num<M, T, KS>(p, n, k, 0, 1, 0, w, &P0);
     s.jac(n, -P0 * ih * ih);
-    for (int j = 0; j < p.K1; ++j) s.jac(c.z(n, j, 0), T(p.C[j * p.K1 + k]) * ih);
+    for (int j = 0; j < K1S(p); ++j) s.jac(c.z(n, j, 0), T(p.C[j * K1S(p) + k]) * ih);
     s.row(P0 * ih, 0.0, ATO_INF);
 }
 
 // f_i(Z_k, U_k) - poly_ode_i = 0 for rows i in [R0, R1), k > 0  (base_raceline.py:427-430)
-template <class M, class T, int R0, int R1, class W, class S>
+template <class M, class T, int KS, int R0, int R1, class W, class S>
 ATO_HD void seg_ode(const ProbD& p, int n, int k, const W& w, S& s) {
     constexpr int NZ = M::NZ, NU = M::NU;
-    const Cols<M> c{p.N, p.K1};
-    const int K1 = p.K1;
+    const Cols<M> c{p.N, K1S(p)};
+    const int K1 = K1S(p);
     const T h = w(n);
     const T ih = T(1) / h, ih2 = ih * ih;
     T Pz[R1 - R0 > 0 ? R1 - R0 : 1];
-    poly_num<M, T>(p, n, k, R0, R1, 0, w, Pz);
+    poly_num<M, T, KS>(p, n, k, R0, R1, 0, w, Pz);
     T z[NZ], u[NU];
 #pragma unroll
     for (int i = 0; i < NZ; ++i) z[i] = w(c.z(n, k, i));
@@ -151,17 +156,18 @@ ATO_HD void seg_ode(const ProbD& p, int n, int k, const W& w, S& s) {
 }
 
 // dU - poly_du = 0  (base_raceline.py:432-434)
-template <class M, class T, class W, class S>
+template <class M, class T, int KS, class W, class S>
 ATO_HD void seg_du(const ProbD& p, int n, int k, const W& w, S& s) {
     constexpr int NU = M::NU;
-    const Cols<M> c{p.N, p.K1};
-    const int K1 = p.K1;
+    const Cols<M> c{p.N, K1S(p)};
+    const int K1 = K1S(p);
     const T h = w(n), ih = T(1) / h, ih2 = ih * ih;
     T Pu[NU];
-    poly_num<M, T>(p, n, k, 0, NU, 1, w, Pu);
+    poly_num<M, T, KS>(p, n, k, 0, NU, 1, w, Pu);
 #pragma unroll
     for (int i = 0; i < NU; ++i) {
         s.jac(n, Pu[i] * ih2);
+#pragma unroll
         for (int j = 0; j < K1; ++j) {
             s.jac(c.u(n, j, i), -T(p.C[j * K1 + k]) * ih);
             if (j == k) s.jac(c.du(n, k, i), T(1));
@@ -171,10 +177,10 @@ ATO_HD void seg_du(const ProbD& p, int n, int k, const W& w, S& s) {
 }
 
 // regularity: k_n y - k_y n <= gamma at nodes with k_y^2 + k_n^2 > 0.1 (base_raceline.py:1121-1129)
-template <class M, class T, class W, class S>
+template <class M, class T, int KS, class W, class S>
 ATO_HD void seg_reg(const ProbD& p, int n, int k, const W& w, S& s) {
-    const Cols<M> c{p.N, p.K1};
-    const double* gp = p.geom + (long)(n * p.K1 + k) * ATO_GEOM_WIDTH;
+    const Cols<M> c{p.N, K1S(p)};
+    const double* gp = p.geom + (long)(n * K1S(p) + k) * ATO_GEOM_WIDTH;
     const T ky = T(gp[10]), kn = T(gp[11]);
     s.jac(c.z(n, k, 1), kn);
     s.jac(c.z(n, k, 2), -ky);
@@ -182,9 +188,9 @@ ATO_HD void seg_reg(const ProbD& p, int n, int k, const W& w, S& s) {
 }
 
 // point-mass thrust ball u.u / T_max^2 <= 1  (point_model.py:122-129)
-template <class M, class T, class W, class S>
+template <class M, class T, int KS, class W, class S>
 ATO_HD void seg_stage(const ProbD& p, int n, int k, const W& w, S& s) {
-    const Cols<M> c{p.N, p.K1};
+    const Cols<M> c{p.N, K1S(p)};
     const T it2 = T(1) / (T(p.veh.Tmax) * T(p.veh.Tmax));
     T uu = T(0);
 #pragma unroll
@@ -197,10 +203,10 @@ ATO_HD void seg_stage(const ProbD& p, int n, int k, const W& w, S& s) {
 }
 
 // obstacle tube: (y - dy)^2 + (n - dn)^2 <= r_avail^2  (mesh_obstacle.py:219-237)
-template <class M, class T, class W, class S>
+template <class M, class T, int KS, class W, class S>
 ATO_HD void seg_sphere(const ProbD& p, int n, int k, const W& w, S& s) {
-    const Cols<M> c{p.N, p.K1};
-    const double* sp = p.spheres + (long)(n * p.K1 + k) * 3;
+    const Cols<M> c{p.N, K1S(p)};
+    const double* sp = p.spheres + (long)(n * K1S(p) + k) * 3;
     const T ey = w(c.z(n, k, 1)) - T(sp[0]);
     const T en = w(c.z(n, k, 2)) - T(sp[1]);
     s.jac(c.z(n, k, 1), T(2) * ey);
@@ -217,16 +223,17 @@ ATO_HD void qnormalize(const T* q, T* qh, T& inv_norm) {
 }
 
 // continuity into interval n >= 1 (base_raceline.py:474-490, parametric :1149-1163)
-template <class M, class T, class W, class S>
+template <class M, class T, int KS, class W, class S>
 ATO_HD void seg_cont(const ProbD& p, int n, const W& w, S& s) {
     constexpr int NZ = M::NZ, NU = M::NU, IR = M::IR;
-    const Cols<M> c{p.N, p.K1};
-    const int K1 = p.K1;
+    const Cols<M> c{p.N, K1S(p)};
+    const int K1 = K1S(p);
     T zb[NZ], ub[NU];
 #pragma unroll
     for (int i = 0; i < NZ; ++i) zb[i] = T(0);
 #pragma unroll
     for (int i = 0; i < NU; ++i) ub[i] = T(0);
+#pragma unroll
     for (int k = 0; k < K1; ++k) {
         const T dk = T(p.D[k]);
 #pragma unroll
@@ -241,6 +248,7 @@ ATO_HD void seg_cont(const ProbD& p, int n, const W& w, S& s) {
         const bool isq = M::HAS_QUAT && i >= IR && i < IR + 4;
         if (isq) {
             const int a = i - IR;
+#pragma unroll
             for (int k = 0; k < K1; ++k) {
                 const T dk = T(p.D[k]);
 #pragma unroll
@@ -264,13 +272,14 @@ ATO_HD void seg_cont(const ProbD& p, int n, const W& w, S& s) {
 }
 
 // fixed path length at both ends of interval n (base_raceline.py:1165-1181)
-template <class M, class T, class W, class S>
+template <class M, class T, int KS, class W, class S>
 ATO_HD void seg_srows(const ProbD& p, int n, const W& w, S& s) {
-    const Cols<M> c{p.N, p.K1};
+    const Cols<M> c{p.N, K1S(p)};
     s.jac(c.z(n, 0, 0), T(1));
     s.row(w(c.z(n, 0, 0)) - T(p.interval_s[n]), 0.0, 0.0);
     T zN = T(0);
-    for (int k = 0; k < p.K1; ++k) {
+#pragma unroll
+    for (int k = 0; k < K1S(p); ++k) {
         zN += w(c.z(n, k, 0)) * T(p.D[k]);
         s.jac(c.z(n, k, 0), T(p.D[k]));
     }
@@ -279,7 +288,7 @@ ATO_HD void seg_srows(const ProbD& p, int n, const W& w, S& s) {
 
 // -------------------------------------------------------------------------- tail segments
 // equal step sizes within each gate phase (base_raceline.py:891-905)
-template <class M, class T, class W, class S>
+template <class M, class T, int KS, class W, class S>
 ATO_HD void seg_heq(const ProbD& p, const W& w, S& s) {
     for (int n = 0; n < p.N; n += p.phase_len) {
         for (int n2 = n + 1; n2 < n + p.phase_len; ++n2) {
@@ -293,12 +302,12 @@ ATO_HD void seg_heq(const ProbD& p, const W& w, S& s) {
 // gate rows (base_raceline.py:545-595). Gate state x = xoff + E zc, zc = sum_k coef_k Z[n,k][comp]
 //   parametric: comps (y, n), E = [e_y e_n], xoff = x_c(s)   (:1028-1030)
 //   global:     comps (x1, x2, x3), E = I, xoff = 0          (:912)
-template <class M, class T, class W, class S>
+template <class M, class T, int KS, class W, class S>
 ATO_HD void seg_gate(const ProbD& p, int gi, const W& w, S& s) {
     const ato_gate& gt = p.gates[gi];
-    const Cols<M> c{p.N, p.K1};
+    const Cols<M> c{p.N, K1S(p)};
     const int n = gt.interval;
-    const int nk = gt.single_node ? 1 : p.K1;
+    const int nk = gt.single_node ? 1 : K1S(p);
     const int nc = M::PARAM ? 2 : 3;
     const int comp0 = M::PARAM ? 1 : 0;
     T E[3][3];
@@ -376,16 +385,17 @@ ATO_HD void seg_gate(const ProbD& p, int gi, const W& w, S& s) {
 // (base_raceline.py:322-348)
 
 // drone loop closure (drone_raceline.py:47-104), appended after gates
-template <class M, class T, class W, class S>
+template <class M, class T, int KS, class W, class S>
 ATO_HD void seg_drone_closure(const ProbD& p, const W& w, S& s) {
     constexpr int NZ = M::NZ, NU = M::NU, IR = M::IR, NR = M::NR;
-    const Cols<M> c{p.N, p.K1};
-    const int K1 = p.K1, nl = p.N - 1;
+    const Cols<M> c{p.N, K1S(p)};
+    const int K1 = K1S(p), nl = p.N - 1;
     T zb[NZ], ub[NU];
 #pragma unroll
     for (int i = 0; i < NZ; ++i) zb[i] = T(0);
 #pragma unroll
     for (int i = 0; i < NU; ++i) ub[i] = T(0);
+#pragma unroll
     for (int k = 0; k < K1; ++k) {
         const T dk = T(p.D[k]);
 #pragma unroll
@@ -417,6 +427,7 @@ ATO_HD void seg_drone_closure(const ProbD& p, const W& w, S& s) {
 #pragma unroll
         for (int a = 0; a < 4; ++a) {
             s.jac(c.z(0, 0, IR + a), sgn);
+#pragma unroll
             for (int k = 0; k < K1; ++k) {
                 const T dk = T(p.D[k]);
 #pragma unroll
@@ -434,16 +445,17 @@ ATO_HD void seg_drone_closure(const ProbD& p, const W& w, S& s) {
 }
 
 // base loop closure used by the point-mass racelines (base_raceline.py:492-514, :1183-1227)
-template <class M, class T, class W, class S>
+template <class M, class T, int KS, class W, class S>
 ATO_HD void seg_closure_base(const ProbD& p, const W& w, S& s) {
     constexpr int NZ = M::NZ, NU = M::NU;
-    const Cols<M> c{p.N, p.K1};
-    const int K1 = p.K1, nl = p.N - 1;
+    const Cols<M> c{p.N, K1S(p)};
+    const int K1 = K1S(p), nl = p.N - 1;
     T zb[NZ], ub[NU];
 #pragma unroll
     for (int i = 0; i < NZ; ++i) zb[i] = T(0);
 #pragma unroll
     for (int i = 0; i < NU; ++i) ub[i] = T(0);
+#pragma unroll
     for (int k = 0; k < K1; ++k) {
         const T dk = T(p.D[k]);
 #pragma unroll
@@ -483,10 +495,10 @@ ATO_HD void seg_closure_base(const ProbD& p, const W& w, S& s) {
 // -------------------------------------------------------------------------- cost
 // J = sum_{n,k} h_n B_k (u'Ru + du'dR du + 1)   (base_raceline.py:601-623)
 // stage cost at node (n, k) and its input / input-rate gradient (without the h_n B_k factor)
-template <class M, class T, class W>
+template <class M, class T, int KS, class W>
 ATO_HD T stage_cost(const ProbD& p, int n, int k, const W& w, T* gu, T* gdu) {
     constexpr int NU = M::NU;
-    const Cols<M> c{p.N, p.K1};
+    const Cols<M> c{p.N, K1S(p)};
     T u[NU], du[NU];
 #pragma unroll
     for (int i = 0; i < NU; ++i) {

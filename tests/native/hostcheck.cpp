@@ -28,6 +28,7 @@ struct HostSink {
         if (g) g[r] = gv;
         r += ge;
     }
+    void finish() {}
 };
 
 template <class T>
@@ -93,7 +94,7 @@ int atoh_eval(const atoh_handle* h, int B, const double* w, double* g, double* J
             const ato::GradOut<double> go{gf + (long)b * p.nw, 1, fpart.data(), 1};
             for (int u = 0; u < p.n_units; ++u) {
                 const int32_t* ut = p.units + 4 * u;
-                ato::run_unit<M, double, true, true>(p, ut[0], ut[1], ut[2], W, s, go);
+                ato::run_unit<M, double, 0, true, true>(p, ut[0], ut[1], ut[2], W, s, go);
             }
             f[b] = ato::reduce_cost(fpart.data(), 1, p.N);
         }

@@ -59,17 +59,19 @@ def _racetrack(B, seed=5):
     return spec, nlp, W, rng
 
 
-def test_full_size_racetrack_batch():
-    ''' 50 x 4 x 13 racetrack, B = 130 (two full 64-lane chunks + a partial one) '''
-    spec, nlp, W, rng = _racetrack(130)
-    bn = _batched(spec, 130)
+@pytest.mark.parametrize('B', [130, 128, 2, 1])
+def test_full_size_racetrack_batch(B):
+    ''' 50 x 4 x 13 racetrack. B = 128: full 64-lane chunks (paired 16-byte stores); 130: a
+    partial last chunk; 2: one partial chunk; 1: odd batch (one-entry-per-store path) '''
+    spec, nlp, W, rng = _racetrack(B)
+    bn = _batched(spec, B)
     bn.set_w(W)
     bn.evaluate()
     g, J, f, gf = bn.results()
     go = nlp.g(W.T)                        # oracle vectorised over the batch: (ng, B)
     _close(g, go.T)
     _close(f, nlp.f(W.T))
-    for b in (0, 63, 64, 129):
+    for b in sorted({0, min(63, B - 1), min(64, B - 1), B - 1}):
         V = rng.standard_normal((bn.sizes[0], 2))
         Jv = np.stack([np.add.reduceat(J[b] * V[bn.col, j], bn.row_ptr[:-1]) for j in range(2)], axis=1)
         _close(Jv, nlp.jvp(W[b], V), 1e-11)
