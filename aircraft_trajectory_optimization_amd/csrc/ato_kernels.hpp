@@ -37,6 +37,8 @@ struct DevSink {
         if (WG) g[r] = gv;
         r += ge;
     }
+    __device__ __forceinline__ void skip() { e += je; }
+    __device__ __forceinline__ void row_skip() { r += ge; }
     __device__ __forceinline__ void finish() {}
 };
 
@@ -114,6 +116,12 @@ struct DevSinkPaired {
         if (WG && (FULL || svalid)) *reinterpret_cast<T*>(gr + self_off) = gv;
         gr += Bb;
     }
+    // an entry another work unit writes: the pending entry (if any) is stored alone
+    __device__ __forceinline__ void skip() {
+        flush();
+        Jr += Bb;
+    }
+    __device__ __forceinline__ void row_skip() { gr += Bb; }
 };
 
 // decision-vector reads for the paired kernel: uniform row base + 32-bit lane byte offset
@@ -136,7 +144,7 @@ struct DevW {
 
 constexpr int WAVE = 64;
 
-template <class M, class T, int KS, bool WJ, bool WG, bool WF>
+template <class M, class T, int KS, bool WJ, bool WG, bool WF, int UMASK>
 __global__ __launch_bounds__(WAVE) void k_eval(ProbD p, int B, int layout, const T* __restrict__ w,
                                                T* __restrict__ g, T* __restrict__ J,
                                                T* __restrict__ gf, T* __restrict__ fpart) {
@@ -162,7 +170,7 @@ __global__ __launch_bounds__(WAVE) void k_eval(ProbD p, int B, int layout, const
     const DevW<T> W{wb, st};
     DevSink<T, WJ, WG> s{Jb, gb, st, st, 0, 0};
     const GradOut<T> go{gfb, st, WF ? fpart + b : nullptr, B};
-    run_unit<M, T, KS, WJ || WG, WF>(p, ut[0], ut[1], ut[2], W, s, go);
+    run_unit<M, T, KS, WJ || WG, WF, UMASK>(p, ut[0], ut[1], ut[2], W, s, go);
 }
 
 // Interleaved layout, even B: every lane stays active (permlane swaps need the whole wave);
@@ -226,20 +234,23 @@ hipError_t launch_eval(const ProbD& p, int B, int layout, const T* w, T* g, T* J
     // occupancy to one wave per SIMD.)
     const bool paired = layout == ATO_LAYOUT_INTERLEAVED && (B % WAVE) == 0 && wg;
     if (ev) (void)hipEventRecord(ev[0], st);
-    if (paired) {
+    // Collocation and RK4 problems get separate instantiations so neither pays the other's
+    // register allocation (the RK4 dual-number step vs the collocation ODE units).
+    auto launch = [&]<int UM>() {
         const dim3 grid(chunks, p.n_units);
-        if (wj && wg && wf)
-            hipLaunchKernelGGL((k_eval_paired<M, T, 0, true, true, true, true, UMASK_ALL>), grid, block, 0, st, p, B, 0, w, g, J, gf, fpart);
-        else if (wj && wg)
-            hipLaunchKernelGGL((k_eval_paired<M, T, 0, true, true, false, true, UMASK_ALL>), grid, block, 0, st, p, B, 0, w, g, J, gf, fpart);
-        else if (wg && wf)
-            hipLaunchKernelGGL((k_eval_paired<M, T, 0, false, true, true, true, UMASK_ALL>), grid, block, 0, st, p, B, 0, w, g, J, gf, fpart);
-        else
-            hipLaunchKernelGGL((k_eval_paired<M, T, 0, false, true, false, true, UMASK_ALL>), grid, block, 0, st, p, B, 0, w, g, J, gf, fpart);
-    } else {
-        const dim3 grid(chunks, p.n_units);
+        if (paired) {
+            if (wj && wg && wf)
+                hipLaunchKernelGGL((k_eval_paired<M, T, 0, true, true, true, true, UM>), grid, block, 0, st, p, B, 0, w, g, J, gf, fpart);
+            else if (wj && wg)
+                hipLaunchKernelGGL((k_eval_paired<M, T, 0, true, true, false, true, UM>), grid, block, 0, st, p, B, 0, w, g, J, gf, fpart);
+            else if (wg && wf)
+                hipLaunchKernelGGL((k_eval_paired<M, T, 0, false, true, true, true, UM>), grid, block, 0, st, p, B, 0, w, g, J, gf, fpart);
+            else
+                hipLaunchKernelGGL((k_eval_paired<M, T, 0, false, true, false, true, UM>), grid, block, 0, st, p, B, 0, w, g, J, gf, fpart);
+            return;
+        }
         auto go = [&]<bool WJ, bool WG, bool WF>() {
-            hipLaunchKernelGGL((k_eval<M, T, 0, WJ, WG, WF>), grid, block, 0, st, p, B, layout, w, g, J, gf, fpart);
+            hipLaunchKernelGGL((k_eval<M, T, 0, WJ, WG, WF, UM>), grid, block, 0, st, p, B, layout, w, g, J, gf, fpart);
         };
         if (wj && wg && wf) go.template operator()<true, true, true>();
         else if (wj && wg) go.template operator()<true, true, false>();
@@ -248,7 +259,9 @@ hipError_t launch_eval(const ProbD& p, int B, int layout, const T* w, T* g, T* J
         else if (wj && wf) go.template operator()<true, false, true>();
         else if (wj) go.template operator()<true, false, false>();
         else if (wf) go.template operator()<false, false, true>();
-    }
+    };
+    if (p.trans == ATO_TRANS_RK4) launch.template operator()<UMASK_RK4>();
+    else launch.template operator()<UMASK_COLLOC>();
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (ev) (void)hipEventRecord(ev[1], st);

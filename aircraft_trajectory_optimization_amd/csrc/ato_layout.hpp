@@ -45,8 +45,14 @@ struct PatSink {
         cur = 0;
         last = -1;
     }
+    // value-mode only (RK4 column groups); never reached in pattern mode
+    void skip() { sorted = false; }
+    void row_skip() { sorted = false; }
     void finish() {}
 };
+
+template <>
+struct SinkTraits<PatSink> { static constexpr bool pattern = true; };
 
 struct OnesW {
     double operator()(int) const { return 1.0; }
@@ -73,9 +79,10 @@ bool with_model(const ProbD& p, F&& f) {
     return false;
 }
 
-// Run one segment of the given kind with any sink / accessor.
-template <class M, class T, int KS, class W, class S>
-ATO_HD void run_node_seg(const ProbD& p, int kind, int n, int k, const W& w, S& s) {
+// Run one segment of the given kind with any sink / accessor. grp: RK4 Jacobian column group.
+// RK4 = false leaves the RK4 programs out of an instantiation (collocation kernels).
+template <class M, class T, int KS, class W, class S, bool RK4 = true>
+ATO_HD void run_node_seg(const ProbD& p, int kind, int n, int k, const W& w, S& s, int grp = 0) {
     switch (kind) {
         case SEG_SDOT: seg_sdot<M, T, KS>(p, n, k, w, s); break;
         case SEG_ODE_A: seg_ode<M, T, KS, 0, ode_split<M>()>(p, n, k, w, s); break;
@@ -88,19 +95,39 @@ ATO_HD void run_node_seg(const ProbD& p, int kind, int n, int k, const W& w, S& 
         case SEG_SPHERE: seg_sphere<M, T, KS>(p, n, k, w, s); break;
         case SEG_CONT: seg_cont<M, T, KS>(p, n, w, s); break;
         case SEG_SROWS: seg_srows<M, T, KS>(p, n, w, s); break;
+        case SEG_RK4S: seg_rk4s<M, T, KS>(p, n, w, s); break;
+        case SEG_RK4:
+            if constexpr (RK4) seg_rk4<M, T, KS>(p, n, grp, w, s);
+            break;
         default: break;
     }
 }
 
-template <class M, class T, int KS, class W, class S>
-ATO_HD void run_tail_seg(const ProbD& p, int kind, int index, const W& w, S& s) {
+template <class M, class T, int KS, class W, class S, bool RK4 = true>
+ATO_HD void run_tail_seg(const ProbD& p, int kind, int index, const W& w, S& s, int grp = 0) {
+    const bool rk4 = RK4 && p.trans == ATO_TRANS_RK4;
     switch (kind) {
         case TAIL_HEQ: seg_heq<M, T, KS>(p, w, s); break;
-        case TAIL_CLOSURE_BASE: seg_closure_base<M, T, KS>(p, w, s); break;
+        case TAIL_CLOSURE_BASE:
+            if constexpr (RK4)
+                if (rk4) { seg_closure_base_rk4<M, T, KS>(p, grp, w, s); break; }
+            seg_closure_base<M, T, KS>(p, w, s);
+            break;
         case TAIL_GATE: seg_gate<M, T, KS>(p, index, w, s); break;
-        case TAIL_DRONE_CLOSURE: seg_drone_closure<M, T, KS>(p, w, s); break;
+        case TAIL_DRONE_CLOSURE:
+            if constexpr (RK4)
+                if (rk4) { seg_drone_closure_rk4<M, T, KS>(p, grp, w, s); break; }
+            seg_drone_closure<M, T, KS>(p, w, s);
+            break;
         default: break;
     }
+}
+
+// number of work units of a tail segment (RK4 closures: one per Jacobian column group)
+template <class M>
+int tail_units(const ProbD& p, int kind) {
+    const bool closure = kind == TAIL_CLOSURE_BASE || kind == TAIL_DRONE_CLOSURE;
+    return (closure && p.trans == ATO_TRANS_RK4) ? rk4_groups<M>() : 1;
 }
 
 // where an instance's gradient / cost go (pointers already offset to the instance)
@@ -132,19 +159,23 @@ ATO_HD T reduce_cost(const T* fpart, long pst, int N) {
 // call this, so the dispatch is identical.
 // UMASK: unit kinds compiled into this instantiation (bit = 1 << UnitKind), so a kernel that
 // only runs light units is not register-allocated for the heavy ones.
-constexpr int UMASK_ALL = 0x1f;
 constexpr int UMASK_TAIL = 1 << UNIT_TAIL;
 constexpr int UMASK_ODE = (1 << UNIT_ODE_A) | (1 << UNIT_ODE_B);
 constexpr int UMASK_LIN = (1 << UNIT_NODE) | (1 << UNIT_INTERVAL);
+constexpr int UMASK_RK4U = 1 << UNIT_RK4;
+constexpr int UMASK_COLLOC = UMASK_TAIL | UMASK_ODE | UMASK_LIN;    // collocation problems
+constexpr int UMASK_RK4 = UMASK_TAIL | UMASK_LIN | UMASK_RK4U;      // RK4 problems
+constexpr int UMASK_ALL = UMASK_COLLOC | UMASK_RK4;
 
 template <class M, class T, int KS, bool ROWS, bool GRAD, int UMASK = UMASK_ALL, class W, class S>
 ATO_HD void run_unit(const ProbD& p, int kind, int n, int k, const W& w, S& s, const GradOut<T>& go) {
     constexpr int NZ = M::NZ, NU = M::NU;
-    const int32_t* sg = p.seg + (long)(n * K1S(p) + k) * NSEG * 2;
+    constexpr bool RK4 = (UMASK & UMASK_RK4U) != 0;
+    const int32_t* sg = p.seg + (long)(n * K1S(p) + (kind == UNIT_RK4 ? 0 : k)) * NSEG * 2;
     auto seg = [&](int sk) {
         if (sg[2 * sk] < 0) return;
         s.begin(sg[2 * sk], sg[2 * sk + 1]);
-        run_node_seg<M, T, KS>(p, sk, n, k, w, s);
+        run_node_seg<M, T, KS, W, S, RK4>(p, sk, n, k, w, s, k);
     };
     switch (kind) {
         case UNIT_TAIL:   // one tail segment: n = its index in p.tail
@@ -152,7 +183,7 @@ ATO_HD void run_unit(const ProbD& p, int kind, int n, int k, const W& w, S& s, c
                 if (ROWS) {
                     const int32_t* tl = p.tail + 4 * n;
                     s.begin(tl[2], tl[3]);
-                    run_tail_seg<M, T, KS>(p, tl[0], tl[1], w, s);
+                    run_tail_seg<M, T, KS, W, S, RK4>(p, tl[0], tl[1], w, s, k);
                 }
             }
             break;
@@ -172,6 +203,7 @@ ATO_HD void run_unit(const ProbD& p, int kind, int n, int k, const W& w, S& s, c
                 seg(SEG_REG);
                 seg(SEG_STAGE);
                 seg(SEG_SPHERE);
+                seg(SEG_RK4S);
             }
             if (GRAD) {
                 const Cols<M> c{p.N, K1S(p)};
@@ -200,6 +232,10 @@ ATO_HD void run_unit(const ProbD& p, int kind, int n, int k, const W& w, S& s, c
                 go.gf[(long)n * go.st] = acc;
                 go.fpart[(long)n * go.pst] = w(n) * acc;
             }
+            break;
+        case UNIT_RK4:   // k = Jacobian column group
+            if constexpr (RK4)
+                if (ROWS) seg(SEG_RK4);
             break;
         default:
             break;
@@ -233,8 +269,13 @@ struct Layout {
     std::string build(const ato_problem_desc& d) {
         if (d.abi_version != ATO_ABI_VERSION) return "abi_version mismatch";
         if (d.N < 1) return "N must be >= 1";
-        if (d.transcription != ATO_TRANS_COLLOCATION) return "RK4 transcription not supported by this build";
-        if (d.K < 1 || d.K > ATO_KMAX) return "K out of range [1, ATO_KMAX]";
+        if (d.transcription == ATO_TRANS_RK4) {
+            if (d.K != 0) return "RK4 transcription needs K = 0 (one node per interval)";
+        } else if (d.transcription == ATO_TRANS_COLLOCATION) {
+            if (d.K < 1 || d.K > ATO_KMAX) return "K out of range [1, ATO_KMAX]";
+        } else {
+            return "unknown transcription";
+        }
         if (d.closed && d.N < 2) return "closed problems need N >= 2";
         if (!d.closed) return "open (non-periodic) racelines are not supported by this build";
         std::memset(&p, 0, sizeof(p));
@@ -306,6 +347,10 @@ struct Layout {
         for (const ato_gate& g : gates) {
             if (g.interval < 0 || g.interval >= p.N) return "gate interval out of range";
             if (g.shape != ATO_GATE_CIRCLE && g.shape != ATO_GATE_SQUARE) return "bad gate shape";
+            if (g.n_coef < 1 || g.n_coef > ATO_KMAX + 1 || g.interval * p.K1 + g.n_coef > p.P)
+                return "gate n_coef out of range";
+            if (d.transcription == ATO_TRANS_RK4 && g.at_end)
+                return "RK4 gate at the end of the horizon is not supported by this build";
         }
         spheres.clear();
         if (d.has_spheres) spheres.assign(d.spheres, d.spheres + (size_t)p.P * 3);
@@ -343,7 +388,11 @@ struct Layout {
             units.push_back(0);
         };
         p.cls_off[0] = 0;
-        for (int t = 0; t < (int)(tail.size() / 4); ++t) add(UNIT_TAIL, t, 0);
+        for (int t = 0; t < (int)(tail.size() / 4); ++t) {
+            int nu_t = 1;
+            with_model(p, [&]<class M>() { nu_t = tail_units<M>(p, tail[4 * t]); });
+            for (int g = 0; g < nu_t; ++g) add(UNIT_TAIL, t, g);
+        }
         p.cls_off[1] = (int32_t)(units.size() / 4);
         for (int n = 0; n < p.N; ++n)
             for (int k = 1; k < p.K1; ++k) {
@@ -351,6 +400,13 @@ struct Layout {
                 if (sg[2 * SEG_ODE_A] >= 0) add(UNIT_ODE_A, n, k);
                 if (sg[2 * SEG_ODE_B] >= 0) add(UNIT_ODE_B, n, k);
             }
+        for (int n = 0; n < p.N; ++n) {
+            const int32_t* sg = &seg[((size_t)(n * p.K1) * NSEG) * 2];
+            if (sg[2 * SEG_RK4] < 0) continue;
+            int ng_ = 1;
+            with_model(p, [&]<class M>() { ng_ = rk4_groups<M>(); });
+            for (int g = 0; g < ng_; ++g) add(UNIT_RK4, n, g);
+        }
         p.cls_off[2] = (int32_t)(units.size() / 4);
         for (int n = 0; n < p.N; ++n) {
             add(UNIT_INTERVAL, n, 0);
@@ -409,6 +465,15 @@ struct Layout {
         if (p.phase_len > 0) ATO_TRY(tail_segment<M>(TAIL_HEQ, 0));
         const bool param = M::PARAM;
         for (int n = 0; n < p.N; ++n) {
+            if (p.trans == ATO_TRANS_RK4) {   // base_raceline.py:363-391 / :1052-1112
+                if (param) ATO_TRY(node_segment<M>(SEG_RK4S, n, 0));
+                if (n == p.N - 1) continue;
+                ATO_TRY(node_segment<M>(SEG_RK4, n, 0));
+                if (!M::IS_DRONE) ATO_TRY(node_segment<M>(SEG_STAGE, n, 0));
+                if (param && p.force_reg && geom[(size_t)n * ATO_GEOM_WIDTH + 13] != 0.0)
+                    ATO_TRY(node_segment<M>(SEG_REG, n, 0));
+                continue;
+            }
             for (int k = 0; k < p.K1; ++k) {
                 if (param) ATO_TRY(node_segment<M>(SEG_SDOT, n, k));
                 if (k > 0) {

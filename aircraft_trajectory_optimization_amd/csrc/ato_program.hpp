@@ -23,6 +23,7 @@
 //   cost                                          :601-623
 #pragma once
 #include "ato_models.hpp"
+#include "ato_dual.hpp"
 #include "../../include/ato.h"
 
 namespace ato {
@@ -30,15 +31,30 @@ namespace ato {
 // Row segments of node (n, k) in reference order: s-dot row, ODE rows (two groups), dU rows;
 // then per interval: regularity rows, stage rows, continuity, fixed-s rows.
 enum SegKind { SEG_SDOT = 0, SEG_ODE_A, SEG_ODE_B, SEG_DU, SEG_REG, SEG_STAGE, SEG_SPHERE, SEG_CONT,
-               SEG_SROWS, NSEG };
+               SEG_SROWS, SEG_RK4S, SEG_RK4, NSEG };
 enum TailKind { TAIL_HEQ = 0, TAIL_CLOSURE_BASE, TAIL_INITIAL, TAIL_TERMINAL, TAIL_GATE,
                 TAIL_DRONE_CLOSURE };
 // Work units of the evaluation kernel (one per grid.y index; see ato_layout.hpp)
-//   UNIT_TAIL      equal-h rows, gates, closure, f
+//   UNIT_TAIL      one tail segment (equal-h rows, a gate, the closure); for RK4 closures one
+//                  unit per column group of the step Jacobian
 //   UNIT_ODE_A/B   ODE defect rows [0, SPLIT) / [SPLIT, NZ) of node (n, k > 0)
-//   UNIT_NODE      s-dot, dU, regularity, stage and sphere rows of node (n, k); grad f of its inputs
+//   UNIT_NODE      s-dot, dU, regularity, stage, sphere and RK4 s rows of node (n, k); grad f of its inputs
 //   UNIT_INTERVAL  continuity and fixed-s rows of interval n; d f / d h_n
-enum UnitKind { UNIT_TAIL = 0, UNIT_ODE_A, UNIT_ODE_B, UNIT_NODE, UNIT_INTERVAL };
+//   UNIT_RK4       RK4 step rows of interval n, Jacobian column group k
+enum UnitKind { UNIT_TAIL = 0, UNIT_ODE_A, UNIT_ODE_B, UNIT_NODE, UNIT_INTERVAL, UNIT_RK4 };
+
+// Jacobian columns of one RK4 step Phi(z_n, u_n, h_n) handled by one work unit. The local
+// columns are numbered h = 0, z_m = 1 + m, u_j = 1 + NZ + j; group g covers [g RK4_CG, (g+1) RK4_CG).
+#ifndef ATO_RK4_CG
+#define ATO_RK4_CG 3
+#endif
+constexpr int RK4_CG = ATO_RK4_CG;
+template <class M>
+constexpr int rk4_groups() { return (1 + M::NZ + M::NU + RK4_CG - 1) / RK4_CG; }
+
+// sinks that only record the sparsity pattern (no values, sequential entries)
+template <class S>
+struct SinkTraits { static constexpr bool pattern = false; };
 
 #ifndef ATO_INF
 #define ATO_INF (__builtin_huge_val())
@@ -307,7 +323,7 @@ ATO_HD void seg_gate(const ProbD& p, int gi, const W& w, S& s) {
     const ato_gate& gt = p.gates[gi];
     const Cols<M> c{p.N, K1S(p)};
     const int n = gt.interval;
-    const int nk = gt.single_node ? 1 : K1S(p);
+    const int nk = gt.n_coef;
     const int nc = M::PARAM ? 2 : 3;
     const int comp0 = M::PARAM ? 1 : 0;
     T E[3][3];
@@ -322,7 +338,7 @@ ATO_HD void seg_gate(const ProbD& p, int gi, const W& w, S& s) {
     }
     T zc[3] = {T(0), T(0), T(0)};
     for (int k = 0; k < nk; ++k) {
-        const T ck = gt.single_node ? T(1) : T(gt.coef[k]);
+        const T ck = T(gt.coef[k]);
         for (int q = 0; q < nc; ++q) zc[q] += w(c.z(n, k, comp0 + q)) * ck;
     }
     T x[3], dx[3];
@@ -334,7 +350,7 @@ ATO_HD void seg_gate(const ProbD& p, int gi, const W& w, S& s) {
     // emit one row whose value is linear or quadratic in zc:  dval/dzc given
     auto emit_row = [&](const T* dzc, T val, double lb, double ub) {
         for (int k = 0; k < nk; ++k) {
-            const T ck = gt.single_node ? T(1) : T(gt.coef[k]);
+            const T ck = T(gt.coef[k]);
             for (int q = 0; q < nc; ++q) s.jac(c.z(n, k, comp0 + q), ck * dzc[q]);
         }
         s.row(val, lb, ub);
@@ -488,6 +504,284 @@ ATO_HD void seg_closure_base(const ProbD& p, const W& w, S& s) {
             s.jac(c.z(0, 0, i), T(1));
             for (int k = 0; k < K1; ++k) s.jac(c.z(nl, k, i), -T(p.D[k]));
             s.row(w(c.z(0, 0, i)) - zb[i], 0.0, 0.0);
+        }
+    }
+}
+
+// -------------------------------------------------------------------------- RK4 transcription
+// Multiple shooting with one fixed RK4 step per interval (use_rk4; base_raceline.py:363-391
+// global, :1052-1112 parametric with the geometry frozen at s_n, dynamics_model.py:91-114):
+//   Phi(z, u, h) = z + h/6 (k1 + 2 k2 + 2 k3 + k4),  k_i = f(z + c_i h k_{i-1}, u), c = (0, 1/2, 1/2, 1)
+// The Jacobian of Phi is obtained exactly by forward-mode dual numbers through the model's value
+// path, RK4_CG columns per work unit.
+
+// structural dependencies of Phi_i (dep) and of op(Phi)_i (dop): bit m < NZ = z_m, bit NZ + j = u_j;
+// every row also depends on h
+template <class M>
+struct RK4Dep {
+    static constexpr int NZ = M::NZ, NU = M::NU;
+    uint32_t dep[NZ] = {}, dop[NZ] = {};
+    constexpr RK4Dep() {
+        uint32_t ub[NZ] = {}, kd[NZ] = {}, acc[NZ] = {};
+        for (int i = 0; i < NZ; ++i) {
+            for (int j = 0; j < NU; ++j)
+                if (M::umask(i, j)) ub[i] |= 1u << (NZ + j);
+            for (int m = 0; m < NZ; ++m)
+                if (M::zmask(i, m)) kd[i] |= 1u << m;
+            kd[i] |= ub[i];
+            acc[i] = kd[i];
+        }
+        for (int st = 1; st < 4; ++st) {
+            uint32_t zs[NZ] = {}, kn[NZ] = {};
+            for (int m = 0; m < NZ; ++m) zs[m] = (1u << m) | kd[m];
+            for (int i = 0; i < NZ; ++i) {
+                kn[i] = ub[i];
+                for (int m = 0; m < NZ; ++m)
+                    if (M::zmask(i, m)) kn[i] |= zs[m];
+                acc[i] |= kn[i];
+            }
+            for (int i = 0; i < NZ; ++i) kd[i] = kn[i];
+        }
+        for (int i = 0; i < NZ; ++i) dep[i] = dop[i] = (1u << i) | acc[i];
+        if (M::HAS_QUAT) {
+            uint32_t q = 0;
+            for (int a = 0; a < 4; ++a) q |= dep[M::IR + a];
+            for (int a = 0; a < 4; ++a) dop[M::IR + a] = q;
+        }
+    }
+};
+
+// Phi of interval n (op applied to the quaternion if OP) with tangents along local columns
+// [grp RK4_CG, (grp + 1) RK4_CG)
+template <class M, class T, bool OP, class W>
+ATO_HD void rk4_phi(const ProbD& p, int n, int grp, const W& w, Dual<T, RK4_CG>* phi) {
+    using D = Dual<T, RK4_CG>;
+    constexpr int NZ = M::NZ, NU = M::NU;
+    const Cols<M> c{p.N, 1};
+    const int l0 = grp * RK4_CG;
+    auto ld = [&](int col, int lid) {
+        const int dir = lid - l0;
+        return D::seed(w(col), (dir >= 0 && dir < RK4_CG) ? dir : -1);
+    };
+    const D h = ld(n, 0);
+    D z[NZ], u[NU];
+#pragma unroll
+    for (int m = 0; m < NZ; ++m) z[m] = ld(c.z(n, 0, m), 1 + m);
+#pragma unroll
+    for (int j = 0; j < NU; ++j) u[j] = ld(c.u(n, 0, j), 1 + NZ + j);
+    const NodeGeom<D> G = load_geom<D>(p, n);
+    D k[NZ], acc[NZ], zs[NZ];
+#pragma unroll
+    for (int i = 0; i < NZ; ++i) {
+        k[i] = D(0.0);
+        acc[i] = D(0.0);
+    }
+    const D hh = h / 2.0;
+    // one model instance in a rolled loop over the 4 stages (unrolling it keeps all stages'
+    // temporaries live and spills)
+#pragma unroll 1
+    for (int st = 0; st < 4; ++st) {
+        const D cs = st == 0 ? D(0.0) : (st == 3 ? h : hh);
+#pragma unroll
+        for (int i = 0; i < NZ; ++i) zs[i] = z[i] + cs * k[i];
+        M::template rows<0, NZ>(zs, u, G, p.veh, [&](int i, D fi, const D*, const D*) { k[i] = fi; });
+        const double wt = (st == 0 || st == 3) ? 1.0 : 2.0;
+#pragma unroll
+        for (int i = 0; i < NZ; ++i) acc[i] += k[i] * wt;
+    }
+    const D h6 = h / 6.0;
+#pragma unroll
+    for (int i = 0; i < NZ; ++i) phi[i] = z[i] + h6 * acc[i];
+    if (OP && M::HAS_QUAT) {
+        D qh[4], iq;
+        qnormalize(phi + M::IR, qh, iq);
+#pragma unroll
+        for (int a = 0; a < 4; ++a) phi[M::IR + a] = qh[a];
+    }
+}
+
+// Writes the entries of one RK4-dependent row for work-unit group grp:
+//   lin(col, v)   an entry that does not come from Phi (written by group 0)
+//   dh(sgn)       sgn dPhi_i/dh        dzu(sgn)  sgn dPhi_i/d(z_n, u_n) in mask order
+//   row(g, lb, ub) closes the row (g written by group 0)
+// In pattern mode (SinkTraits<S>::pattern) every entry is emitted without values.
+template <class M, class T, class S>
+struct RK4Row {
+    using D = Dual<T, RK4_CG>;
+    static constexpr bool PAT = SinkTraits<S>::pattern;
+    S& s;
+    int grp, n, l0;
+    const Cols<M>& c;
+    ATO_HD bool mine(int lid) const { return lid >= l0 && lid < l0 + RK4_CG; }
+    // tangent j of x without a dynamic register-array index
+    ATO_HD static T pick(const D& x, int j) {
+        T r = x.d[0];
+#pragma unroll
+        for (int q = 1; q < RK4_CG; ++q)
+            if (j == q) r = x.d[q];
+        return r;
+    }
+    ATO_HD void lin(int col, T v) {
+        if (PAT || grp == 0) s.jac(col, v);
+        else s.skip();
+    }
+    ATO_HD void dh(const D& x, T sgn) {
+        if (PAT) s.jac(n, T(0));
+        else if (mine(0)) s.jac(n, sgn * pick(x, 0 - l0));
+        else s.skip();
+    }
+    ATO_HD void dzu(const D& x, uint32_t mask, T sgn) {
+        constexpr int NZ = M::NZ, NU = M::NU;
+#pragma unroll
+        for (int m = 0; m < NZ + NU; ++m) {
+            if (!(mask & (1u << m))) continue;
+            const int col = m < NZ ? c.z(n, 0, m) : c.u(n, 0, m - NZ);
+            if (PAT) s.jac(col, T(0));
+            else if (mine(1 + m)) s.jac(col, sgn * pick(x, 1 + m - l0));
+            else s.skip();
+        }
+    }
+    ATO_HD void row(T g, double lb, double ub) {
+        if (PAT || grp == 0) s.row(g, lb, ub);
+        else s.row_skip();
+    }
+};
+
+// s rows of RK4 interval n: Z[n,0][0] = s_n (parametric, every interval; base_raceline.py:1059-1063)
+template <class M, class T, int KS, class W, class S>
+ATO_HD void seg_rk4s(const ProbD& p, int n, const W& w, S& s) {
+    const Cols<M> c{p.N, 1};
+    s.jac(c.z(n, 0, 0), T(1));
+    s.row(w(c.z(n, 0, 0)) - T(p.interval_s[n]), 0.0, 0.0);
+}
+
+// step rows of RK4 interval n < N-1 (base_raceline.py:379-386 global, :1079-1097 parametric):
+//   Z[n+1][i] - op(Phi)_i (i >= 1 parametric), U[n+1] - (U_n + dU_n h/2) (F10),
+//   Phi_0 - s_{n+1} (parametric)
+template <class M, class T, int KS, class W, class S>
+ATO_HD void seg_rk4(const ProbD& p, int n, int grp, const W& w, S& s) {
+    using D = Dual<T, RK4_CG>;
+    constexpr int NZ = M::NZ, NU = M::NU;
+    constexpr RK4Dep<M> dp{};
+    const Cols<M> c{p.N, 1};
+    D phi[NZ];
+    if constexpr (!SinkTraits<S>::pattern) rk4_phi<M, T, true>(p, n, grp, w, phi);
+    RK4Row<M, T, S> r{s, grp, n, grp * RK4_CG, c};
+#pragma unroll
+    for (int i = (M::PARAM ? 1 : 0); i < NZ; ++i) {
+        r.dh(phi[i], T(-1));
+        r.dzu(phi[i], dp.dop[i], T(-1));
+        r.lin(c.z(n + 1, 0, i), T(1));
+        r.row(w(c.z(n + 1, 0, i)) - phi[i].v, 0.0, 0.0);
+    }
+    const T h = w(n);
+#pragma unroll
+    for (int i = 0; i < NU; ++i) {
+        const T dui = w(c.du(n, 0, i));
+        r.lin(n, -dui / T(2));
+        r.lin(c.u(n, 0, i), T(-1));
+        r.lin(c.du(n, 0, i), -h / T(2));
+        r.lin(c.u(n + 1, 0, i), T(1));
+        r.row(w(c.u(n + 1, 0, i)) - w(c.u(n, 0, i)) - dui * h / T(2), 0.0, 0.0);
+    }
+    if (M::PARAM) {
+        // s at the end of the step is Phi_0 itself (no continuity operator on s)
+        r.dh(phi[0], T(1));
+        r.dzu(phi[0], dp.dep[0], T(1));
+        r.row(phi[0].v - T(p.interval_s[n + 1]), 0.0, 0.0);
+    }
+}
+
+// drone loop closure with zF = op(Phi(Z[N-1])), uF = U[N-1] + dU[N-1] h (base_raceline.py:322-348,
+// :1034-1050; drone_raceline.py:47-104)
+template <class M, class T, int KS, class W, class S>
+ATO_HD void seg_drone_closure_rk4(const ProbD& p, int grp, const W& w, S& s) {
+    using D = Dual<T, RK4_CG>;
+    constexpr int NZ = M::NZ, NU = M::NU, IR = M::IR;
+    constexpr RK4Dep<M> dp{};
+    const Cols<M> c{p.N, 1};
+    const int nl = p.N - 1;
+    D phi[NZ];
+    if constexpr (!SinkTraits<S>::pattern) rk4_phi<M, T, true>(p, nl, grp, w, phi);
+    RK4Row<M, T, S> r{s, grp, nl, grp * RK4_CG, c};
+    const T h = w(nl);
+#pragma unroll
+    for (int i = 0; i < NU; ++i) {
+        const T dui = w(c.du(nl, 0, i));
+        r.lin(nl, dui);
+        r.lin(c.u(0, 0, i), T(-1));
+        r.lin(c.u(nl, 0, i), T(1));
+        r.lin(c.du(nl, 0, i), h);
+        r.row(w(c.u(nl, 0, i)) + dui * h - w(c.u(0, 0, i)), 0.0, 0.0);
+    }
+    auto plain = [&](int i, T offset) {
+        r.dh(phi[i], T(1));
+        r.lin(c.z(0, 0, i), T(-1));
+        r.dzu(phi[i], dp.dop[i], T(1));
+        r.row(phi[i].v - w(c.z(0, 0, i)) - offset, 0.0, 0.0);
+    };
+    plain(1, T(0));
+    plain(2, T(0));
+    const int first_after = M::HAS_QUAT ? IR + 4 : IR + 1;
+    for (int i = first_after; i < NZ; ++i) plain(i, T(0));
+    if (M::HAS_QUAT) {
+        const T sgn = p.quat_flip ? T(1) : T(-1);
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+            r.dh(phi[IR + a], T(1));
+            r.lin(c.z(0, 0, IR + a), sgn);
+            r.dzu(phi[IR + a], dp.dop[IR + a], T(1));
+            r.row(phi[IR + a].v + sgn * w(c.z(0, 0, IR + a)), 0.0, 0.0);
+        }
+    } else {
+        plain(IR, T(6.283185307179586 * p.euler_wraps));
+    }
+    if (!M::PARAM) plain(0, T(0));
+}
+
+// point-mass loop closure with the RK4 end state (base_raceline.py:492-514, :1183-1227)
+template <class M, class T, int KS, class W, class S>
+ATO_HD void seg_closure_base_rk4(const ProbD& p, int grp, const W& w, S& s) {
+    using D = Dual<T, RK4_CG>;
+    constexpr int NZ = M::NZ, NU = M::NU;
+    constexpr RK4Dep<M> dp{};
+    const Cols<M> c{p.N, 1};
+    const int nl = p.N - 1;
+    D phi[NZ];
+    if constexpr (!SinkTraits<S>::pattern) rk4_phi<M, T, true>(p, nl, grp, w, phi);
+    RK4Row<M, T, S> r{s, grp, nl, grp * RK4_CG, c};
+    const T h = w(nl);
+#pragma unroll
+    for (int i = 0; i < NU; ++i) {
+        const T dui = w(c.du(nl, 0, i));
+        r.lin(nl, dui);
+        r.lin(c.u(0, 0, i), T(-1));
+        r.lin(c.u(nl, 0, i), T(1));
+        r.lin(c.du(nl, 0, i), h);
+        r.row(w(c.u(nl, 0, i)) + dui * h - w(c.u(0, 0, i)), 0.0, 0.0);
+    }
+    if (!M::PARAM || p.cleanly_closed) {
+        for (int i = M::PARAM ? 1 : 0; i < NZ; ++i) {
+            r.dh(phi[i], T(1));
+            r.lin(c.z(0, 0, i), T(-1));
+            r.dzu(phi[i], dp.dop[i], T(1));
+            r.row(phi[i].v - w(c.z(0, 0, i)), 0.0, 0.0);
+        }
+    } else {
+        // A z0[1:3] - zF[1:3] ; z0[3:] - zF[3:]
+        for (int q = 0; q < 2; ++q) {
+            r.dh(phi[1 + q], T(-1));
+            r.lin(c.z(0, 0, 1), T(p.A_skew[q * 2 + 0]));
+            r.lin(c.z(0, 0, 2), T(p.A_skew[q * 2 + 1]));
+            r.dzu(phi[1 + q], dp.dop[1 + q], T(-1));
+            r.row(T(p.A_skew[q * 2]) * w(c.z(0, 0, 1)) + T(p.A_skew[q * 2 + 1]) * w(c.z(0, 0, 2)) - phi[1 + q].v,
+                  0.0, 0.0);
+        }
+        for (int i = 3; i < NZ; ++i) {
+            r.dh(phi[i], T(-1));
+            r.lin(c.z(0, 0, i), T(1));
+            r.dzu(phi[i], dp.dop[i], T(-1));
+            r.row(w(c.z(0, 0, i)) - phi[i].v, 0.0, 0.0);
         }
     }
 }

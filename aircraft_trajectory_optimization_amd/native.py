@@ -19,7 +19,7 @@ ATO_FRAME_GLOBAL, ATO_FRAME_PARAMETRIC = 0, 1
 ATO_TRANS_COLLOCATION, ATO_TRANS_RK4 = 0, 1
 ATO_GATE_CIRCLE, ATO_GATE_SQUARE = 0, 1
 ATO_LAYOUT_INTERLEAVED, ATO_LAYOUT_INSTANCE_MAJOR = 0, 1
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 _c_double_p = ctypes.POINTER(ctypes.c_double)
 
@@ -32,7 +32,7 @@ class AtoGate(ctypes.Structure):
         ('fix_center', ctypes.c_int32),
         ('axial', ctypes.c_int32),
         ('at_end', ctypes.c_int32),
-        ('single_node', ctypes.c_int32),
+        ('n_coef', ctypes.c_int32),
         ('coef', ctypes.c_double * (KMAX + 1)),
         ('gate_x', ctypes.c_double * 3),
         ('R', ctypes.c_double * 9),
@@ -198,7 +198,7 @@ class DescHolder:
         garr = (AtoGate * max(len(gates), 1))()
         for i, gspec in enumerate(gates):
             g = garr[i]
-            for key in ('interval', 'shape', 'fix_center', 'axial', 'at_end', 'single_node'):
+            for key in ('interval', 'shape', 'fix_center', 'axial', 'at_end', 'n_coef'):
                 setattr(g, key, int(gspec[key]))
             g.coef = _carr(ctypes.c_double, gspec['coef'], KMAX + 1)
             g.gate_x = _carr(ctypes.c_double, gspec['gate_x'], 3)

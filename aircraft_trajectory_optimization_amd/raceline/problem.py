@@ -66,11 +66,11 @@ class ProblemSpec:
         self.nv = self.nz + 2 * self.nu
 
         # ---- config mutations the reference performs during setup
-        if config.use_rk4:
+        self.rk4 = bool(config.use_rk4)
+        if self.rk4:
             config.h0 /= config.K
             config.N *= config.K
             config.K = 0
-            raise NotImplementedError('RK4 transcription is not implemented by this build yet')
         if self.param and not line.cleanly_closed and self.is_drone and not vehicle.global_r:
             raise NotImplementedError('Global orientation must be used for skewly closed centerlines')
         self.phase_len = 0
@@ -90,7 +90,11 @@ class ProblemSpec:
         self.K1 = self.K + 1
         self.P = self.N * self.K1
         self.nw = self.N + self.P * self.nv
-        self.tau, self.B, self.C, self.D = get_collocation_coefficients(self.K)
+        if self.rk4:
+            # one node per interval; the stage cost is weighted by h_n alone (base_raceline.py:610-611)
+            self.tau, self.B, self.C, self.D = np.zeros(1), np.ones(1), np.zeros((1, 1)), np.ones(1)
+        else:
+            self.tau, self.B, self.C, self.D = get_collocation_coefficients(self.K)
 
         # ---- node s and geometry (parametric)
         self.node_s = np.array([self.get_s(n, k) for n in range(self.N) for k in range(self.K1)])
@@ -137,8 +141,8 @@ class ProblemSpec:
         if not self.param:
             for gate_no, n in enumerate(range(0, self.N, self.phase_len)):
                 g = self._gate_common(gate_no)
-                g.update({'interval': n, 'axial': 1, 'at_end': 0, 'single_node': 1,
-                          'coef': np.zeros(self.K1), 'xc': np.zeros(3), 'ey': np.zeros(3), 'en': np.zeros(3)})
+                g.update({'interval': n, 'axial': 1, 'at_end': 0, 'n_coef': 1,
+                          'coef': np.ones(1), 'xc': np.zeros(3), 'ey': np.zeros(3), 'en': np.zeros(3)})
                 gates.append(g)
             if not self.config.closed:
                 raise NotImplementedError('open global racelines are not implemented by this build')
@@ -163,13 +167,21 @@ class ProblemSpec:
                     raise TypeError('Gate is after end')
             g = self._gate_common(s)
             if n == self.N:
-                g.update({'interval': self.N - 1, 'at_end': 1, 'coef': self.D.copy()})
+                if self.rk4:
+                    raise NotImplementedError('RK4 gate at the end of the horizon is not supported by this build')
+                g.update({'interval': self.N - 1, 'at_end': 1, 'n_coef': self.K1, 'coef': self.D.copy()})
             else:
                 sf = self.get_s(n + 1, 0)
                 d = (s - s0) / (sf - s0)
-                g.update({'interval': n, 'at_end': 0,
-                          'coef': get_intermediate_collocation_coefficients(self.K, d)})
-            g.update({'axial': 0, 'single_node': 0, 'xc': self.line.p2xc(s), 'ey': self.line.p2ey(s),
+                if self.rk4:
+                    # Z[n] + d (Z[n+1] - Z[n])  (base_raceline.py:1018-1019)
+                    if n + 1 >= self.N:
+                        raise IndexError('RK4 gate in the last interval needs Z[N] (as in the reference)')
+                    g.update({'interval': n, 'at_end': 0, 'n_coef': 2, 'coef': np.array([1 - d, d])})
+                else:
+                    g.update({'interval': n, 'at_end': 0, 'n_coef': self.K1,
+                              'coef': get_intermediate_collocation_coefficients(self.K, d)})
+            g.update({'axial': 0, 'xc': self.line.p2xc(s), 'ey': self.line.p2ey(s),
                       'en': self.line.p2en(s)})
             gates.append(g)
         return gates
@@ -210,7 +222,7 @@ class ProblemSpec:
                 v = self.config.v0 * self.line.p2es(s)
                 z[3], z[4], z[5] = v
         else:
-            gate_no = (n + k / self.K) / self.phase_len
+            gate_no = n / self.phase_len if self.rk4 else (n + k / self.K) / self.phase_len
             xg = self.line.p2xc(gate_no)
             vg = self.line.p2es(gate_no)
             vg = vg / np.linalg.norm(vg) * self.config.v0
@@ -268,7 +280,7 @@ class ProblemSpec:
             'attitude': native.ATO_ATT_ESP if (self.is_drone and v.use_quat) else native.ATO_ATT_YPR,
             'frame': native.ATO_FRAME_PARAMETRIC if self.param else native.ATO_FRAME_GLOBAL,
             'global_r': int(bool(v.global_r)),
-            'transcription': native.ATO_TRANS_COLLOCATION,
+            'transcription': native.ATO_TRANS_RK4 if self.rk4 else native.ATO_TRANS_COLLOCATION,
             'N': self.N, 'K': self.K, 'closed': int(bool(self.config.closed)),
             'cleanly_closed': int(bool(self.line.cleanly_closed)),
             'quat_flip': int(self.quat_flip),

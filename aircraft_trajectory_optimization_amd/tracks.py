@@ -36,15 +36,15 @@ def make_line(track: str) -> SplineCenterline:
 
 
 def make_spec(track='race', model='drone', frame='parametric', N=50, K=4, use_quat=True, global_r=True,
-              fix_gate_center=False, quat_flip=False, spheres=None, v0=1.0, h0=1) -> ProblemSpec:
+              fix_gate_center=False, quat_flip=False, spheres=None, v0=1.0, h0=1, rk4=False) -> ProblemSpec:
     ''' ProblemSpec of a scenario the way solve_util configures it (utils/solve_util.py:29-75) '''
     line = make_line(track)
     if frame == 'parametric':
-        cfg = ParametricRacelineConfig(verbose=False, N=N, K=K, v0=v0, h0=h0)
+        cfg = ParametricRacelineConfig(verbose=False, N=N, K=K, v0=v0, h0=h0, use_rk4=rk4)
         cfg.closed = line.config.closed
         cfg.fixed_gates = line.config.s[:-1]
     else:
-        cfg = GlobalRacelineConfig(verbose=False, N=N, K=K, v0=v0, h0=h0)
+        cfg = GlobalRacelineConfig(verbose=False, N=N, K=K, v0=v0, h0=h0, use_rk4=rk4)
         cfg.closed = line.config.closed
         cfg.gate_xi, cfg.gate_xj, cfg.gate_xk = line.config.x
     cfg.fix_gate_center = fix_gate_center

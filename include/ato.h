@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define ATO_ABI_VERSION 1
+#define ATO_ABI_VERSION 2
 #define ATO_KMAX 9            /* highest collocation degree supported */
 #define ATO_GEOM_WIDTH 16     /* doubles per node in the geometry table */
 
@@ -60,7 +60,9 @@ typedef struct ato_gate {
     int32_t fix_center;   /* 1: x - gate_x == 0 (3 rows)                         */
     int32_t axial;        /* 1: axial equality row (global frame)                */
     int32_t at_end;       /* 1: state is z_F of the last interval                */
-    int32_t single_node;  /* 1: state is Z[interval, 0] itself (global frame)   */
+    int32_t n_coef;       /* weights in coef, on the consecutive nodes starting at   *
+                           * node (interval, 0): K+1 (collocation), 1 (global frame:  *
+                           * Z[interval, 0] itself), 2 (RK4: Z[n], Z[n+1] interpolated)*/
     double coef[ATO_KMAX + 1];  /* Lagrange weights l_k(d) on Z[interval, k]     */
     double gate_x[3];     /* gate centre                                          */
     double R[9];          /* gate orientation (row-major, columns e1 e2 e3)       */

@@ -15,6 +15,8 @@ hand-written Jacobians.
   gates                                base_raceline.py:545-595, :891-918, :986-1032
   obstacle spheres                     obstacles/mesh_obstacle.py:219-237
   cost                                 base_raceline.py:601-623
+  RK4 transcription (use_rk4)          base_raceline.py:226-230, :322-348, :363-391, :1034-1112;
+                                       dynamics_model.py:91-114
 '''
 import numpy as np
 
@@ -37,7 +39,7 @@ class RefNLP:
 
     def __init__(self, line, model, frame, N, K, veh=None, closed=True, fix_gate_center=False,
                  R=1e-7, dR=1e-7, h0=1, v0=1, fixed_gates=None, force_regularity=True,
-                 quat_flip=False, euler_wraps=0.0, spheres=None):
+                 quat_flip=False, euler_wraps=0.0, spheres=None, rk4=False):
         self.line, self.model, self.frame = line, model, frame
         base = dict(DRONE_DEFAULTS if model == 'drone' else POINT_DEFAULTS)
         base.update(veh or {})
@@ -55,6 +57,12 @@ class RefNLP:
         self.quat_flip, self.euler_wraps, self.spheres = quat_flip, euler_wraps, spheres
         self.Rm = np.eye(self.nu) * R if np.isscalar(R) else np.asarray(R)
         self.dRm = np.eye(self.nu) * dR if np.isscalar(dR) else np.asarray(dR)
+        # BaseRaceline._setup_checks (base_raceline.py:226-230), run first by the global override
+        self.rk4 = bool(rk4)
+        if self.rk4:
+            self.h0 = h0 = h0 / K
+            N = N * K
+            K = 0
         # BaseGlobalRaceline._setup_checks (base_raceline.py:873-885)
         if frame == 'global':
             x = np.array(line.x)
@@ -64,7 +72,10 @@ class RefNLP:
             N = int(phases * np.ceil(N / phases))
             self.gate_n_interval = int(N / phases)
         self.N, self.K = N, K
-        self.tau, self.B, self.C, self.D = coefficients(K)
+        if self.rk4:
+            self.tau, self.B, self.C, self.D = np.zeros(1), np.ones(1), np.zeros((1, 1)), np.ones(1)
+        else:
+            self.tau, self.B, self.C, self.D = coefficients(K)
         self.nw = N + N * (K + 1) * self.nv
         self._geo_cache = {}
         self.lbg, self.ubg = None, None
@@ -93,6 +104,15 @@ class RefNLP:
         return ref_models.point_zdot(z, u, self.veh, self.frame, self.global_r,
                                      self.geo(s) if self.frame == 'parametric' else None)
 
+    def rk4_step(self, z, u, h, s):
+        ''' one RK4 step with u held and geometry frozen at s (dynamics_model.py:91-114,
+        base_raceline.py:1071-1077) '''
+        k1 = self.f_ode(z, u, s)
+        k2 = self.f_ode(z + h / 2 * k1, u, s)
+        k3 = self.f_ode(z + h / 2 * k2, u, s)
+        k4 = self.f_ode(z + h * k3, u, s)
+        return z + h / 6 * (k1 + k2 * 2 + k3 * 2 + k4)
+
     def continuity_op(self, z):
         ''' drone_raceline.py:42-45 '''
         if self.model == 'drone' and self.use_quat:
@@ -120,7 +140,7 @@ class RefNLP:
                 v = self.v0 * self.geo(self.get_s(n, k))['es']
                 z[3], z[4], z[5] = v
         else:
-            gate_no = (n + k / self.K) / self.gate_n_interval
+            gate_no = n / self.gate_n_interval if self.rk4 else (n + k / self.K) / self.gate_n_interval
             xg = self.geo(gate_no)['xc']
             vg = self.geo(gate_no)['es']
             vg = vg / np.linalg.norm(vg) * self.v0
@@ -196,6 +216,29 @@ class RefNLP:
                 for n2 in range(n + 1, n + gi):
                     add(H[n2] - H[n], 0., 0.)
         for n in range(N):
+            if self.rk4:
+                # _enforce_rk4_interval (base_raceline.py:363-391 global, :1052-1112 parametric)
+                if param:
+                    add(Z[n][0][0] - self.get_s(n, 0), 0., 0.)
+                if n == N - 1:
+                    continue
+                zn = self.continuity_op(self.rk4_step(Z[n][0], U[n][0], H[n], self.get_s(n, 0)))
+                un = U[n][0] + dU[n][0] * H[n] / 2
+                if param:
+                    add(Z[n + 1][0][1:] - zn[1:], 0., 0.)
+                    add(U[n + 1][0] - un, 0., 0.)
+                    add(zn[0] - self.get_s(n + 1, 0), 0., 0.)
+                else:
+                    add(Z[n + 1][0] - zn, 0., 0.)
+                    add(U[n + 1][0] - un, 0., 0.)
+                if self.model == 'point':
+                    u_mag = sum(U[n][0][i] * U[n][0][i] for i in range(nu))
+                    add(u_mag / self.veh['T_max'] / self.veh['T_max'], -inf, 1)
+                if param and self.force_regularity:
+                    gk = self.geo(self.get_s(n, 0))
+                    if gk['ky'] ** 2 + gk['kn'] ** 2 > 0.1:
+                        add(gk['kn'] * Z[n][0][1] - gk['ky'] * Z[n][0][2], -inf, self.line.gamma)
+                continue
             # _enforce_collocation_interval_ode
             for k in range(K + 1):
                 poly_ode = 0
@@ -241,12 +284,16 @@ class RefNLP:
                 add(zN[0] - self.get_s(n + 1, 0), 0., 0.)
 
         def zF():
+            if self.rk4:    # base_raceline.py:324-330, :1034-1050
+                return self.continuity_op(self.rk4_step(Z[-1][0], U[-1][0], H[-1], self.get_s(N - 1, 0)))
             acc = 0
             for k in range(K + 1):
                 acc = acc + Z[-1][k] * D[k]
             return self.continuity_op(acc)
 
         def uF():
+            if self.rk4:    # full step, unlike the interval rows (F10; base_raceline.py:340-341)
+                return U[-1][0] + dU[-1][0] * H[-1]
             acc = 0
             for k in range(K + 1):
                 acc = acc + U[-1][k] * D[k]
@@ -283,10 +330,13 @@ class RefNLP:
                 else:
                     sf = self.get_s(n + 1, 0)
                     d = (s - s0) / (sf - s0)
-                    Dd = intermediate(K, d)
-                    z_gate = 0
-                    for k in range(K + 1):
-                        z_gate = z_gate + Z[n][k] * Dd[k]
+                    if self.rk4:
+                        z_gate = Z[n][0] + d * (Z[n + 1][0] - Z[n][0])
+                    else:
+                        Dd = intermediate(K, d)
+                        z_gate = 0
+                        for k in range(K + 1):
+                            z_gate = z_gate + Z[n][k] * Dd[k]
                 gs = self.geo(s)
                 x_gate = gs['xc'][:, None] + z_gate[1] * gs['ey'][:, None] + z_gate[2] * gs['en'][:, None]
                 self._fix_gate(add, x_gate, s, False)

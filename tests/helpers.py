@@ -22,13 +22,13 @@ def oracle_line(track):
 
 
 def oracle_nlp(track='race', model='drone', frame='parametric', N=50, K=4, use_quat=True, global_r=True,
-               fix_gate_center=False, quat_flip=False, spheres=None, v0=1.0, h0=1):
+               fix_gate_center=False, quat_flip=False, spheres=None, v0=1.0, h0=1, rk4=False):
     from oracle.ref_transcription import RefNLP
     line = oracle_line(track)
     veh = {'use_quat': use_quat, 'global_r': global_r} if model == 'drone' else {'global_r': global_r}
     fixed = line.s[:-1] if frame == 'parametric' else None
     return RefNLP(line, model, frame, N, K, veh=veh, fix_gate_center=fix_gate_center, fixed_gates=fixed,
-                  quat_flip=quat_flip, spheres=spheres, v0=v0, h0=h0)
+                  quat_flip=quat_flip, spheres=spheres, v0=v0, h0=h0, rk4=rk4)
 
 
 def random_w(spec_or_nlp, rng, scale=0.05):
@@ -54,7 +54,7 @@ HOSTCHECK_LIB = os.path.join(REPO, 'tests', 'native', 'libato_hostcheck.so')
 
 def build_hostcheck(force=False):
     srcs = [HOSTCHECK_SRC] + [os.path.join(REPO, 'aircraft_trajectory_optimization_amd', 'csrc', f)
-                              for f in ('ato_models.hpp', 'ato_program.hpp', 'ato_layout.hpp')]
+                              for f in ('ato_models.hpp', 'ato_dual.hpp', 'ato_program.hpp', 'ato_layout.hpp')]
     if not force and os.path.exists(HOSTCHECK_LIB) and \
             os.path.getmtime(HOSTCHECK_LIB) >= max(os.path.getmtime(s) for s in srcs):
         return HOSTCHECK_LIB

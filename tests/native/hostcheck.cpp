@@ -28,6 +28,8 @@ struct HostSink {
         if (g) g[r] = gv;
         r += ge;
     }
+    void skip() { e += je; }
+    void row_skip() { r += ge; }
     void finish() {}
 };
 

@@ -120,3 +120,27 @@ def test_fp32_tracks_fp64():
     for x, y in zip(rs, rd):
         tol = 2e-4 * max(1.0, float(np.abs(y).max()))
         assert np.abs(x - y).max() <= tol
+
+
+@pytest.mark.parametrize('frame', ['parametric', 'global'])
+def test_race_script_rk4(frame):
+    ''' scripts/race.py's transcription: use_rk4 with N = 70, K = 7 -> 490 RK4 steps (F4).
+    B = 128 runs the paired-store kernel with the dual-number step units. '''
+    cfg = dict(track='race', frame=frame, N=70, K=7, rk4=True)
+    rng = np.random.default_rng(17)
+    spec = product_spec(**cfg)
+    nlp = oracle_nlp(**cfg)
+    B = 128
+    W = np.stack([random_w(nlp, rng, scale=0.02) for _ in range(B)])
+    bn = _batched(spec, B)
+    assert bn.sizes[:2] == (nlp.nw, nlp.ng)
+    bn.set_w(W)
+    bn.evaluate()
+    g, J, f, gf = bn.results()
+    _close(g, nlp.g(W.T).T)
+    _close(f, nlp.f(W.T))
+    for b in (0, 77, 127):
+        V = rng.standard_normal((bn.sizes[0], 2))
+        Jv = np.stack([np.add.reduceat(J[b] * V[bn.col, j], bn.row_ptr[:-1]) for j in range(2)], axis=1)
+        _close(Jv, nlp.jvp(W[b], V), 1e-11)
+        _close(gf[b], nlp.grad_f(W[b]))

@@ -21,6 +21,13 @@ for _track in ('race', 'fig8'):
 VARIANTS.append(dict(track='race', fix_gate_center=True, N=4, K=3))
 VARIANTS.append(dict(track='fig8', quat_flip=True, N=4, K=3))
 VARIANTS.append(dict(track='fig8', N=3, K=7))
+# RK4 multiple shooting (use_rk4; scripts/race.py): N x K steps of one node each
+for _model, _frame, _quat, _gr in [('drone', 'parametric', True, True), ('drone', 'parametric', False, True),
+                                   ('drone', 'parametric', True, False), ('drone', 'global', True, True),
+                                   ('drone', 'global', False, True), ('point', 'parametric', False, True),
+                                   ('point', 'global', False, True)]:
+    VARIANTS.append(dict(track='race', model=_model, frame=_frame, use_quat=_quat, global_r=_gr, N=7, K=2, rk4=True))
+VARIANTS.append(dict(track='fig8', N=8, K=2, rk4=True, quat_flip=True))
 
 
 def _id(c):
