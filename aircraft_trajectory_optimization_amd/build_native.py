@@ -2,7 +2,8 @@
 Build libato.so for gfx950 in-tree (aircraft_trajectory_optimization_amd/_lib/).
 
 One object per model variant (ato_inst.hip, -DATO_INST=i) plus the C-ABI object, compiled
-in parallel with hipcc, then linked into a shared library. Objects are rebuilt only when
+in parallel with hipcc, and the host-only Hessian structure analysis (ato_hstruct.cpp, g++),
+then linked into a shared library. Objects are rebuilt only when
 a source or header is newer.
 '''
 import glob
@@ -33,11 +34,17 @@ def _stale(target, sources):
     return any(os.path.getmtime(s) > t for s in sources)
 
 
+HOST_FLAGS = ['-std=c++20', '-O2', '-fPIC', '-I', os.path.join(REPO, 'include')]
+
+
 def _compile(job):
     src, obj, extra = job
     if not _stale(obj, [src] + _deps()):
         return obj, 'cached'
-    cmd = ['hipcc', *FLAGS, *extra, '-c', src, '-o', obj]
+    if src.endswith('.cpp'):      # host-only translation unit
+        cmd = ['g++', *HOST_FLAGS, *extra, '-c', src, '-o', obj]
+    else:
+        cmd = ['hipcc', *FLAGS, *extra, '-c', src, '-o', obj]
     res = subprocess.run(cmd, capture_output=True, text=True, check=False)
     if res.returncode != 0:
         raise RuntimeError(f'hipcc failed for {os.path.basename(src)}:\n{res.stderr}')
@@ -47,7 +54,8 @@ def _compile(job):
 def build(verbose=True, jobs=None) -> str:
     ''' compile and link; returns the library path '''
     os.makedirs(OBJ, exist_ok=True)
-    work = [(os.path.join(CSRC, 'ato_capi.hip'), os.path.join(OBJ, 'ato_capi.o'), [])]
+    work = [(os.path.join(CSRC, 'ato_capi.hip'), os.path.join(OBJ, 'ato_capi.o'), []),
+            (os.path.join(CSRC, 'ato_hstruct.cpp'), os.path.join(OBJ, 'ato_hstruct.o'), [])]
     for i in range(N_INST):
         work.append((os.path.join(CSRC, 'ato_inst.hip'), os.path.join(OBJ, f'ato_inst{i}.o'), [f'-DATO_INST={i}']))
     jobs = jobs or min(len(work), max(1, min(8, os.cpu_count() or 4)))

@@ -5,6 +5,7 @@
 #include <new>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include "ato_kernels.hpp"
 
 #include "ato_handle.hpp"
@@ -42,6 +43,9 @@ static void release(ato_handle* h) {
     (void)hipFree(h->d_tail);
     (void)hipFree(h->d_units);
     (void)hipFree(h->d_fpart);
+    for (int32_t* d : {h->d_color, h->d_take_e, h->d_take_r, h->d_csc_ptr, h->d_csc_ent, h->d_csc_row}) (void)hipFree(d);
+    (void)hipFree(h->d_dJ);
+    (void)hipFree(h->d_dgf);
     for (hipEvent_t e : h->events) (void)hipEventDestroy(e);
     h->events.clear();
 }
@@ -50,7 +54,7 @@ extern "C" {
 
 const char* ato_last_error(void) { return g_last_error.c_str(); }
 
-const char* ato_version(void) { return "ato 1 gfx950"; }
+const char* ato_version(void) { return "ato 2 gfx950"; }
 
 int ato_create(const ato_problem_desc* desc, ato_handle** out) {
     if (!desc || !out) return fail(ATO_ERR_ARG, "null argument");
@@ -140,8 +144,24 @@ int ato_bounds(const ato_handle* h, double* lbg, double* ubg) {
     return ATO_OK;
 }
 
+static int hess_reserve(ato_handle* h, int32_t max_batch) {
+    if (max_batch <= h->hess_reserved) return ATO_OK;
+    (void)hipFree(h->d_dJ);
+    (void)hipFree(h->d_dgf);
+    h->d_dJ = h->d_dgf = nullptr;
+    h->hess_reserved = 0;
+    ATO_HIP(hipMalloc(&h->d_dJ, (size_t)std::max(h->L.p.nnz, 1) * max_batch * sizeof(double)));
+    ATO_HIP(hipMalloc(&h->d_dgf, (size_t)h->L.p.nw * max_batch * sizeof(double)));
+    h->hess_reserved = max_batch;
+    return ATO_OK;
+}
+
 int ato_reserve(ato_handle* h, int32_t max_batch) {
     if (!h || max_batch < 1) return fail(ATO_ERR_ARG, "bad reserve arguments");
+    if (h->hess_ready) {
+        int rc = hess_reserve(h, max_batch);
+        if (rc) return rc;
+    }
     if (max_batch <= h->reserved) return ATO_OK;
     if (h->d_fpart) ATO_HIP(hipFree(h->d_fpart));
     h->d_fpart = nullptr;
@@ -207,6 +227,53 @@ extern "C" int ato_timing_read(ato_handle* h, double* eval_ms, double* reduce_ms
     if (eval_ms) *eval_ms = se;
     if (reduce_ms) *reduce_ms = sr;
     if (calls) *calls = h->timed_calls;
+    return ATO_OK;
+}
+
+// Hessian structure, colouring and recovery tables (host analysis + upload), once per handle
+static int ensure_hess(ato_handle* h) {
+    if (h->hess_ready) return ATO_OK;
+    std::string err = h->HL.build(h->L);
+    if (!err.empty()) return fail(ATO_ERR_UNSUPPORTED, err);
+    int rc;
+    if ((rc = upload(h->HL.color, &h->d_color)) || (rc = upload(h->HL.take_e, &h->d_take_e)) ||
+        (rc = upload(h->HL.take_r, &h->d_take_r)) || (rc = upload(h->HL.csc_ptr, &h->d_csc_ptr)) ||
+        (rc = upload(h->HL.csc_ent, &h->d_csc_ent)) || (rc = upload(h->HL.csc_row, &h->d_csc_row)))
+        return rc;
+    h->hess_ready = true;
+    return ATO_OK;
+}
+
+extern "C" int ato_hess_sparsity(ato_handle* h, int32_t* nnz, const int32_t** row_ptr, const int32_t** col,
+                                 int32_t* n_colors) {
+    if (!h) return fail(ATO_ERR_ARG, "null handle");
+    int rc = ensure_hess(h);
+    if (rc) return rc;
+    if (nnz) *nnz = h->HL.nnz();
+    if (row_ptr) *row_ptr = h->HL.row_ptr.data();
+    if (col) *col = h->HL.col.data();
+    if (n_colors) *n_colors = h->HL.n_colors;
+    return ATO_OK;
+}
+
+extern "C" int ato_hess_eval(ato_handle* h, int32_t batch, int32_t layout, const double* w, const double* lam,
+                             const double* sigma, double* hess, void* stream) {
+    if (!h) return fail(ATO_ERR_ARG, "null handle");
+    if (batch < 1) return fail(ATO_ERR_ARG, "batch must be >= 1");
+    if (layout != ATO_LAYOUT_INTERLEAVED && layout != ATO_LAYOUT_INSTANCE_MAJOR)
+        return fail(ATO_ERR_ARG, "unknown layout");
+    if (!w || !lam || !sigma || !hess) return fail(ATO_ERR_ARG, "null buffer");
+    int rc = ensure_hess(h);
+    if (rc) return rc;
+    if ((rc = hess_reserve(h, batch))) return rc;
+    const ato::HessDev hd{h->d_color, h->d_take_e, h->d_take_r, h->d_csc_ptr, h->d_csc_ent, h->d_csc_row,
+                          h->HL.take_off.data(), h->HL.n_colors, h->HL.nnz()};
+    hipError_t e = hipSuccess;
+    ato::with_model(h->pd, [&]<class M>() {
+        e = ato::launch_hess<M>(h->pd, hd, batch, layout, w, lam, sigma, hess, h->d_dJ, h->d_dgf,
+                                (hipStream_t)stream);
+    });
+    if (e != hipSuccess) return fail(ATO_ERR_HIP, std::string("hessian launch: ") + hipGetErrorString(e));
     return ATO_OK;
 }
 

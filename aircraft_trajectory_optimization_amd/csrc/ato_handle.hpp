@@ -20,4 +20,12 @@ struct ato_handle {
     int32_t reserved = 0;
     std::vector<hipEvent_t> events;   // 3 per timed call
     int32_t timed_calls = 0;
+    // Hessian of the Lagrangian (built on first use)
+    bool hess_ready = false;
+    ato::HessLayout HL;
+    int32_t *d_color = nullptr, *d_take_e = nullptr, *d_take_r = nullptr;
+    int32_t *d_csc_ptr = nullptr, *d_csc_ent = nullptr, *d_csc_row = nullptr;
+    double* d_dJ = nullptr;     // [nnz][hess_reserved] Jacobian tangents of one colour
+    double* d_dgf = nullptr;    // [nw][hess_reserved] grad f tangents of one colour
+    int32_t hess_reserved = 0;
 };

@@ -14,8 +14,10 @@
 //   of every interval (which also write the interval's cost partial). k_cost_reduce then
 //   sums the partials into f in a fixed order.
 #pragma once
+#include <vector>
 #include <hip/hip_runtime.h>
 #include "ato_layout.hpp"
+#include "ato_hessian.hpp"
 
 namespace ato {
 
@@ -213,6 +215,74 @@ __global__ __launch_bounds__(256) void k_cost_reduce(int N, int B, const T* __re
     f[b] = reduce_cost(fpart + b, (long)B, N);
 }
 
+// ------------------------------------------------------------------ Hessian of the Lagrangian
+// Tangents of the Jacobian entries of a seeded pass (see ato_hessian.hpp); g rows are ignored.
+template <class T>
+struct DevTangentSink {
+    T* J;
+    long je, e;
+    __device__ __forceinline__ void begin(int, int nnz0) { e = (long)nnz0 * je; }
+    __device__ __forceinline__ void jac(int, const Dual<T, 1>& v) {
+        J[e] = v.d[0];
+        e += je;
+    }
+    __device__ __forceinline__ void row(const Dual<T, 1>&, double, double) {}
+    __device__ __forceinline__ void skip() { e += je; }
+    __device__ __forceinline__ void row_skip() {}
+    __device__ __forceinline__ void finish() {}
+};
+
+// one seeded pass for colour c: dJ = d J / d eps, dgf = d grad f / d eps along v_c
+// (outputs interleaved [entry][B]; w in either layout)
+template <class M, int UMASK>
+__global__ __launch_bounds__(WAVE) void k_hess_dual(ProbD p, int B, int layout, const double* __restrict__ w,
+                                                   const int32_t* __restrict__ color, int c,
+                                                   double* __restrict__ dJ, double* __restrict__ dgf) {
+    const int b = blockIdx.x * WAVE + threadIdx.x;
+    if (b >= B) return;
+    const int32_t* ut = p.units + 4 * blockIdx.y;
+    const bool il = layout == ATO_LAYOUT_INTERLEAVED;
+    const ColorW<double, DevW<double>> W{DevW<double>{il ? w + b : w + (long)b * p.nw, il ? (long)B : 1L}, color, c};
+    DevTangentSink<double> s{dJ + b, (long)B, 0};
+    const TangentGrad<double> go{dgf + b, (long)B};
+    run_unit<M, Dual<double, 1>, 0, true, true, UMASK>(p, ut[0], ut[1], ut[2], W, s, go);
+}
+
+// Hessian entries recovered from colour c: one wave = one take for 64 instances
+// (a template only so that every translation unit may instantiate it)
+template <int UNUSED = 0>
+__global__ __launch_bounds__(WAVE) void k_hess_take(int B, int layout, int ng, int nnzh, int t0,
+                                                   const int32_t* __restrict__ take_e,
+                                                   const int32_t* __restrict__ take_r,
+                                                   const int32_t* __restrict__ csc_ptr,
+                                                   const int32_t* __restrict__ csc_ent,
+                                                   const int32_t* __restrict__ csc_row,
+                                                   const double* __restrict__ lam, const double* __restrict__ sigma,
+                                                   const double* __restrict__ dJ, const double* __restrict__ dgf,
+                                                   double* __restrict__ H) {
+    const int b = blockIdx.x * WAVE + threadIdx.x;
+    if (b >= B) return;
+    const int t = t0 + blockIdx.y;
+    const int e = take_e[t], r = take_r[t];
+    const bool il = layout == ATO_LAYOUT_INTERLEAVED;
+    const double* lb = il ? lam + b : lam + (long)b * ng;
+    const long ls = il ? (long)B : 1L;
+    const double v = hess_take(csc_ptr, csc_ent, csc_row, r, sigma[b], lb, ls, dJ + b, (long)B, dgf + b, (long)B);
+    if (il) H[(long)e * B + b] = v;
+    else H[(long)b * nnzh + e] = v;
+}
+
+// device copies of the HessLayout tables
+struct HessDev {
+    const int32_t *color, *take_e, *take_r, *csc_ptr, *csc_ent, *csc_row;
+    const int32_t* take_off_host;   // host array [n_colors + 1]
+    int n_colors, nnzh;
+};
+
+template <class M>
+hipError_t launch_hess(const ProbD& p, const HessDev& hd, int B, int layout, const double* w, const double* lam,
+                       const double* sigma, double* H, double* dJ, double* dgf, hipStream_t st);
+
 // Host-side launcher, explicitly instantiated per model in ato_inst.hip (one translation unit
 // per model variant so the library builds in parallel).
 // ev (optional): events recorded before / after the g, J kernels and after the cost reduction
@@ -271,6 +341,28 @@ hipError_t launch_eval(const ProbD& p, int B, int layout, const T* w, T* g, T* J
     }
     if (ev) (void)hipEventRecord(ev[2], st);
     return e;
+}
+
+template <class M>
+hipError_t launch_hess(const ProbD& p, const HessDev& hd, int B, int layout, const double* w, const double* lam,
+                       const double* sigma, double* H, double* dJ, double* dgf, hipStream_t st) {
+    const int chunks = (B + WAVE - 1) / WAVE;
+    for (int c = 0; c < hd.n_colors; ++c) {
+        if (p.trans == ATO_TRANS_RK4)
+            hipLaunchKernelGGL((k_hess_dual<M, UMASK_RK4>), dim3(chunks, p.n_units), dim3(WAVE), 0, st, p, B, layout,
+                               w, hd.color, c, dJ, dgf);
+        else
+            hipLaunchKernelGGL((k_hess_dual<M, UMASK_COLLOC>), dim3(chunks, p.n_units), dim3(WAVE), 0, st, p, B,
+                               layout, w, hd.color, c, dJ, dgf);
+        const int t0 = hd.take_off_host[c], nt = hd.take_off_host[c + 1] - t0;
+        if (nt > 0)
+            hipLaunchKernelGGL(k_hess_take<0>, dim3(chunks, nt), dim3(WAVE), 0, st, B, layout, p.ng, hd.nnzh, t0,
+                               hd.take_e, hd.take_r, hd.csc_ptr, hd.csc_ent, hd.csc_row, lam, sigma,
+                               (const double*)dJ, (const double*)dgf, H);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 #endif
 

@@ -137,6 +137,8 @@ struct GradOut {
     long st;
     T* fpart;    // per-interval cost partials h_n sum_k B_k L_nk, element stride pst
     long pst;
+    ATO_HD void put_gf(long i, const T& v) const { gf[i * st] = v; }
+    ATO_HD void put_fpart(long n, const T& v) const { fpart[n * pst] = v; }
 };
 
 // f = sum_n partial(n), fixed order (the k_cost_reduce kernel and the CPU harness)
@@ -167,8 +169,8 @@ constexpr int UMASK_COLLOC = UMASK_TAIL | UMASK_ODE | UMASK_LIN;    // collocati
 constexpr int UMASK_RK4 = UMASK_TAIL | UMASK_LIN | UMASK_RK4U;      // RK4 problems
 constexpr int UMASK_ALL = UMASK_COLLOC | UMASK_RK4;
 
-template <class M, class T, int KS, bool ROWS, bool GRAD, int UMASK = UMASK_ALL, class W, class S>
-ATO_HD void run_unit(const ProbD& p, int kind, int n, int k, const W& w, S& s, const GradOut<T>& go) {
+template <class M, class T, int KS, bool ROWS, bool GRAD, int UMASK = UMASK_ALL, class W, class S, class GO>
+ATO_HD void run_unit(const ProbD& p, int kind, int n, int k, const W& w, S& s, const GO& go) {
     constexpr int NZ = M::NZ, NU = M::NU;
     constexpr bool RK4 = (UMASK & UMASK_RK4U) != 0;
     const int32_t* sg = p.seg + (long)(n * K1S(p) + (kind == UNIT_RK4 ? 0 : k)) * NSEG * 2;
@@ -210,13 +212,13 @@ ATO_HD void run_unit(const ProbD& p, int kind, int n, int k, const W& w, S& s, c
                 T gu[NU], gdu[NU];
                 stage_cost<M, T, KS>(p, n, k, w, gu, gdu);
                 const T hB = w(n) * T(p.Bq[k]);
-                const long base = (long)c.node(n, k) * go.st;
+                const long base = c.node(n, k);
 #pragma unroll
-                for (int i = 0; i < NZ; ++i) go.gf[base + i * go.st] = T(0);
+                for (int i = 0; i < NZ; ++i) go.put_gf(base + i, T(0));
 #pragma unroll
-                for (int i = 0; i < NU; ++i) go.gf[base + (NZ + i) * go.st] = hB * gu[i];
+                for (int i = 0; i < NU; ++i) go.put_gf(base + NZ + i, hB * gu[i]);
 #pragma unroll
-                for (int i = 0; i < NU; ++i) go.gf[base + (NZ + NU + i) * go.st] = hB * gdu[i];
+                for (int i = 0; i < NU; ++i) go.put_gf(base + NZ + NU + i, hB * gdu[i]);
             }
             break;
         case UNIT_INTERVAL:
@@ -229,8 +231,8 @@ ATO_HD void run_unit(const ProbD& p, int kind, int n, int k, const W& w, S& s, c
                 T acc = T(0);
                 for (int j = 0; j < K1S(p); ++j)
                     acc += T(p.Bq[j]) * stage_cost<M, T, KS>(p, n, j, w, (T*)nullptr, (T*)nullptr);
-                go.gf[(long)n * go.st] = acc;
-                go.fpart[(long)n * go.pst] = w(n) * acc;
+                go.put_gf(n, acc);
+                go.put_fpart(n, w(n) * acc);
             }
             break;
         case UNIT_RK4:   // k = Jacobian column group

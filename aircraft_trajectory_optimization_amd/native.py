@@ -88,8 +88,8 @@ class AtoProblemDesc(ctypes.Structure):
 
 
 EXPORTED_SYMBOLS = ('ato_create', 'ato_destroy', 'ato_sizes', 'ato_sparsity', 'ato_bounds',
-                    'ato_reserve', 'ato_eval', 'ato_eval_f32', 'ato_timing', 'ato_timing_read',
-                    'ato_last_error', 'ato_version')
+                    'ato_reserve', 'ato_eval', 'ato_eval_f32', 'ato_hess_sparsity', 'ato_hess_eval',
+                    'ato_timing', 'ato_timing_read', 'ato_last_error', 'ato_version')
 
 
 def library_path() -> str:
@@ -112,10 +112,13 @@ def declare(lib: ctypes.CDLL, prefix: str = 'ato') -> ctypes.CDLL:
         lib.ato_reserve.argtypes = [vp, ctypes.c_int32]
         lib.ato_eval.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, vp, vp, vp, vp, vp, vp]
         lib.ato_eval_f32.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, vp, vp, vp, vp, vp, vp]
+        lib.ato_hess_sparsity.argtypes = [vp, i32p, ctypes.POINTER(i32p), ctypes.POINTER(i32p), i32p]
+        lib.ato_hess_eval.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, vp, vp, vp, vp, vp]
         lib.ato_timing.argtypes = [vp, ctypes.c_int32]
         lib.ato_timing_read.argtypes = [vp, _c_double_p, _c_double_p, i32p]
         for fn in ('ato_create', 'ato_destroy', 'ato_sizes', 'ato_sparsity', 'ato_bounds', 'ato_reserve',
-                   'ato_eval', 'ato_eval_f32', 'ato_timing', 'ato_timing_read'):
+                   'ato_eval', 'ato_eval_f32', 'ato_hess_sparsity', 'ato_hess_eval', 'ato_timing',
+                   'ato_timing_read'):
             getattr(lib, fn).restype = ctypes.c_int
     return lib
 
@@ -264,6 +267,23 @@ class NativeProblem:
         fn = self.lib.ato_eval_f32 if fp32 else self.lib.ato_eval
         self._check(fn(self.handle, int(batch), int(layout), w or None, g or None, jac or None,
                        f or None, grad_f or None, stream or None))
+
+    def hess_sparsity(self) -> Tuple[np.ndarray, np.ndarray, int]:
+        ''' lower-triangle CSR (row_ptr[nw+1], col[nnz_h]) of the Lagrangian Hessian, colour count '''
+        nnz, nc = ctypes.c_int32(), ctypes.c_int32()
+        rp = ctypes.POINTER(ctypes.c_int32)()
+        cp = ctypes.POINTER(ctypes.c_int32)()
+        self._check(self.lib.ato_hess_sparsity(self.handle, ctypes.byref(nnz), ctypes.byref(rp), ctypes.byref(cp),
+                                               ctypes.byref(nc)))
+        row_ptr = np.ctypeslib.as_array(rp, shape=(self.nw + 1,)).copy()
+        col = np.ctypeslib.as_array(cp, shape=(nnz.value,)).copy() if nnz.value else np.zeros(0, np.int32)
+        return row_ptr, col, nc.value
+
+    def hess_eval_ptrs(self, batch: int, w: int, lam: int, sigma: int, hess: int,
+                       layout: int = ATO_LAYOUT_INTERLEAVED, stream: int = 0):
+        ''' Hessian of the Lagrangian on device pointers (fp64, asynchronous on `stream`) '''
+        self._check(self.lib.ato_hess_eval(self.handle, int(batch), int(layout), w, lam, sigma, hess,
+                                           stream or None))
 
     def timing_start(self, max_calls: int):
         ''' record HIP events around the kernels of the next max_calls evaluations '''

@@ -67,6 +67,26 @@ class BatchedNLP:
             grad_f=self.grad_f.data_ptr() if cost else 0,
             layout=self.layout, stream=st.cuda_stream, fp32=self.fp32)
 
+    def hessian(self, lam: torch.Tensor, sigma: torch.Tensor, stream=None) -> torch.Tensor:
+        '''
+        Hessian of the Lagrangian (lower triangle, values in hess_sparsity() order) for multipliers
+        lam (same layout as g) and objective factors sigma [B]; fp64 only.
+        '''
+        if self.fp32:
+            raise TypeError('the Hessian is evaluated in fp64')
+        if not hasattr(self, 'hess_row_ptr'):
+            self.hess_row_ptr, self.hess_col, self.hess_colors = self.problem.hess_sparsity()
+            shape = (len(self.hess_col), self.batch) if self.layout == native.ATO_LAYOUT_INTERLEAVED \
+                else (self.batch, len(self.hess_col))
+            self.hess = torch.zeros(shape, device=self.device, dtype=torch.float64)
+            self.problem.reserve(self.batch)
+        lam = lam.contiguous()
+        sigma = sigma.contiguous()
+        st = stream if stream is not None else torch.cuda.current_stream(self.device)
+        self.problem.hess_eval_ptrs(self.batch, self.w.data_ptr(), lam.data_ptr(), sigma.data_ptr(),
+                                    self.hess.data_ptr(), layout=self.layout, stream=st.cuda_stream)
+        return self.hess
+
     def _host(self, t: torch.Tensor) -> np.ndarray:
         a = t.detach().to('cpu', torch.float64).numpy()
         return a.T.copy() if self.layout == native.ATO_LAYOUT_INTERLEAVED else a

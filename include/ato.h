@@ -133,6 +133,19 @@ int ato_eval(ato_handle* h, int32_t batch, int32_t layout, const double* w,
 int ato_eval_f32(ato_handle* h, int32_t batch, int32_t layout, const float* w,
                  float* g, float* jac, float* f, float* grad_f, void* stream);
 
+/* Hessian of the Lagrangian  sigma * grad^2 f + sum_i lam_i * grad^2 g_i  (IPOPT's nlp_hess_l,
+ * base_raceline.py:752-799). Structure: lower triangle (col <= row) CSR with ascending columns
+ * (host arrays owned by the handle). The first call analyses the structure and colours the
+ * columns; n_colors seeded passes make up one evaluation. */
+int ato_hess_sparsity(ato_handle* h, int32_t* nnz, const int32_t** row_ptr, const int32_t** col,
+                      int32_t* n_colors);
+
+/* hess [nnz_h x batch] (layout) for w [nw x batch], lam [ng x batch], sigma [batch] (fp64).
+ * Asynchronous on stream; allocates its scratch on the first call for a larger batch
+ * (ato_reserve after ato_hess_sparsity pre-allocates it). */
+int ato_hess_eval(ato_handle* h, int32_t batch, int32_t layout, const double* w, const double* lam,
+                  const double* sigma, double* hess, void* stream);
+
 /* Per-kernel timing with HIP events recorded on the evaluation stream. ato_timing(h, n)
  * allocates n event slots and starts recording (n = 0 stops); while on, each ato_eval
  * records events around its Jacobian kernel and its cost-reduction kernel. ato_timing_read

@@ -443,3 +443,27 @@ class RefNLP:
         W = np.repeat(w[:, None], self.nw, axis=1).astype(complex)
         W[np.arange(self.nw), np.arange(self.nw)] += 1j * h
         return np.imag(self.f(W)) / h
+
+    # -------------------------------------------------------------- Hessian of the Lagrangian (checker)
+    def grad_lagrangian(self, w, lam, sigma, h=1e-30, chunk=256):
+        ''' sigma grad f + J^T lam by complex step of sigma f + lam^T g (w real) '''
+        w = np.asarray(w, float)
+        out = np.zeros(self.nw)
+        for c0 in range(0, self.nw, chunk):
+            c1 = min(self.nw, c0 + chunk)
+            W = np.repeat(w[:, None], c1 - c0, axis=1).astype(complex)
+            W[np.arange(c0, c1), np.arange(c1 - c0)] += 1j * h
+            L = sigma * self.f(W) + np.asarray(lam, float) @ self._build(W)
+            out[c0:c1] = np.imag(L) / h
+        return out
+
+    def hvp(self, w, lam, sigma, V, eps=1e-5):
+        ''' (sigma grad^2 f + sum lam_i grad^2 g_i) V by central differences of the exact
+        (complex-step) Lagrangian gradient; truncation error O(eps^2) '''
+        V = np.atleast_2d(np.asarray(V, float).T).T
+        cols = []
+        for j in range(V.shape[1]):
+            gp = self.grad_lagrangian(w + eps * V[:, j], lam, sigma)
+            gm = self.grad_lagrangian(w - eps * V[:, j], lam, sigma)
+            cols.append((gp - gm) / (2 * eps))
+        return np.stack(cols, axis=1)

@@ -40,6 +40,15 @@ def random_w(spec_or_nlp, rng, scale=0.05):
     return w
 
 
+def sym_dense(row_ptr, col, vals, n):
+    ''' symmetric dense matrix from a lower-triangle CSR '''
+    H = np.zeros((n, n))
+    for r in range(n):
+        c = col[row_ptr[r]:row_ptr[r + 1]]
+        H[r, c] = vals[row_ptr[r]:row_ptr[r + 1]]
+    return H + np.tril(H, -1).T
+
+
 def csr_dense(row_ptr, col, vals, ng, nw):
     J = np.zeros((ng, nw))
     for r in range(ng):
@@ -54,7 +63,8 @@ HOSTCHECK_LIB = os.path.join(REPO, 'tests', 'native', 'libato_hostcheck.so')
 
 def build_hostcheck(force=False):
     srcs = [HOSTCHECK_SRC] + [os.path.join(REPO, 'aircraft_trajectory_optimization_amd', 'csrc', f)
-                              for f in ('ato_models.hpp', 'ato_dual.hpp', 'ato_program.hpp', 'ato_layout.hpp')]
+                              for f in ('ato_models.hpp', 'ato_dual.hpp', 'ato_program.hpp', 'ato_layout.hpp',
+                                        'ato_hessian.hpp')]
     if not force and os.path.exists(HOSTCHECK_LIB) and \
             os.path.getmtime(HOSTCHECK_LIB) >= max(os.path.getmtime(s) for s in srcs):
         return HOSTCHECK_LIB
@@ -75,6 +85,9 @@ class HostCheck:
         lib.atoh_sizes.argtypes = [vp] + [ctypes.POINTER(ctypes.c_int32)] * 3
         lib.atoh_sparsity.argtypes = [vp, vp, vp]
         lib.atoh_bounds.argtypes = [vp, vp, vp]
+        lib.atoh_hess_sparsity.argtypes = [vp, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)]
+        lib.atoh_hess_pattern.argtypes = [vp, vp, vp]
+        lib.atoh_hess_eval.argtypes = [vp, ctypes.c_int, vp, vp, vp, vp]
         self.lib = lib
         self.holder = native.DescHolder(spec_dict)
         h = vp()
@@ -105,8 +118,56 @@ class HostCheck:
             raise RuntimeError(self.lib.atoh_last_error().decode())
         return g, J, f, gf
 
+    def hess_pattern(self):
+        nnz, nc = ctypes.c_int32(), ctypes.c_int32()
+        if self.lib.atoh_hess_sparsity(self.h, ctypes.byref(nnz), ctypes.byref(nc)) != 0:
+            raise RuntimeError(self.lib.atoh_last_error().decode())
+        rp = np.zeros(self.nw + 1, np.int32)
+        col = np.zeros(nnz.value, np.int32)
+        self.lib.atoh_hess_pattern(self.h, rp.ctypes.data, col.ctypes.data)
+        return rp, col, nc.value
+
+    def hess(self, W, LAM, sigma):
+        ''' W (B, nw), LAM (B, ng), sigma (B,) -> lower-triangle values (B, nnz_h) '''
+        rp, col, _ = self.hess_pattern()
+        W = np.ascontiguousarray(np.atleast_2d(W), dtype=np.float64)
+        LAM = np.ascontiguousarray(np.atleast_2d(LAM), dtype=np.float64)
+        sig = np.ascontiguousarray(np.atleast_1d(sigma), dtype=np.float64)
+        H = np.zeros((W.shape[0], len(col)))
+        if self.lib.atoh_hess_eval(self.h, W.shape[0], W.ctypes.data, LAM.ctypes.data, sig.ctypes.data,
+                                   H.ctypes.data) != 0:
+            raise RuntimeError(self.lib.atoh_last_error().decode())
+        return H
+
     def __del__(self):
         try:
             self.lib.atoh_destroy(self.h)
         except Exception:  # pylint: disable=broad-except
             pass
+
+
+class HostEvaluator:
+    ''' evaluator interface of solver.ipm over the CPU build of the programs (tests only) '''
+
+    def __init__(self, spec):
+        self.hc = HostCheck(spec.native_spec())
+        self.nw, self.ng = self.hc.nw, self.hc.ng
+        self.j_row_ptr, self.j_col = self.hc.row_ptr, self.hc.col
+        self.h_row_ptr, self.h_col, _ = self.hc.hess_pattern()
+        self.lbg, self.ubg = self.hc.lbg, self.hc.ubg
+        self.var_stage = var_stages(spec)
+
+    def eval(self, x):
+        g, J, f, gf = self.hc.eval(x)
+        return f[0], g[0], gf[0], J[0]
+
+    def hess(self, x, lam, sigma):
+        return self.hc.hess(x, lam, sigma)[0]
+
+
+def var_stages(spec):
+    ''' interval of every decision variable: h_n -> n, node (n, k) -> n '''
+    st = np.zeros(spec.nw, int)
+    st[:spec.N] = np.arange(spec.N)
+    st[spec.N:] = np.repeat(np.arange(spec.P) // spec.K1, spec.nv)
+    return st

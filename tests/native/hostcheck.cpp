@@ -7,7 +7,8 @@
 // whose evaluation path is the HIP library only.
 #include <string>
 #include <vector>
-#include "../../aircraft_trajectory_optimization_amd/csrc/ato_layout.hpp"
+#define ATO_HESS_ANALYSIS_IMPL
+#include "../../aircraft_trajectory_optimization_amd/csrc/ato_hessian.hpp"
 
 namespace {
 
@@ -44,8 +45,22 @@ thread_local std::string last_err;
 
 }  // namespace
 
+template <class T>
+struct HostTangentSink {
+    T* J;
+    long e;
+    void begin(int, int nnz0) { e = nnz0; }
+    void jac(int, const ato::Dual<T, 1>& v) { J[e++] = v.d[0]; }
+    void row(const ato::Dual<T, 1>&, double, double) {}
+    void skip() { ++e; }
+    void row_skip() {}
+    void finish() {}
+};
+
 struct atoh_handle {
     ato::Layout L;
+    ato::HessLayout HL;
+    bool hess = false;
 };
 
 extern "C" {
@@ -99,6 +114,57 @@ int atoh_eval(const atoh_handle* h, int B, const double* w, double* g, double* J
                 ato::run_unit<M, double, 0, true, true>(p, ut[0], ut[1], ut[2], W, s, go);
             }
             f[b] = ato::reduce_cost(fpart.data(), 1, p.N);
+        }
+    });
+    if (!ok) {
+        last_err = "unsupported model";
+        return -1;
+    }
+    return 0;
+}
+
+int atoh_hess_sparsity(atoh_handle* h, int32_t* nnz, int32_t* n_colors) {
+    if (!h->hess) {
+        std::string e = h->HL.build(h->L);
+        if (!e.empty()) {
+            last_err = e;
+            return -1;
+        }
+        h->hess = true;
+    }
+    *nnz = h->HL.nnz();
+    *n_colors = h->HL.n_colors;
+    return 0;
+}
+
+void atoh_hess_pattern(const atoh_handle* h, int32_t* row_ptr, int32_t* col) {
+    for (size_t i = 0; i < h->HL.row_ptr.size(); ++i) row_ptr[i] = h->HL.row_ptr[i];
+    for (size_t i = 0; i < h->HL.col.size(); ++i) col[i] = h->HL.col[i];
+}
+
+// instance-major: w [B][nw], lam [B][ng], sigma [B], H [B][nnz_h]; the same seeded passes and
+// recovery as the HIP launcher
+int atoh_hess_eval(atoh_handle* h, int B, const double* w, const double* lam, const double* sigma, double* H) {
+    int32_t nnzh, nc;
+    if (atoh_hess_sparsity(h, &nnzh, &nc)) return -1;
+    const ato::ProbD& p = h->L.p;
+    const ato::HessLayout& HL = h->HL;
+    std::vector<double> dJ(p.nnz), dgf(p.nw);
+    bool ok = ato::with_model(p, [&]<class M>() {
+        for (int b = 0; b < B; ++b) {
+            for (int c = 0; c < HL.n_colors; ++c) {
+                ato::ColorW<double, HostW<double>> W{HostW<double>{w + (long)b * p.nw, 1}, HL.color.data(), c};
+                HostTangentSink<double> s{dJ.data(), 0};
+                const ato::TangentGrad<double> go{dgf.data(), 1};
+                for (int u = 0; u < p.n_units; ++u) {
+                    const int32_t* ut = p.units + 4 * u;
+                    ato::run_unit<M, ato::Dual<double, 1>, 0, true, true>(p, ut[0], ut[1], ut[2], W, s, go);
+                }
+                for (int t = HL.take_off[c]; t < HL.take_off[c + 1]; ++t)
+                    H[(long)b * nnzh + HL.take_e[t]] =
+                        ato::hess_take(HL.csc_ptr.data(), HL.csc_ent.data(), HL.csc_row.data(), HL.take_r[t],
+                                       sigma[b], lam + (long)b * p.ng, 1L, dJ.data(), 1L, dgf.data(), 1L);
+            }
         }
     });
     if (!ok) {

@@ -144,3 +144,33 @@ def test_race_script_rk4(frame):
         Jv = np.stack([np.add.reduceat(J[b] * V[bn.col, j], bn.row_ptr[:-1]) for j in range(2)], axis=1)
         _close(Jv, nlp.jvp(W[b], V), 1e-11)
         _close(gf[b], nlp.grad_f(W[b]))
+
+
+HESS_CASES = [dict(track='race', N=4, K=2), dict(track='fig8', N=3, K=3, use_quat=False),
+              dict(track='race', frame='global', N=7, K=2), dict(track='race', model='point', use_quat=False, N=4, K=2),
+              dict(track='race', N=7, K=2, rk4=True), dict(track='race', N=50, K=4)]
+
+
+@pytest.mark.parametrize('cfg', HESS_CASES, ids=_id)
+def test_hessian_matches_host_programs(cfg):
+    ''' device Hessian (seeded dual passes + recovery kernels) against the CPU build of the same
+    programs, which tests/test_hessian_cpu.py checks against the oracle '''
+    from tests.helpers import HostCheck
+    rng = np.random.default_rng(23)
+    spec = product_spec(**cfg)
+    nlp = oracle_nlp(**cfg)
+    B = 64 if cfg.get('N', 0) >= 50 else 3
+    W = np.stack([random_w(nlp, rng) for _ in range(B)])
+    LAM = rng.standard_normal((B, nlp.ng))
+    sig = rng.uniform(0.5, 1.5, B)
+    bn = _batched(spec, B)
+    bn.set_w(W)
+    H = bn.hessian(torch.as_tensor(LAM.T.copy(), device=bn.device), torch.as_tensor(sig, device=bn.device))
+    Hd = H.cpu().numpy().T
+    hc = HostCheck(spec.native_spec())
+    rp, col, _ = hc.hess_pattern()
+    np.testing.assert_array_equal(rp, bn.hess_row_ptr)
+    np.testing.assert_array_equal(col, bn.hess_col)
+    for b in sorted({0, B // 2, B - 1}):
+        Hh = hc.hess(W[b], LAM[b], sig[b])[0]
+        _close(Hd[b], Hh)

@@ -24,7 +24,7 @@ def test_library_loads_and_exports_header_symbols():
     for name in declared:
         assert hasattr(lib, name), f'{name} declared in ato.h but not exported'
     assert set(declared) == set(native.EXPORTED_SYMBOLS)
-    assert lib.ato_version().decode().startswith('ato 1')
+    assert lib.ato_version().decode().startswith('ato 2')
 
 
 def test_ctypes_struct_layout():
