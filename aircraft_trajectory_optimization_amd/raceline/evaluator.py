@@ -1,0 +1,62 @@
+'''
+Evaluator of one raceline NLP on the HIP library, in the interface of solver.ipm:
+f, g, grad f, Jacobian values (CSR of ato_sparsity) and the Lagrangian Hessian (lower CSR of
+ato_hess_sparsity), computed on the device (ato_eval / ato_hess_eval) and returned as numpy.
+
+This replaces the CasADi functions IPOPT calls (nlp_f, nlp_g, nlp_grad_f, nlp_jac_g,
+nlp_hess_l; base_raceline.py:165, :182-189). Time spent here is the reference's feval_time.
+'''
+import time
+
+import numpy as np
+import torch
+
+from aircraft_trajectory_optimization_amd.raceline.batched import BatchedNLP
+from aircraft_trajectory_optimization_amd.raceline.problem import ProblemSpec
+
+
+def variable_stages(spec: ProblemSpec) -> np.ndarray:
+    ''' interval of every decision variable (h_n -> n, node (n, k) -> n): the KKT block order '''
+    st = np.zeros(spec.nw, dtype=np.int64)
+    st[:spec.N] = np.arange(spec.N)
+    st[spec.N:] = np.repeat(np.arange(spec.P) // spec.K1, spec.nv)
+    return st
+
+
+class DeviceEvaluator:
+    ''' single-instance evaluator on the current HIP device '''
+
+    def __init__(self, spec: ProblemSpec, device=None):
+        self.spec = spec
+        self.bn = BatchedNLP(spec, 1, device=device)
+        self.nw, self.ng, self.nnz = self.bn.sizes
+        self.j_row_ptr, self.j_col = self.bn.row_ptr, self.bn.col
+        self.lbg, self.ubg = self.bn.lbg, self.bn.ubg
+        self.h_row_ptr, self.h_col, self.n_colors = self.bn.problem.hess_sparsity()
+        self.var_stage = variable_stages(spec)
+        self._lam = torch.zeros((self.ng, 1), dtype=torch.float64, device=self.bn.device)
+        self._sig = torch.zeros(1, dtype=torch.float64, device=self.bn.device)
+        self.feval_time = 0.0
+
+    def _set(self, x):
+        self.bn.w.copy_(torch.as_tensor(np.asarray(x, float).reshape(-1, 1), device=self.bn.device))
+
+    def eval(self, x):
+        t0 = time.perf_counter()
+        self._set(x)
+        self.bn.evaluate()
+        torch.cuda.synchronize(self.bn.device)
+        out = (float(self.bn.f[0].item()), self.bn.g[:, 0].cpu().numpy(), self.bn.grad_f[:, 0].cpu().numpy(),
+               self.bn.jac[:, 0].cpu().numpy())
+        self.feval_time += time.perf_counter() - t0
+        return out
+
+    def hess(self, x, lam, sigma):
+        t0 = time.perf_counter()
+        self._set(x)
+        self._lam.copy_(torch.as_tensor(np.asarray(lam, float).reshape(-1, 1)))
+        self._sig.fill_(float(sigma))
+        H = self.bn.hessian(self._lam, self._sig)
+        out = H[:, 0].cpu().numpy()
+        self.feval_time += time.perf_counter() - t0
+        return out

@@ -7,8 +7,8 @@ LDL^T, base_raceline.py:765-782).
 
 The transcription is a chain of intervals: every decision variable belongs to one interval
 (stage), the Hessian is block diagonal by stage, and almost every constraint row touches one
-stage or two neighbouring ones (continuity). Ordering each stage's variables and rows together
-makes K block tridiagonal; the few rows that reach further (loop closure, equal step sizes of
+stage or two neighbouring ones (continuity, joined to the later stage). Ordering each stage's
+variables and rows together makes K block tridiagonal; the few rows that reach further (loop closure, equal step sizes of
 the global frame) form a border eliminated last:
 
     S_0 = A_0,   S_n = A_n - B_n S_{n-1}^{-1} B_n^T
@@ -26,24 +26,24 @@ from scipy.linalg import lapack
 
 
 def _inertia_ldl(ldu, ipiv):
-    ''' (n_pos, n_neg, n_zero) of a sytrf factor (lower storage) '''
-    n = ldu.shape[0]
-    pos = neg = zero = 0
-    i = 0
-    while i < n:
-        if ipiv[i] > 0:
-            d = ldu[i, i]
-            pos += d > 0
-            neg += d < 0
-            zero += d == 0
-            i += 1
-        else:
-            a, b, c = ldu[i, i], ldu[i + 1, i], ldu[i + 1, i + 1]
-            ev = np.linalg.eigvalsh(np.array([[a, b], [b, c]]))
-            pos += int((ev > 0).sum())
-            neg += int((ev < 0).sum())
-            zero += int((ev == 0).sum())
-            i += 2
+    ''' (n_pos, n_neg, n_zero) of a sytrf factor (lower storage): 1x1 pivots by sign, 2x2
+    pivots [[a, b], [b, c]] (ipiv < 0 on both rows) by determinant and trace '''
+    d = np.diag(ldu)
+    two = ipiv < 0
+    # rows of 2x2 blocks come in pairs: the first row of every pair
+    idx2 = np.nonzero(two)[0][::2]
+    one = ~two
+    pos = int((d[one] > 0).sum())
+    neg = int((d[one] < 0).sum())
+    zero = int((d[one] == 0).sum())
+    if len(idx2):
+        a, c = d[idx2], d[idx2 + 1]
+        b = ldu[idx2 + 1, idx2]
+        det = a * c - b * b
+        tr = a + c
+        pos += int((det < 0).sum() + 2 * ((det > 0) & (tr > 0)).sum() + ((det == 0) & (tr > 0)).sum())
+        neg += int((det < 0).sum() + 2 * ((det > 0) & (tr < 0)).sum() + ((det == 0) & (tr < 0)).sum())
+        zero += int((det == 0).sum() + ((det == 0) & (tr == 0)).sum())
     return pos, neg, zero
 
 
@@ -56,7 +56,7 @@ class _Factor:
             self.ldu, self.ipiv, self.info = S, np.zeros(0, np.int32), 0
             self.inertia = (0, 0, 0)
             return
-        self.ldu, self.ipiv, self.info = lapack.dsytrf(S, lower=1)
+        self.ldu, self.ipiv, self.info = lapack.dsytrf(S, lower=1, lwork=max(1, 64 * self.n))
         self.inertia = _inertia_ldl(self.ldu, self.ipiv) if self.info >= 0 else (0, 0, self.n)
         if self.info > 0:                      # exactly singular D block
             self.inertia = (self.inertia[0], self.inertia[1], max(1, self.inertia[2]))
@@ -73,7 +73,7 @@ class BlockKKT:
     '''
     Block structure of the KKT matrix for one problem: var_stage[j] (interval of variable j),
     Jacobian CSR pattern, lower-CSR Hessian pattern. Rows that touch one stage or two
-    neighbouring stages join the lower one; all other rows form the border.
+    neighbouring stages join the later one; all other rows form the border.
     '''
 
     def __init__(self, n: int, m: int, var_stage: np.ndarray, j_row_ptr, j_col, h_row_ptr, h_col):
@@ -86,7 +86,11 @@ class BlockKKT:
         hi = np.full(m, -1)
         np.minimum.at(lo, jr, st)
         np.maximum.at(hi, jr, st)
-        row_stage = np.where(hi - lo <= 1, lo, -1)
+        # rows spanning two neighbouring stages join the LATER one: a continuity row then carries
+        # its identity entry on the new interval's first node inside its own block (joined to the
+        # earlier stage, a quaternion continuity block would keep only its rank-3 normalisation
+        # Jacobian and leave that stage block singular)
+        row_stage = np.where(hi - lo <= 1, hi, -1)
         row_stage[hi < 0] = 0                       # empty rows (none expected)
         self.row_stage = row_stage
         # global ordering: per stage [variables, rows], then border rows
