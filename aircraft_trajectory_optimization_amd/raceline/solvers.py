@@ -1,0 +1,244 @@
+'''
+Raceline solver classes with the reference's public surface (drone3d/raceline/*.py):
+
+    GlobalDroneRaceline, ParametricDroneRaceline          drone_raceline.py:280-368
+    GlobalPointRaceline, ParametricPointRaceline          point_raceline.py:48-74
+    ParametricObstacleDroneRaceline / ...PointRaceline    drone_raceline.py:371-427, point_raceline.py:77-90
+
+    solver = XxxRaceline(line, config, vehicle_config[, ...], ws_raceline=None, ws_model=None,
+                         generate_ws=True)
+    results: RacelineResults = solver.solve()          base_raceline.py:157-191
+    solver.setup_time, solver.model, solver.ws_solver, solver.ws_raceline, solver.get_ws()
+
+Instead of CasADi SX graphs and IPOPT, the constructor builds a ProblemSpec (host tables) and
+a device evaluator over libato.so; solve() runs the interior-point solver (solver/ipm.py) whose
+every g / J / f / grad f / Hessian evaluation runs in the HIP kernels. RacelineResults keeps the
+reference's timing split: feval_time = time in device evaluation, ipopt_time = the rest.
+'''
+import time
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+
+from aircraft_trajectory_optimization_amd.centerlines.base_centerline import BaseCenterline
+from aircraft_trajectory_optimization_amd.pytypes import DroneConfig, DroneState, GlobalEulerAngles, \
+    GlobalQuaternion, PointConfig, PointState, RelativeEulerAngles, RelativeQuaternion
+from aircraft_trajectory_optimization_amd.raceline.config import GlobalRacelineConfig, \
+    ParametricRacelineConfig, RacelineConfig, RacelineResults
+from aircraft_trajectory_optimization_amd.raceline.problem import ProblemSpec
+from aircraft_trajectory_optimization_amd.utils.discretization_utils import interpolate_collocation, \
+    interpolate_linear
+
+# decision vectors of solutions produced here, so a RacelineResults can warm-start a drone solve
+_SOLUTIONS: Dict[int, Tuple[ProblemSpec, np.ndarray, RacelineResults]] = {}
+
+
+class RacelineModel:
+    ''' the parts of the reference DynamicsModel the scripts and viewers use '''
+
+    def __init__(self, spec: ProblemSpec):
+        self.spec = spec
+        self.config = spec.vehicle
+
+    def get_empty_state(self):
+        return DroneState() if self.spec.is_drone else PointState()
+
+    def _R_global(self, z) -> np.ndarray:
+        sp_, v = self.spec, self.spec.vehicle
+        if sp_.is_drone:
+            if v.use_quat:
+                q = GlobalQuaternion()
+                q.from_vec(z[3:7])
+                R = q.R()
+            else:
+                e = GlobalEulerAngles()
+                e.from_vec(z[3:6])
+                R = e.R()
+            if sp_.param and not v.global_r:
+                R = self.spec.line.p2Rp(z[0]) @ R
+            return R
+        if sp_.param and not v.global_r:
+            return self.spec.line.p2Rp(z[0])
+        return np.eye(3)
+
+    def zu2state(self, state, z, u, last_q=None):
+        ''' node state, input (drone_models.py:162-183, :306-328; point_model.py) '''
+        sp_ = self.spec
+        state.u.from_vec(u)
+        if sp_.param:
+            state.p.from_vec(z[:3])
+            state.x.from_vec(sp_.line.p2x(*z[:3]))
+        else:
+            state.x.from_vec(z[:3])
+        if sp_.is_drone:
+            nr = 4 if sp_.vehicle.use_quat else 3
+            if sp_.vehicle.use_quat:
+                state.r = GlobalQuaternion() if sp_.vehicle.global_r else RelativeQuaternion()
+            else:
+                state.r = GlobalEulerAngles() if sp_.vehicle.global_r else RelativeEulerAngles()
+            state.r.from_vec(z[3:3 + nr])
+            state.v.from_vec(z[3 + nr:6 + nr])
+            state.w.from_vec(z[6 + nr:9 + nr])
+        else:
+            state.v.from_vec(z[3:6])
+        if sp_.is_drone and sp_.vehicle.use_quat and not sp_.param:
+            state.q.from_vec(z[3:7])
+        else:
+            state.q.from_mat(self._R_global(z))
+            if last_q is not None and np.linalg.norm(last_q - state.q.to_vec()) > 1.8:
+                state.q.from_vec(-state.q.to_vec())
+        return state.q.to_vec()
+
+
+class _Raceline:
+    ''' shared machinery of every raceline solver '''
+    frame = 'parametric'
+    label = ''
+    color: List[float] = [1, 1, 1, 1]
+    sphere_table: Optional[np.ndarray] = None
+
+    # evaluator over libato.so (tests substitute the CPU build of the programs here)
+    evaluator_factory = None
+
+    def __init__(self, line: BaseCenterline, config: RacelineConfig, vehicle_config, ws_raceline=None,
+                 ws_model=None, guess=None):
+        t0 = time.time()
+        factory = _Raceline.evaluator_factory
+        if factory is None:
+            from aircraft_trajectory_optimization_amd.raceline.evaluator import DeviceEvaluator as factory
+        self.line, self.config, self.vehicle_config = line, config, vehicle_config
+        self.ws_raceline, self.ws_model = ws_raceline, ws_model
+        quat_flip, wraps = False, 0.0
+        w_guess = None
+        if guess is not None:
+            w_guess, quat_flip, wraps = guess
+        self.spec = ProblemSpec(line, config, vehicle_config, self.frame, quat_flip=quat_flip, euler_wraps=wraps,
+                                sphere_table=self.sphere_table)
+        if w_guess is not None:
+            self.spec.w0, self.spec.lbw, self.spec.ubw = w_guess
+        self.model = RacelineModel(self.spec)
+        self.evaluator = factory(self.spec)
+        self.global_frame = not self.spec.param
+        self.solve_time = self.ipopt_time = self.feval_time = 0.0
+        self.result = None
+        self.setup_time = time.time() - t0
+
+    # ------------------------------------------------------------------ solving
+    def solve(self) -> RacelineResults:
+        from aircraft_trajectory_optimization_amd.solver.ipm import InteriorPointSolver, IPMOptions
+        ev = self.evaluator
+        ev.feval_time = 0.0
+        solver = InteriorPointSolver(ev, self.spec.lbw, self.spec.ubw, ev.lbg, ev.ubg,
+                                     IPMOptions(max_iter=self.config.max_iter,
+                                                verbose=bool(getattr(self.config, 'verbose', False))))
+        t0 = time.time()
+        self.result = solver.solve(self.spec.w0)
+        self.solve_time = time.time() - t0
+        self.feval_time = ev.feval_time
+        self.ipopt_time = self.solve_time - self.feval_time
+        out = self._unpack(self.result.x, self.result.success)
+        _SOLUTIONS[id(out)] = (self.spec, self.result.x.copy(), out)
+        return out
+
+    def get_ws(self) -> RacelineResults:
+        ''' the initial guess, unpacked like a solution (base_raceline.py:193-198) '''
+        return self._unpack(self.spec.w0, False)
+
+    def _unpack(self, x, feasible) -> RacelineResults:
+        ''' base_raceline.py:801-864 '''
+        sp_ = self.spec
+        N, K1, nz, nu = sp_.N, sp_.K1, sp_.nz, sp_.nu
+        h = np.asarray(x[:N], float)
+        t0 = np.concatenate([[0.0], np.cumsum(h)])[:-1]
+        nodes = x[N:].reshape(N * K1, sp_.nv)
+        Z, U, dU = nodes[:, :nz], nodes[:, nz:nz + nu], nodes[:, nz + nu:]
+        states = []
+        last_q = None
+        for n in range(N):
+            for k in range(K1):
+                i = n * K1 + k
+                st = self.model.get_empty_state()
+                st.t = float(t0[n] + sp_.tau[k] * h[n])
+                last_q = self.model.zu2state(st, Z[i], U[i], last_q)
+                st.du.from_vec(dU[i])
+                states.append(st)
+        if sp_.rk4:
+            zi, ui, dui = interpolate_linear(h, Z), interpolate_linear(h, U), interpolate_linear(h, dU)
+        else:
+            zi = interpolate_collocation(h, Z.reshape(N, K1, nz), sp_.K)
+            ui = interpolate_collocation(h, U.reshape(N, K1, nu), sp_.K)
+            dui = interpolate_collocation(h, dU.reshape(N, K1, nu), sp_.K)
+        return RacelineResults(
+            states=states, step_sizes=h, time=float(np.sum(h)), periodic=bool(self.config.closed),
+            label=self.label, color=list(self.color), z_interp=zi, u_interp=ui, du_interp=dui,
+            solve_time=self.solve_time, feval_time=self.feval_time, ipopt_time=self.ipopt_time,
+            feasible=bool(feasible), global_frame=self.global_frame)
+
+
+def _point_guess(solver_cls, line, config, vehicle_config: DroneConfig, generate_ws, ws_raceline, extra=()):
+    ''' point-mass warm start: (ws_solver, ws_raceline, ws_model, drone guess builder) '''
+    ws_solver = None
+    if generate_ws:
+        ws_config = config.copy()
+        ws_config.verbose = False
+        ws_config.plot_iterations = False
+        point_config = PointConfig(global_r=vehicle_config.global_r,
+                                   collision_radius=vehicle_config.collision_radius)
+        print('Generating Warmstart... ')
+        t0 = time.time()
+        ws_solver = solver_cls(line, ws_config, point_config, *extra)
+        ws_raceline = ws_solver.solve()
+        print(f'Done (Lap Time: {ws_raceline.time:0.2f}s) (Setup + Solve: {time.time() - t0:0.2f}s)')
+    if ws_raceline is None or id(ws_raceline) not in _SOLUTIONS:
+        return ws_solver, ws_raceline, None, None
+    pspec, x, _ = _SOLUTIONS[id(ws_raceline)]
+    return ws_solver, ws_raceline, RacelineModel(pspec), (pspec, x)
+
+
+class _DroneRaceline(_Raceline):
+    ''' drone racelines, optionally warm-started from a point-mass solve (drone_raceline.py:24-277) '''
+    point_cls = None
+
+    def __init__(self, line, config, vehicle_config: DroneConfig, ws_raceline=None, ws_model=None,
+                 generate_ws: bool = True, extra=()):
+        from aircraft_trajectory_optimization_amd.raceline.warmstart import drone_guess
+        self.ws_solver, ws_raceline, pmodel, ws = _point_guess(self.point_cls, line, config, vehicle_config,
+                                                               generate_ws, ws_raceline, extra)
+        guess = None
+        if ws is not None:
+            # a provisional spec (on a copy of the config) gives the indexing and bounds
+            prov = ProblemSpec(line, config.copy(), vehicle_config, self.frame, sphere_table=self.sphere_table)
+            w0, lbw, ubw, flip, wraps = drone_guess(prov, ws[0], ws[1])
+            guess = ((w0, lbw, ubw), flip, wraps)
+        super().__init__(line, config, vehicle_config, ws_raceline, pmodel or ws_model, guess)
+
+
+class GlobalPointRaceline(_Raceline):
+    frame = 'global'
+    label, color = 'Global PM', [1, 1, 1, 1]
+
+
+class ParametricPointRaceline(_Raceline):
+    frame = 'parametric'
+    label, color = 'Parametric PM', [.5, .5, .5, 1]
+
+
+class GlobalDroneRaceline(_DroneRaceline):
+    frame = 'global'
+    label, color = 'Global Drone', [0, 1, 0, 1]
+    point_cls = GlobalPointRaceline
+
+    def __init__(self, line, config: GlobalRacelineConfig, vehicle_config: DroneConfig, ws_raceline=None,
+                 ws_model=None, generate_ws: bool = True):
+        vehicle_config.global_r = True      # GlobalDroneRaceline._get_model (drone_raceline.py:314-316)
+        super().__init__(line, config, vehicle_config, ws_raceline, ws_model, generate_ws)
+
+
+class ParametricDroneRaceline(_DroneRaceline):
+    frame = 'parametric'
+    label, color = 'Parametric Drone', [1, 0, 0, 1]
+    point_cls = ParametricPointRaceline
+
+    def __init__(self, line, config: ParametricRacelineConfig, vehicle_config: DroneConfig, ws_raceline=None,
+                 ws_model=None, generate_ws: bool = True):
+        super().__init__(line, config, vehicle_config, ws_raceline, ws_model, generate_ws)
