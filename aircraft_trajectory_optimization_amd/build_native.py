@@ -55,7 +55,8 @@ def build(verbose=True, jobs=None) -> str:
     ''' compile and link; returns the library path '''
     os.makedirs(OBJ, exist_ok=True)
     work = [(os.path.join(CSRC, 'ato_capi.hip'), os.path.join(OBJ, 'ato_capi.o'), []),
-            (os.path.join(CSRC, 'ato_hstruct.cpp'), os.path.join(OBJ, 'ato_hstruct.o'), [])]
+            (os.path.join(CSRC, 'ato_hstruct.cpp'), os.path.join(OBJ, 'ato_hstruct.o'), []),
+            (os.path.join(CSRC, 'ato_mesh.hip'), os.path.join(OBJ, 'ato_mesh.o'), [])]
     for i in range(N_INST):
         work.append((os.path.join(CSRC, 'ato_inst.hip'), os.path.join(OBJ, f'ato_inst{i}.o'), [f'-DATO_INST={i}']))
     jobs = jobs or min(len(work), max(1, min(8, os.cpu_count() or 4)))

@@ -17,6 +17,8 @@ static int fail(int code, const std::string& msg) {
     return code;
 }
 
+void ato_internal_set_error(const std::string& msg) { g_last_error = msg; }
+
 #define ATO_HIP(call)                                                                        \
     do {                                                                                     \
         hipError_t e_ = (call);                                                              \

@@ -89,6 +89,7 @@ class AtoProblemDesc(ctypes.Structure):
 
 EXPORTED_SYMBOLS = ('ato_create', 'ato_destroy', 'ato_sizes', 'ato_sparsity', 'ato_bounds',
                     'ato_reserve', 'ato_eval', 'ato_eval_f32', 'ato_hess_sparsity', 'ato_hess_eval',
+                    'ato_mesh_create', 'ato_mesh_destroy', 'ato_mesh_signed_distance',
                     'ato_timing', 'ato_timing_read', 'ato_last_error', 'ato_version')
 
 
@@ -114,11 +115,14 @@ def declare(lib: ctypes.CDLL, prefix: str = 'ato') -> ctypes.CDLL:
         lib.ato_eval_f32.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, vp, vp, vp, vp, vp, vp]
         lib.ato_hess_sparsity.argtypes = [vp, i32p, ctypes.POINTER(i32p), ctypes.POINTER(i32p), i32p]
         lib.ato_hess_eval.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, vp, vp, vp, vp, vp]
+        lib.ato_mesh_create.argtypes = [vp, ctypes.c_int32, vp, ctypes.c_int32, ctypes.POINTER(vp)]
+        lib.ato_mesh_destroy.argtypes = [vp]
+        lib.ato_mesh_signed_distance.argtypes = [vp, ctypes.c_int32, vp, vp, vp, vp]
         lib.ato_timing.argtypes = [vp, ctypes.c_int32]
         lib.ato_timing_read.argtypes = [vp, _c_double_p, _c_double_p, i32p]
         for fn in ('ato_create', 'ato_destroy', 'ato_sizes', 'ato_sparsity', 'ato_bounds', 'ato_reserve',
                    'ato_eval', 'ato_eval_f32', 'ato_hess_sparsity', 'ato_hess_eval', 'ato_timing',
-                   'ato_timing_read'):
+                   'ato_timing_read', 'ato_mesh_create', 'ato_mesh_destroy', 'ato_mesh_signed_distance'):
             getattr(lib, fn).restype = ctypes.c_int
     return lib
 

@@ -3,7 +3,8 @@ Raceline solver classes with the reference's public surface (drone3d/raceline/*.
 
     GlobalDroneRaceline, ParametricDroneRaceline          drone_raceline.py:280-368
     GlobalPointRaceline, ParametricPointRaceline          point_raceline.py:48-74
-    ParametricObstacleDroneRaceline / ...PointRaceline    drone_raceline.py:371-427, point_raceline.py:77-90
+    ParametricObstacleDroneRaceline, ParametricObstaclePointRaceline
+                                                          drone_raceline.py:371-427, point_raceline.py:77-90
 
     solver = XxxRaceline(line, config, vehicle_config[, ...], ws_raceline=None, ws_model=None,
                          generate_ws=True)
@@ -242,3 +243,65 @@ class ParametricDroneRaceline(_DroneRaceline):
     def __init__(self, line, config: ParametricRacelineConfig, vehicle_config: DroneConfig, ws_raceline=None,
                  ws_model=None, generate_ws: bool = True):
         super().__init__(line, config, vehicle_config, ws_raceline, ws_model, generate_ws)
+
+
+class _ObstacleMixin:
+    ''' obstacle-tube rows and the post-solve collision check (base_raceline.py:1254-1327) '''
+
+    def _setup_tube(self, line, config, vehicle_config, mesh_obstacle, tube):
+        self.mesh_obstacle = mesh_obstacle
+        self.tube = tube
+        self.calc_tube_time = -1.0
+        prov = ProblemSpec(line, config.copy(), vehicle_config, 'parametric')
+        if self.tube is None:
+            t0 = time.time()
+            self.tube = mesh_obstacle.compute_plannning_tube(line, prov.node_s, vehicle_config.collision_radius)
+            self.calc_tube_time = time.time() - t0
+        self.sphere_table = self.tube.sphere_table(prov.node_s)
+
+    def _after_setup(self):
+        if self.calc_tube_time > 0:
+            self.setup_time -= self.calc_tube_time
+
+    def _unpack(self, x, feasible) -> RacelineResults:
+        out = super()._unpack(x, feasible)
+        xs = np.array([st.x.to_vec() for st in out.states])
+        d = self.mesh_obstacle.signed_distance(xs)
+        for st, dk in zip(out.states, d):
+            st.d = float(dk)
+        if getattr(self.config, 'verbose', False) and feasible:
+            cr = self.vehicle_config.collision_radius
+            verdict = 'Passed' if d.min() >= cr else 'Failed'
+            print(f'{verdict} Collision Test (min: {d.min():0.3f}m, max: {d.max():0.3f}m, pass: {cr:0.3f}m)')
+        return out
+
+
+class ParametricObstaclePointRaceline(_ObstacleMixin, _Raceline):
+    frame = 'parametric'
+    label, color = 'PM w/ obstacles', [.3, .3, .3, 1]
+
+    def __init__(self, line, config: ParametricRacelineConfig, vehicle_config: PointConfig, mesh_obstacle,
+                 tube=None, ws_raceline=None, ws_model=None):
+        self._setup_tube(line, config, vehicle_config, mesh_obstacle, tube)
+        super().__init__(line, config, vehicle_config, ws_raceline, ws_model)
+        self._after_setup()
+
+
+class ParametricObstacleDroneRaceline(_ObstacleMixin, _DroneRaceline):
+    frame = 'parametric'
+    label, color = 'Drone w/ obstacles', [0, .3, 1, 1]
+    point_cls = ParametricObstaclePointRaceline
+
+    def __init__(self, line, config: ParametricRacelineConfig, vehicle_config: DroneConfig, mesh_obstacle,
+                 tube=None, ws_raceline=None, ws_model=None, generate_ws: bool = True):
+        if generate_ws:
+            # the warm start computes the tube once; the drone reuses it (drone_raceline.py:376-410)
+            ws_solver, ws_raceline, _, _ = _point_guess(ParametricObstaclePointRaceline, line, config,
+                                                        vehicle_config, True, None, (mesh_obstacle,))
+            tube = ws_solver.tube
+            self._pre_ws = ws_solver
+        self._setup_tube(line, config, vehicle_config, mesh_obstacle, tube)
+        super().__init__(line, config, vehicle_config, ws_raceline, ws_model, generate_ws=False)
+        if generate_ws:
+            self.ws_solver = self._pre_ws
+        self._after_setup()

@@ -2,3 +2,4 @@
 from aircraft_trajectory_optimization_amd.raceline.solvers import GlobalDroneRaceline, \
     ParametricDroneRaceline  # noqa: F401
 from aircraft_trajectory_optimization_amd.raceline.solvers import _DroneRaceline as DroneRaceline  # noqa: F401
+from aircraft_trajectory_optimization_amd.raceline.solvers import ParametricObstacleDroneRaceline  # noqa: F401

@@ -146,6 +146,20 @@ int ato_hess_sparsity(ato_handle* h, int32_t* nnz, const int32_t** row_ptr, cons
 int ato_hess_eval(ato_handle* h, int32_t batch, int32_t layout, const double* w, const double* lam,
                   const double* sigma, double* hess, void* stream);
 
+/* Triangle mesh of an obstacle environment (MeshObstacle, drone3d/obstacles/mesh_obstacle.py:18-161;
+ * replaces trimesh.proximity.signed_distance / closest_point). vertices [nv][3], faces [nf][3]
+ * (0-based triangles), host arrays copied at creation. */
+typedef struct ato_mesh ato_mesh;
+int ato_mesh_create(const double* vertices, int32_t n_vertices, const int32_t* faces, int32_t n_faces,
+                    ato_mesh** out);
+int ato_mesh_destroy(ato_mesh* mesh);
+
+/* Signed distance of n points (device [n][3]) to the mesh into dist (device [n]): positive
+ * outside, negative inside (ray-crossing parity). closest (device [n][3], may be NULL) gets the
+ * closest surface point. Asynchronous on stream. */
+int ato_mesh_signed_distance(ato_mesh* mesh, int32_t n, const double* points, double* dist, double* closest,
+                             void* stream);
+
 /* Per-kernel timing with HIP events recorded on the evaluation stream. ato_timing(h, n)
  * allocates n event slots and starts recording (n = 0 stops); while on, each ato_eval
  * records events around its Jacobian kernel and its cost-reduction kernel. ato_timing_read
