@@ -39,6 +39,7 @@ def parse():
     ap.add_argument('--layout', choices=['interleaved', 'instance'], default='interleaved')
     ap.add_argument('--cpu-seconds', type=float, default=15.0, help='budget of the oracle CPU baseline')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-solve', action='store_true', help='skip the single-instance interior-point solve')
     ap.add_argument('--traffic-json', default=os.path.join(ROOT, 'profiles', 'traffic_latest.json'))
     return ap.parse_args()
 
@@ -62,6 +63,36 @@ def cpu_baseline(spec_kwargs, W, budget_s):
     return {'value': n / dt, 'unit': 'evals/s', 'cores': 1, 'kind': 'port',
             'sample': f'{n} instances of the same 50x4x13 racetrack workload: oracle g + complex-step '
                       f'dense J + f + grad f, numpy fp64, single thread, {dt:.1f} s'}
+
+
+def single_solve(dev):
+    '''
+    BASELINE config 2: the racetrack 50x4 drone NLP solved to IPOPT tolerance for ONE instance,
+    every evaluation (g, J, f, grad f, Lagrangian Hessian) on the GPU, the interior-point
+    iteration and its KKT factorisation on the host (warm-started from the point-mass solve as
+    race.py's use_ws does). Reported beside the batched evaluation throughput; the batched
+    on-device KKT is the next step.
+    '''
+    from aircraft_trajectory_optimization_amd.raceline.evaluator import DeviceEvaluator
+    from aircraft_trajectory_optimization_amd.solver.ipm import InteriorPointSolver, IPMOptions
+    from aircraft_trajectory_optimization_amd.tracks import make_spec, make_warm_spec
+    kw = dict(track='race', frame='parametric', N=50, K=4)
+    pspec = make_spec(model='point', use_quat=False, **kw)
+    pev = DeviceEvaluator(pspec, device=dev)
+    t0 = time.perf_counter()
+    pres = InteriorPointSolver(pev, pspec.lbw, pspec.ubw, pev.lbg, pev.ubg, IPMOptions(max_iter=1000)).solve(pspec.w0)
+    t_ws = time.perf_counter() - t0
+    spec = make_warm_spec(pres.x, **kw)
+    ev = DeviceEvaluator(spec, device=dev)
+    t0 = time.perf_counter()
+    res = InteriorPointSolver(ev, spec.lbw, spec.ubw, ev.lbg, ev.ubg, IPMOptions(max_iter=1000)).solve(spec.w0)
+    t = time.perf_counter() - t0
+    return {'workload': 'racetrack_parametric_esp_drone_colloc_N50_K4 (single instance, point-mass warm start)',
+            'status': res.status, 'iterations': res.iters, 'lap_time_s': float(res.x[:spec.N].sum()),
+            'solve_s': t, 'iterations_per_s': res.iters / t, 'feval_s': ev.feval_time,
+            'warm_start': {'status': pres.status, 'iterations': pres.iters, 'solve_s': t_ws,
+                           'lap_time_s': float(pres.x[:pspec.N].sum())},
+            'lap_time_vs_casadi': 'unpinned (no IPOPT reachable here)'}
 
 
 def main():
@@ -156,6 +187,8 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             out['cpu_baseline'] = cpu_baseline(spec_kwargs, W, args.cpu_seconds)
+        if world == 1 and not args.no_solve:
+            out['solve'] = single_solve(dev)
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()

@@ -32,26 +32,26 @@ for s in $STEPS; do
         tests) run pytest_gpu 600 python -m pytest tests -m gpu -q -x -p no:cacheprovider ;;
         smoke) run smoke 300 python -c 'import __graft_entry__ as g; g.smoke()' ;;
         bench) run bench 400 python bench.py --steps 50 --warmup 10 ;;
-        bench32) run bench_f32 300 python bench.py --steps 50 --warmup 10 --dtype f32 --no-cpu-baseline ;;
-        benchim) run bench_im 300 python bench.py --steps 50 --warmup 10 --layout instance --no-cpu-baseline ;;
-        benchbig) run bench_b4096 300 python bench.py --steps 20 --warmup 5 --batch 4096 --no-cpu-baseline ;;
+        bench32) run bench_f32 300 python bench.py --steps 50 --warmup 10 --dtype f32 --no-cpu-baseline --no-solve ;;
+        benchim) run bench_im 300 python bench.py --steps 50 --warmup 10 --layout instance --no-cpu-baseline --no-solve ;;
+        benchbig) run bench_b4096 300 python bench.py --steps 20 --warmup 5 --batch 4096 --no-cpu-baseline --no-solve ;;
         prof)  run prof 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
-                   python bench.py --steps 50 --warmup 10 --no-cpu-baseline ;;
+                   python bench.py --steps 50 --warmup 10 --no-cpu-baseline --no-solve ;;
         pmc)   run pmc_fetch 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- \
-                   python bench.py --steps 20 --warmup 5 --no-cpu-baseline
+                   python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-solve
                run pmc_write 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \
-                   python bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
+                   python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-solve ;;
         pmcsq) run pmc_sq 400 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
                    SQ_INSTS_VALU SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD --output-format csv -d "$OUT/pmc_sq" -o run -- \
-                   python bench.py --steps 20 --warmup 5 --no-cpu-baseline
+                   python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-solve
                run pmc_tcc 400 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d "$OUT/pmc_tcc" -o run -- \
-                   python bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
+                   python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-solve ;;
         listpmc) run listpmc 120 rocprofv3 -L ;;
         mbpmc) run mb_fetch 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/mb_fetch" -o run -- ./tools/mb_store
                run mb_write 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/mb_write" -o run -- ./tools/mb_store ;;
         units) for k in 0 1 2 3 4 12 34; do
                    export ATO_DEBUG_UNITS=$k
-                   run bench_units$k 200 python bench.py --steps 30 --warmup 5 --no-cpu-baseline
+                   run bench_units$k 200 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-solve
                    unset ATO_DEBUG_UNITS
                done ;;
         *) echo "unknown step $s" ;;
