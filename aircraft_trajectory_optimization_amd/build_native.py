@@ -24,7 +24,7 @@ FLAGS = ['-std=c++20', '-O3', f'--offload-arch={ARCH}', '-fPIC', '-I', os.path.j
 
 
 def _deps():
-    return glob.glob(os.path.join(CSRC, '*.hpp')) + [os.path.join(REPO, 'include', 'ato.h')]
+    return glob.glob(os.path.join(CSRC, '*.hpp')) + glob.glob(os.path.join(REPO, 'include', '*.h'))
 
 
 def _stale(target, sources):
@@ -56,7 +56,8 @@ def build(verbose=True, jobs=None) -> str:
     os.makedirs(OBJ, exist_ok=True)
     work = [(os.path.join(CSRC, 'ato_capi.hip'), os.path.join(OBJ, 'ato_capi.o'), []),
             (os.path.join(CSRC, 'ato_hstruct.cpp'), os.path.join(OBJ, 'ato_hstruct.o'), []),
-            (os.path.join(CSRC, 'ato_mesh.hip'), os.path.join(OBJ, 'ato_mesh.o'), [])]
+            (os.path.join(CSRC, 'ato_mesh.hip'), os.path.join(OBJ, 'ato_mesh.o'), []),
+            (os.path.join(CSRC, 'ato_kkt.hip'), os.path.join(OBJ, 'ato_kkt.o'), [])]
     for i in range(N_INST):
         work.append((os.path.join(CSRC, 'ato_inst.hip'), os.path.join(OBJ, f'ato_inst{i}.o'), [f'-DATO_INST={i}']))
     jobs = jobs or min(len(work), max(1, min(8, os.cpu_count() or 4)))

@@ -1,0 +1,890 @@
+// ato_kkt.hip -- batched staged LDL^T factorisation and solve of the interior-point KKT system
+// (include/ato_kkt.h). Replaces IPOPT's MUMPS / MA97 factorisation (ref:
+// drone3d/raceline/base_raceline.py:752-799, the `ipopt_time` of :182-189) for a batch of
+// independent instances; the plan tables come from solver/kkt_plan.py.
+//
+// Factor (k_kkt_factor<T>): one 1024-thread workgroup per instance walks the stages. The
+// augmented block of a stage (<= 32*T positions) lives in REGISTERS: thread (ti, tj) = (tid % 32,
+// tid / 32) holds A[32 I + ti][32 J + tj] for every lower tile J <= I (T(T+1)/2 doubles).
+// Assembly goes through a 32-row LDS strip per tile row (entries scattered from the H / J /
+// diagonal arrays, plus the Schur complement carried from the previous stage). Own positions
+// are then eliminated by Bunch-Kaufman pivoting (1x1 or 2x2; candidates and the pivot search
+// restricted to own positions): the pivot column(s) are copied to LDS by their owners, every
+// wave reduces the same max / argmax, and every thread applies the rank-1 / rank-2 update to
+// its tiles (tiles without live rows are skipped). The factor columns are written compactly
+// (live positions only, physical order) into one contiguous stream per instance, with a pivot
+// record and the inverse pivot block per step. The trailing block (next stage's coupling rows +
+// border) goes to LDS and is added into the next stage's assembly.
+//
+// Solve (k_kkt_solve<T>): one 256-thread workgroup per instance. Wave 0 runs the forward
+// (L y = b), D and backward (L^T x = z) sweeps with the stage vector in registers (4 positions
+// per lane); all four waves stream the factor columns through a two-slot LDS ring so that
+// the sweep reads LDS only.
+#include <hip/hip_runtime.h>
+#include <string>
+#include <vector>
+#include <cstdint>
+#include "../../include/ato_kkt.h"
+#include "../../include/ato.h"
+
+void ato_internal_set_error(const std::string& msg);   // ato_capi.hip: ato_last_error()
+
+struct ato_kkt {
+    int n = 0, m = 0, dim = 0, S = 0, T = 0, max_tq = 0, max_ent = 0;
+    int64_t l_size = 0;
+    int32_t *d_stage_ptr = nullptr, *d_n_own = nullptr, *d_pos_index = nullptr, *d_carry_dst = nullptr;
+    int32_t *d_ent_ptr = nullptr, *d_ent_pos = nullptr, *d_ent_src = nullptr, *d_piv_off = nullptr;
+    int32_t cap = 0;                 // instances with factor storage
+    double* d_L = nullptr;           // [cap][l_size]
+    int2* d_piv = nullptr;           // [cap][dim] {p | type << 16, r}
+    double* d_dinv = nullptr;        // [cap][dim][3]
+    int2* d_sinfo = nullptr;         // [cap][S] {steps, stream offset of the stage}
+};
+
+namespace {
+
+int fail(int code, const std::string& m) {
+    ato_internal_set_error(m);
+    return code;
+}
+
+#define KKT_HIP(call)                                                                               \
+    do {                                                                                            \
+        hipError_t e_ = (call);                                                                     \
+        if (e_ != hipSuccess) return fail(ATO_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+constexpr int FT = 1024;                  // factor threads per instance
+constexpr int ST = 256;                   // solve threads per instance
+constexpr int EPT = 4;                    // entries per thread and stage (<= 4096 per stage)
+constexpr int CH = 2048;                  // doubles per ring chunk of the solve
+constexpr int CPT = CH / ST;              // chunk doubles per thread
+constexpr double BK_ALPHA = 0.64038820320220756872767623199676;   // (1 + sqrt(17)) / 8
+constexpr int SRC_SHIFT = 29;
+
+struct Plan {
+    int n, m, dim, S, max_tq;
+    const int* stage_ptr;
+    const int* n_own;
+    const int* pos_index;
+    const int* carry_dst;
+    const int* ent_ptr;
+    const int* ent_pos;
+    const int2* ent_src;
+    const int* piv_off;
+    long long l_size;
+};
+
+struct Vals {
+    const double* H;
+    const double* J;
+    const double* dx;
+    const double* dr;
+    long long se, sb;
+};
+
+__device__ __forceinline__ double src_value(const Vals& v, int code, int b) {
+    if (code < 0) return 0.0;
+    const int kind = code >> SRC_SHIFT;
+    const long long idx = code & ((1 << SRC_SHIFT) - 1);
+    const double* p = kind == 0 ? v.H : kind == 1 ? v.J : kind == 2 ? v.dx : v.dr;
+    if (!p) return 0.0;
+    return p[idx * v.se + (long long)b * v.sb];
+}
+
+template <int NW>
+struct Mask {
+    unsigned long long w[NW];
+    __device__ __forceinline__ bool get(int i) const { return (w[i >> 6] >> (i & 63)) & 1ull; }
+    __device__ __forceinline__ void clear(int i) { w[i >> 6] &= ~(1ull << (i & 63)); }
+    __device__ __forceinline__ void set(int i) { w[i >> 6] |= 1ull << (i & 63); }
+    __device__ __forceinline__ int count() const {
+        int c = 0;
+#pragma unroll
+        for (int k = 0; k < NW; ++k) c += __popcll(w[k]);
+        return c;
+    }
+    // live positions strictly below i
+    __device__ __forceinline__ int below(int i) const {
+        int c = 0;
+        const int wi = i >> 6;
+#pragma unroll
+        for (int k = 0; k < NW; ++k) {
+            if (k < wi) c += __popcll(w[k]);
+            else if (k == wi) c += __popcll(w[k] & ((1ull << (i & 63)) - 1ull));
+        }
+        return c;
+    }
+    __device__ __forceinline__ bool any_in_tile(int I) const {   // positions 32I .. 32I+31
+        return ((w[I >> 1] >> ((I & 1) * 32)) & 0xffffffffull) != 0ull;
+    }
+    __device__ __forceinline__ void set_range(int lo, int hi) {   // [lo, hi)
+#pragma unroll
+        for (int k = 0; k < NW; ++k) {
+            const int l = min(max(lo - 64 * k, 0), 64), h = min(max(hi - 64 * k, 0), 64);
+            const unsigned long long mh = h >= 64 ? ~0ull : ((1ull << h) - 1ull);
+            const unsigned long long ml = l >= 64 ? ~0ull : ((1ull << l) - 1ull);
+            w[k] = mh & ~ml;
+        }
+    }
+};
+
+// max |v| with the smallest index on ties, over the 64 lanes of a wave (all lanes get it)
+__device__ __forceinline__ void wave_argmax(double& v, int& i) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const double ov = __shfl_xor(v, off, 64);
+        const int oi = __shfl_xor(i, off, 64);
+        if (ov > v || (ov == v && oi < i)) {
+            v = ov;
+            i = oi;
+        }
+    }
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+constexpr int slot(int I, int J) { return I * (I + 1) / 2 + J; }
+
+// ------------------------------------------------------------------------------------------
+// factorisation
+// ------------------------------------------------------------------------------------------
+template <int T>
+__device__ __forceinline__ void extract_column(const double (&a)[T * (T + 1) / 2], int k, int ti, int tj,
+                                               double* __restrict__ c) {
+    const int K = k >> 5, kk = k & 31;
+#pragma unroll
+    for (int KK = 0; KK < T; ++KK) {
+        if (K == KK) {
+            if (tj == kk) {
+#pragma unroll
+                for (int I = KK; I < T; ++I) c[32 * I + ti] = a[slot(I, KK)];
+            }
+            if (ti == kk) {
+#pragma unroll
+                for (int J = 0; J < KK; ++J) c[32 * J + tj] = a[slot(KK, J)];
+            }
+        }
+    }
+}
+
+template <int T>
+__global__ __launch_bounds__(FT) void k_kkt_factor(Plan P, Vals V, int batch, const int* __restrict__ list,
+                                                   double* __restrict__ Lst, int2* __restrict__ piv,
+                                                   double* __restrict__ dinv, int2* __restrict__ sinfo,
+                                                   int* __restrict__ inertia) {
+    constexpr int NP = 32 * T;
+    constexpr int NW = (NP + 63) / 64;
+    constexpr int NS = T * (T + 1) / 2;
+    constexpr int SR = NP + 1;                   // strip row stride (odd: conflict-free reads)
+    extern __shared__ double smem[];
+    double* strip = smem;                        // [32][SR]
+    double* colb = strip + 32 * SR;              // [2 parity][2 (k, r)][NP]
+    double* carry = colb + 4 * NP;               // [max_tq][max_tq]
+    int* cdst = reinterpret_cast<int*>(carry + P.max_tq * P.max_tq);   // [max_tq]
+
+    const int bi = blockIdx.x;
+    if (bi >= batch) return;
+    const int b = list ? list[bi] : bi;
+    const int tid = threadIdx.x;
+    const int ti = tid & 31, tj = tid >> 5;
+    const int lane = tid & 63;
+
+    double a[NS];
+    double* Lb = Lst + (long long)b * P.l_size;
+    int2* pv = piv + (long long)b * P.dim;
+    double* dv = dinv + (long long)b * P.dim * 3;
+    int npos = 0, nneg = 0, nzero = 0;
+    long long loff = 0;                          // running offset in the instance's column stream
+    int tq_in = 0;
+
+    for (int s = 0; s < P.S; ++s) {
+        const int p0 = P.stage_ptr[s];
+        const int A = P.stage_ptr[s + 1] - p0;
+        const int own = P.n_own[s];
+        // ---- prefetch this stage's entries (positions and values) into registers
+        const int e0 = P.ent_ptr[s * T], e1 = P.ent_ptr[(s + 1) * T];
+        int epos[EPT];
+        double eval[EPT];
+#pragma unroll
+        for (int q = 0; q < EPT; ++q) {
+            const int e = e0 + tid + q * FT;
+            epos[q] = -1;
+            eval[q] = 0.0;
+            if (e < e1) {
+                epos[q] = P.ent_pos[e];
+                const int2 sc = P.ent_src[e];
+                eval[q] = src_value(V, sc.x, b) + src_value(V, sc.y, b);
+            }
+        }
+        // ---- assemble strip by strip
+#pragma unroll
+        for (int I = 0; I < T; ++I) {
+            if (32 * I < A) {
+                for (int i = tid; i < 32 * SR; i += FT) strip[i] = 0.0;
+                __syncthreads();
+#pragma unroll
+                for (int q = 0; q < EPT; ++q) {
+                    const int pa = epos[q] >> 16, pb = epos[q] & 0xffff;
+                    if (epos[q] >= 0 && (pa >> 5) == I) {
+                        strip[(pa & 31) * SR + pb] = eval[q];
+                        if ((pb >> 5) == I && pa != pb) strip[(pb & 31) * SR + pa] = eval[q];
+                    }
+                }
+                __syncthreads();
+                // carry-in: Schur complement of the previous stage (full symmetric tq x tq)
+                for (int e = tid; e < tq_in * tq_in; e += FT) {
+                    const int q1 = e / tq_in, q2 = e - q1 * tq_in;
+                    const int d1 = cdst[q1], d2 = cdst[q2];
+                    if ((d1 >> 5) == I) strip[(d1 & 31) * SR + d2] += carry[q1 * P.max_tq + q2];
+                }
+                __syncthreads();
+#pragma unroll
+                for (int J = 0; J <= I; ++J) a[slot(I, J)] = strip[ti * SR + 32 * J + tj];
+                __syncthreads();
+            } else {
+#pragma unroll
+                for (int J = 0; J <= I; ++J) a[slot(I, J)] = 0.0;
+            }
+        }
+        // ---- restricted Bunch-Kaufman elimination of the own positions
+        Mask<NW> live;
+        live.set_range(0, A);
+        int kc = 0, steps = 0, par = 0;
+        const int g0 = P.piv_off[s];
+        const long long lstart = loff;
+        while (true) {
+            while (kc < own && !live.get(kc)) ++kc;
+            if (kc >= own) break;
+            const int k = kc;
+            double* ck = colb + (par * 2 + 0) * NP;
+            double* cr = colb + (par * 2 + 1) * NP;
+            extract_column<T>(a, k, ti, tj, ck);
+            __syncthreads();
+            // lambda = max_{i eligible, i != k} |A_ik|
+            double lam = -1.0;
+            int r = NP;
+#pragma unroll
+            for (int q = 0; q < NP / 64 + (NP % 64 ? 1 : 0); ++q) {
+                const int i = lane + 64 * q;
+                if (i < own && i != k && live.get(i)) {
+                    const double v = fabs(ck[i]);
+                    if (v > lam || (v == lam && i < r)) {
+                        lam = v;
+                        r = i;
+                    }
+                }
+            }
+            wave_argmax(lam, r);
+            r = __builtin_amdgcn_readfirstlane(r);
+            if (lam < 0.0) lam = 0.0;
+            const double akk = ck[k];
+            int type;            // 0: 1x1 at p, 1: 2x2 (k, r), 2: zero column
+            int p = k;
+            double* cp = ck;
+            if (r >= own) {                 // no other eligible position: lambda = 0
+                type = akk == 0.0 ? 2 : 0;
+            } else if (lam == 0.0 && akk == 0.0) {
+                type = 2;
+            } else if (fabs(akk) >= BK_ALPHA * lam) {
+                type = 0;
+            } else {
+                extract_column<T>(a, r, ti, tj, cr);
+                __syncthreads();
+                double sig = -1.0;
+                int dummy = 0;
+#pragma unroll
+                for (int q = 0; q < NP / 64 + (NP % 64 ? 1 : 0); ++q) {
+                    const int i = lane + 64 * q;
+                    if (i < own && i != r && live.get(i)) sig = fmax(sig, fabs(cr[i]));
+                }
+                wave_argmax(sig, dummy);
+                if (sig < 0.0) sig = 0.0;
+                if (fabs(akk) * sig >= BK_ALPHA * lam * lam) {
+                    type = 0;
+                } else if (fabs(cr[r]) >= BK_ALPHA * sig) {
+                    type = 0;
+                    p = r;
+                    cp = cr;
+                } else {
+                    type = 1;
+                }
+            }
+            // ---- pivot record, inertia, factor columns, Schur update (decision is wave-uniform)
+            type = __builtin_amdgcn_readfirstlane(type);
+            p = __builtin_amdgcn_readfirstlane(p);
+            cp = type == 0 && p == r && p != k ? cr : ck;
+            double i00 = 0.0, i01 = 0.0, i11 = 0.0;
+            if (type == 2) {
+                live.clear(k);
+                ++nzero;
+            } else if (type == 0) {
+                const double d = cp[p];
+                i00 = 1.0 / d;
+                live.clear(p);
+                if (d > 0.0) ++npos; else ++nneg;
+            } else {
+                const double A00 = ck[k], A01 = ck[r], A11 = cr[r];
+                const double det = A00 * A11 - A01 * A01;
+                i00 = A11 / det;
+                i01 = -A01 / det;
+                i11 = A00 / det;
+                live.clear(k);
+                live.clear(r);
+                if (det < 0.0) { ++npos; ++nneg; }
+                else if (A00 + A11 > 0.0) npos += 2;
+                else nneg += 2;
+            }
+            const int nlive = live.count();
+            const int ncol = type == 1 ? 2 : 1;
+            if (tid == 0) {
+                pv[g0 + steps] = make_int2((type == 1 ? k : p) | (type << 16), type == 1 ? r : -1);
+                dv[3 * (g0 + steps) + 0] = i00;
+                dv[3 * (g0 + steps) + 1] = i01;
+                dv[3 * (g0 + steps) + 2] = i11;
+            }
+            if (tid < A && live.get(tid)) {
+                const int ci = live.below(tid);
+                if (type == 0) {
+                    Lb[loff + ci] = cp[tid] * i00;
+                } else if (type == 1) {
+                    Lb[loff + 2 * ci] = ck[tid] * i00 + cr[tid] * i01;
+                    Lb[loff + 2 * ci + 1] = ck[tid] * i01 + cr[tid] * i11;
+                } else {
+                    Lb[loff + ci] = 0.0;
+                }
+            }
+            loff += (long long)nlive * ncol;
+            // Schur update: one rank-1 pass (1x1 pivot) or two (2x2 pivot: A -= lk ck^T + lr cr^T)
+            const int npass = type == 0 ? 1 : type == 1 ? 2 : 0;
+            for (int pass = 0; pass < npass; ++pass) {
+                const double* cc = type == 0 ? cp : (pass == 0 ? ck : cr);
+                const double fa = type == 0 ? i00 : (pass == 0 ? i00 : i01);
+                const double fb = type == 0 ? 0.0 : (pass == 0 ? i01 : i11);
+                double cj[T];
+#pragma unroll
+                for (int J = 0; J < T; ++J) {
+                    const int j = 32 * J + tj;
+                    cj[J] = live.get(j) ? cc[j] : 0.0;
+                }
+#pragma unroll
+                for (int I = 0; I < T; ++I) {
+                    if (live.any_in_tile(I)) {
+                        const int i = 32 * I + ti;
+                        const double li = live.get(i) ? (type == 0 ? cp[i] * fa : ck[i] * fa + cr[i] * fb) : 0.0;
+#pragma unroll
+                        for (int J = 0; J <= I; ++J)
+                            if (live.any_in_tile(J)) a[slot(I, J)] = fma(-li, cj[J], a[slot(I, J)]);
+                    }
+                }
+            }
+            ++steps;
+            par ^= 1;
+        }
+        if (tid == 0) sinfo[(long long)b * P.S + s] = make_int2(steps, (int)lstart);
+        // ---- trailing Schur complement -> carry for the next stage
+        const int tq = A - own;
+        if (s + 1 < P.S) {
+#pragma unroll
+            for (int I = 0; I < T; ++I) {
+#pragma unroll
+                for (int J = 0; J <= I; ++J) {
+                    const int i = 32 * I + ti, j = 32 * J + tj;
+                    if (i >= own && i < A && j >= own && j < A) {
+                        carry[(i - own) * P.max_tq + (j - own)] = a[slot(I, J)];
+                        carry[(j - own) * P.max_tq + (i - own)] = a[slot(I, J)];
+                    }
+                }
+            }
+            if (tid < tq) cdst[tid] = P.carry_dst[p0 + own + tid];
+            tq_in = tq;
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        inertia[3 * b + 0] = npos;
+        inertia[3 * b + 1] = nneg;
+        inertia[3 * b + 2] = nzero;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// solve
+// ------------------------------------------------------------------------------------------
+// Stream of factor columns through a two-slot LDS ring. Forward: chunks 0, 1, 2, ... of
+// [0, total); backward: the same chunks in reverse. Chunk c lives in slot c & 1.
+struct Ring {
+    double* buf;           // [2][CH]
+    __device__ __forceinline__ double at(long long off) const { return buf[off & (2 * CH - 1)]; }
+};
+
+__device__ __forceinline__ void ring_load(const double* __restrict__ src, long long total, long long c,
+                                          double (&r)[CPT], int tid) {
+#pragma unroll
+    for (int q = 0; q < CPT; ++q) {
+        const long long o = c * CH + q * ST + tid;
+        r[q] = (c >= 0 && o < total) ? src[o] : 0.0;
+    }
+}
+
+__device__ __forceinline__ void ring_store(double* buf, long long c, const double (&r)[CPT], int tid) {
+    double* dst = buf + (c & 1) * CH;
+#pragma unroll
+    for (int q = 0; q < CPT; ++q) dst[q * ST + tid] = r[q];
+}
+
+template <int NQ>
+__device__ __forceinline__ double lane_get(const double (&y)[NQ], int p) {
+    const int q = p >> 6;
+    double v = y[0];
+#pragma unroll
+    for (int k = 1; k < NQ; ++k) v = q == k ? y[k] : v;
+    return __shfl(v, p & 63, 64);
+}
+
+template <int NQ>
+__device__ __forceinline__ void lane_set(double (&y)[NQ], int p, double v, int lane) {
+    if ((p & 63) == lane) {
+#pragma unroll
+        for (int k = 0; k < NQ; ++k)
+            if ((p >> 6) == k) y[k] = v;
+    }
+}
+
+template <int T>
+__global__ __launch_bounds__(ST) void k_kkt_solve(Plan P, int batch, const int* __restrict__ list,
+                                                  const double* __restrict__ Lst, const int2* __restrict__ piv,
+                                                  const double* __restrict__ dinv, const int2* __restrict__ sinfo,
+                                                  double* __restrict__ x, long long se, long long sb) {
+    constexpr int NP = 32 * T;
+    constexpr int NW = (NP + 63) / 64;
+    constexpr int NQ = (NP + 63) / 64;
+    __shared__ double ring_buf[2 * CH];
+    __shared__ double cvec[2][NP];            // carried trailing values (forward) / stage vector (backward)
+    __shared__ int s_done;
+
+    const int bi = blockIdx.x;
+    if (bi >= batch) return;
+    const int b = list ? list[bi] : bi;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const bool w0 = tid < 64;
+    const double* Lb = Lst + (long long)b * P.l_size;
+    const int2* pv = piv + (long long)b * P.dim;
+    const double* dvp = dinv + (long long)b * P.dim * 3;
+    const int2* si = sinfo + (long long)b * P.S;
+    double* xb = x + (long long)b * sb;
+    Ring ring{ring_buf};
+    double stage_r[CPT];
+
+    // total stream length
+    const int2 last = si[P.S - 1];
+    long long total = last.y;
+    {
+        // stream length of the last stage: sum over its steps of live-after counts
+        const int s = P.S - 1;
+        const int A = P.stage_ptr[s + 1] - P.stage_ptr[s];
+        int alive = A;
+        const int nst = min(max(last.x, 0), P.n_own[s]);
+        for (int t = 0; t < nst; ++t) {
+            const int2 rec = pv[P.piv_off[s] + t];
+            const int type = rec.x >> 16;
+            alive -= type == 1 ? 2 : 1;
+            total += (long long)alive * (type == 1 ? 2 : 1);
+        }
+    }
+    const long long nchunks = (total + CH - 1) / CH;
+
+    // ===================== forward: L y = b, then y <- D^{-1} y per stage =====================
+    // wave-0 state
+    double y[NQ];
+    Mask<NW> live;
+    int s = -1, t = 0, steps = 0, A = 0, own = 0, p0 = 0, g0 = 0;
+    long long off = 0;
+    bool finished = false;
+    if (tid == 0) s_done = 0;
+    for (int i = tid; i < 2 * NP; i += ST) (&cvec[0][0])[i] = 0.0;
+    // prime chunks 0 and 1
+    ring_load(Lb, total, 0, stage_r, tid);
+    ring_store(ring.buf, 0, stage_r, tid);
+    ring_load(Lb, total, 1, stage_r, tid);
+    ring_store(ring.buf, 1, stage_r, tid);
+    __syncthreads();
+    for (long long c = 0;; ++c) {
+        ring_load(Lb, total, c + 2, stage_r, tid);     // in flight while wave 0 sweeps
+        if (w0 && !finished) {
+            const long long limit = (c + 2) * CH;
+            while (true) {
+                if (s < 0 || t >= steps) {
+                    // ---- close the current stage: D solve, write own, carry trailing
+                    if (s >= 0) {
+                        for (int u = 0; u < steps; ++u) {
+                            const int2 rec = pv[g0 + u];
+                            const int type = rec.x >> 16, pp = min(rec.x & 0xffff, NP - 1);
+                            const double d0 = dvp[3 * (g0 + u)], d1 = dvp[3 * (g0 + u) + 1],
+                                         d2 = dvp[3 * (g0 + u) + 2];
+                            if (type == 1) {
+                                const int rr = min(max(rec.y, 0), NP - 1);
+                                const double yp = lane_get<NQ>(y, pp), yr = lane_get<NQ>(y, rr);
+                                lane_set<NQ>(y, pp, d0 * yp + d1 * yr, lane);
+                                lane_set<NQ>(y, rr, d1 * yp + d2 * yr, lane);
+                            } else {
+                                lane_set<NQ>(y, pp, d0 * lane_get<NQ>(y, pp), lane);
+                            }
+                        }
+                        const int nb = (s + 1) & 1;
+#pragma unroll
+                        for (int q = 0; q < NQ; ++q) {
+                            const int i = lane + 64 * q;
+                            if (i < own) xb[(long long)P.pos_index[p0 + i] * se] = y[q];
+                        }
+                        for (int i = lane; i < NP; i += 64) cvec[nb][i] = 0.0;
+                        __builtin_amdgcn_wave_barrier();
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+#pragma unroll
+                        for (int q = 0; q < NQ; ++q) {
+                            const int i = lane + 64 * q;
+                            if (i >= own && i < A && s + 1 < P.S) cvec[nb][P.carry_dst[p0 + i]] = y[q];
+                        }
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                        __builtin_amdgcn_wave_barrier();
+                    }
+                    ++s;
+                    if (s >= P.S) {
+                        finished = true;
+                        break;
+                    }
+                    // ---- open stage s
+                    p0 = P.stage_ptr[s];
+                    A = P.stage_ptr[s + 1] - p0;
+                    own = P.n_own[s];
+                    g0 = P.piv_off[s];
+                    const int2 inf = si[s];
+                    steps = min(max(inf.x, 0), own);
+                    off = inf.y;
+                    t = 0;
+                    const int cb = s & 1;
+#pragma unroll
+                    for (int q = 0; q < NQ; ++q) {
+                        const int i = lane + 64 * q;
+                        double v = 0.0;
+                        if (i < own) v = xb[(long long)P.pos_index[p0 + i] * se];
+                        if (i < A) v += cvec[cb][i];
+                        y[q] = v;
+                    }
+                    live.set_range(0, A);
+                    continue;
+                }
+                const int2 rec = pv[g0 + t];
+                const int type = rec.x >> 16, pp = min(rec.x & 0xffff, NP - 1), rr = min(max(rec.y, 0), NP - 1);
+                Mask<NW> nl = live;
+                nl.clear(pp);
+                if (type == 1) nl.clear(rr);
+                const int nlive = nl.count();
+                const int ncol = type == 1 ? 2 : 1;
+                if (off + (long long)nlive * ncol > limit) break;     // column not resident yet
+                const double zp = lane_get<NQ>(y, pp);
+                const double zr = type == 1 ? lane_get<NQ>(y, rr) : 0.0;
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) {
+                    const int i = lane + 64 * q;
+                    if (i < A && nl.get(i)) {
+                        const int ci = nl.below(i);
+                        if (type == 1)
+                            y[q] -= ring.at(off + 2 * ci) * zp + ring.at(off + 2 * ci + 1) * zr;
+                        else
+                            y[q] -= ring.at(off + ci) * zp;
+                    }
+                }
+                off += (long long)nlive * ncol;
+                live = nl;
+                ++t;
+            }
+            if (finished && lane == 0) s_done = 1;
+        }
+        __syncthreads();
+        const bool done = s_done != 0;
+        if (done) break;
+        ring_store(ring.buf, c + 2, stage_r, tid);
+        __syncthreads();
+        if (c + 2 > nchunks + 2) break;               // safety: never loop past the stream
+    }
+    __syncthreads();
+    // make the forward results (written by wave 0) visible to the whole workgroup
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+
+    // ===================== backward: L^T x = z, stages and steps in reverse =====================
+    if (tid == 0) s_done = 0;
+    const long long clast = nchunks - 1;
+    ring_load(Lb, total, clast, stage_r, tid);
+    ring_store(ring.buf, clast, stage_r, tid);
+    ring_load(Lb, total, clast - 1, stage_r, tid);
+    ring_store(ring.buf, clast - 1, stage_r, tid);
+    __syncthreads();
+    s = P.S;
+    t = -1;
+    finished = false;
+    long long oend = 0;
+    for (long long c = clast;; --c) {
+        ring_load(Lb, total, c - 2, stage_r, tid);
+        if (w0 && !finished) {
+            const long long lower = (c - 1) * CH;          // chunks c-1 and c are resident
+            while (true) {
+                if (s >= P.S || t < 0) {
+                    if (s < P.S) {
+                        // ---- close stage s: write own positions, keep the stage vector for s-1
+#pragma unroll
+                        for (int q = 0; q < NQ; ++q) {
+                            const int i = lane + 64 * q;
+                            if (i < own) xb[(long long)P.pos_index[p0 + i] * se] = y[q];
+                            if (i < A) cvec[s & 1][i] = y[q];
+                        }
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                        __builtin_amdgcn_wave_barrier();
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                    }
+                    --s;
+                    if (s < 0) {
+                        finished = true;
+                        break;
+                    }
+                    p0 = P.stage_ptr[s];
+                    A = P.stage_ptr[s + 1] - p0;
+                    own = P.n_own[s];
+                    g0 = P.piv_off[s];
+                    const int2 inf = si[s];
+                    steps = min(max(inf.x, 0), own);
+                    // stream end of this stage = start of the next one (or total)
+                    oend = s + 1 < P.S ? (long long)si[s + 1].y : total;
+                    off = oend;
+                    t = steps - 1;
+                    const int nb = (s + 1) & 1;
+#pragma unroll
+                    for (int q = 0; q < NQ; ++q) {
+                        const int i = lane + 64 * q;
+                        double v = 0.0;
+                        if (i < own) v = xb[(long long)P.pos_index[p0 + i] * se];
+                        else if (i < A) v = cvec[nb][P.carry_dst[p0 + i]];
+                        y[q] = v;
+                    }
+                    live.set_range(own, A);
+                    continue;
+                }
+                const int2 rec = pv[g0 + t];
+                const int type = rec.x >> 16, pp = min(rec.x & 0xffff, NP - 1), rr = min(max(rec.y, 0), NP - 1);
+                const int nlive = live.count();
+                const int ncol = type == 1 ? 2 : 1;
+                const long long o = off - (long long)nlive * ncol;
+                if (o < lower) break;                             // column not resident yet
+                double sp = 0.0, sr = 0.0;
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) {
+                    const int i = lane + 64 * q;
+                    if (i < A && live.get(i)) {
+                        const int ci = live.below(i);
+                        if (type == 1) {
+                            sp += ring.at(o + 2 * ci) * y[q];
+                            sr += ring.at(o + 2 * ci + 1) * y[q];
+                        } else {
+                            sp += ring.at(o + ci) * y[q];
+                        }
+                    }
+                }
+                sp = wave_sum(sp);
+                lane_set<NQ>(y, pp, lane_get<NQ>(y, pp) - sp, lane);
+                live.set(pp);
+                if (type == 1) {
+                    sr = wave_sum(sr);
+                    lane_set<NQ>(y, rr, lane_get<NQ>(y, rr) - sr, lane);
+                    live.set(rr);
+                }
+                off = o;
+                --t;
+            }
+            if (finished && lane == 0) s_done = 1;
+        }
+        __syncthreads();
+        if (s_done != 0) break;
+        ring_store(ring.buf, c - 2, stage_r, tid);
+        __syncthreads();
+        if (c < -2) break;                                // safety
+    }
+}
+
+template <int T>
+int launch_factor(const ato_kkt* h, const Plan& P, const Vals& V, int batch, const int* list, int* inertia,
+                  hipStream_t st) {
+    constexpr int NP = 32 * T;
+    const size_t lds = sizeof(double) * (32 * (NP + 1) + 4 * NP + (size_t)h->max_tq * h->max_tq) +
+                       sizeof(int) * h->max_tq;
+    if (lds > 160 * 1024) return fail(ATO_ERR_UNSUPPORTED, "KKT factor: LDS need exceeds 160 KB");
+    hipLaunchKernelGGL(k_kkt_factor<T>, dim3(batch), dim3(FT), lds, st, P, V, batch, list, h->d_L, h->d_piv,
+                       h->d_dinv, h->d_sinfo, inertia);
+    KKT_HIP(hipGetLastError());
+    return ATO_OK;
+}
+
+template <int T>
+int launch_solve(const ato_kkt* h, const Plan& P, int batch, const int* list, double* x, long long se,
+                 long long sb, hipStream_t st) {
+    hipLaunchKernelGGL(k_kkt_solve<T>, dim3(batch), dim3(ST), 0, st, P, batch, list, h->d_L, h->d_piv, h->d_dinv,
+                       h->d_sinfo, x, se, sb);
+    KKT_HIP(hipGetLastError());
+    return ATO_OK;
+}
+
+Plan make_plan(const ato_kkt* h) {
+    Plan P;
+    P.n = h->n;
+    P.m = h->m;
+    P.dim = h->dim;
+    P.S = h->S;
+    P.max_tq = h->max_tq;
+    P.stage_ptr = h->d_stage_ptr;
+    P.n_own = h->d_n_own;
+    P.pos_index = h->d_pos_index;
+    P.carry_dst = h->d_carry_dst;
+    P.ent_ptr = h->d_ent_ptr;
+    P.ent_pos = h->d_ent_pos;
+    P.ent_src = reinterpret_cast<const int2*>(h->d_ent_src);
+    P.piv_off = h->d_piv_off;
+    P.l_size = h->l_size;
+    return P;
+}
+
+template <class V>
+int upload(const V* host, size_t n, V** dev) {
+    *dev = nullptr;
+    if (n == 0) return ATO_OK;
+    KKT_HIP(hipMalloc((void**)dev, n * sizeof(V)));
+    KKT_HIP(hipMemcpy(*dev, host, n * sizeof(V), hipMemcpyHostToDevice));
+    return ATO_OK;
+}
+
+void free_storage(ato_kkt* h) {
+    (void)hipFree(h->d_L);
+    (void)hipFree(h->d_piv);
+    (void)hipFree(h->d_dinv);
+    (void)hipFree(h->d_sinfo);
+    h->d_L = nullptr;
+    h->d_piv = nullptr;
+    h->d_dinv = nullptr;
+    h->d_sinfo = nullptr;
+    h->cap = 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ato_kkt_create(const ato_kkt_plan_desc* d, ato_kkt** out) {
+    if (!d || !out) return fail(ATO_ERR_ARG, "null argument");
+    *out = nullptr;
+    if (d->tiles < 1 || d->tiles > 8) return fail(ATO_ERR_UNSUPPORTED, "KKT blocks wider than 256 positions");
+    if (d->n_stages < 1 || d->n < 0 || d->m < 0) return fail(ATO_ERR_ARG, "bad KKT plan sizes");
+    ato_kkt* h = new ato_kkt();
+    h->n = d->n;
+    h->m = d->m;
+    h->dim = d->n + d->m;
+    h->S = d->n_stages;
+    h->T = d->tiles;
+    h->l_size = d->l_size;
+    const int S = d->n_stages;
+    const int P = d->stage_ptr[S];
+    const int E = d->ent_ptr[S * d->tiles];
+    for (int s = 0; s < S; ++s) {
+        const int A = d->stage_ptr[s + 1] - d->stage_ptr[s];
+        if (A > 32 * d->tiles || d->n_own[s] > A) {
+            delete h;
+            return fail(ATO_ERR_ARG, "KKT plan: stage larger than its tiles");
+        }
+        h->max_tq = std::max(h->max_tq, A - d->n_own[s]);
+        const int es = d->ent_ptr[(s + 1) * d->tiles] - d->ent_ptr[s * d->tiles];
+        h->max_ent = std::max(h->max_ent, es);
+    }
+    if (h->max_ent > EPT * FT) {
+        delete h;
+        return fail(ATO_ERR_UNSUPPORTED, "KKT plan: more than 4096 entries in one stage");
+    }
+    int rc = ATO_OK;
+    if ((rc = upload(d->stage_ptr, S + 1, &h->d_stage_ptr)) || (rc = upload(d->n_own, S, &h->d_n_own)) ||
+        (rc = upload(d->pos_index, P, &h->d_pos_index)) || (rc = upload(d->carry_dst, P, &h->d_carry_dst)) ||
+        (rc = upload(d->ent_ptr, S * d->tiles + 1, &h->d_ent_ptr)) || (rc = upload(d->ent_pos, E, &h->d_ent_pos)) ||
+        (rc = upload(d->ent_src, 2 * (size_t)E, &h->d_ent_src)) || (rc = upload(d->piv_off, S, &h->d_piv_off))) {
+        ato_kkt_destroy(h);
+        return rc;
+    }
+    *out = h;
+    return ATO_OK;
+}
+
+int ato_kkt_destroy(ato_kkt* h) {
+    if (!h) return ATO_OK;
+    free_storage(h);
+    for (int32_t* p : {h->d_stage_ptr, h->d_n_own, h->d_pos_index, h->d_carry_dst, h->d_ent_ptr, h->d_ent_pos,
+                       h->d_ent_src, h->d_piv_off})
+        (void)hipFree(p);
+    delete h;
+    return ATO_OK;
+}
+
+int ato_kkt_reserve(ato_kkt* h, int32_t max_batch) {
+    if (!h || max_batch < 0) return fail(ATO_ERR_ARG, "bad argument");
+    if (max_batch <= h->cap) return ATO_OK;
+    free_storage(h);
+    KKT_HIP(hipMalloc((void**)&h->d_L, sizeof(double) * (size_t)h->l_size * max_batch));
+    KKT_HIP(hipMalloc((void**)&h->d_piv, sizeof(int2) * (size_t)h->dim * max_batch));
+    KKT_HIP(hipMalloc((void**)&h->d_dinv, sizeof(double) * 3 * (size_t)h->dim * max_batch));
+    KKT_HIP(hipMalloc((void**)&h->d_sinfo, sizeof(int2) * (size_t)h->S * max_batch));
+    h->cap = max_batch;
+    return ATO_OK;
+}
+
+int ato_kkt_factor(ato_kkt* h, int32_t batch, const int32_t* list, int64_t se, int64_t sb, const double* H,
+                   const double* J, const double* dx, const double* dr, int32_t* inertia, void* stream) {
+    if (!h || !inertia || batch < 0) return fail(ATO_ERR_ARG, "bad argument");
+    if (batch == 0) return ATO_OK;
+    if (!list && batch > h->cap) return fail(ATO_ERR_STATE, "ato_kkt_reserve() too small for this batch");
+    if (!h->d_L) return fail(ATO_ERR_STATE, "call ato_kkt_reserve() first");
+    const Plan P = make_plan(h);
+    const Vals V{H, J, dx, dr, se, sb};
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    switch (h->T) {
+        case 1: return launch_factor<1>(h, P, V, batch, list, inertia, st);
+        case 2: return launch_factor<2>(h, P, V, batch, list, inertia, st);
+        case 3: return launch_factor<3>(h, P, V, batch, list, inertia, st);
+        case 4: return launch_factor<4>(h, P, V, batch, list, inertia, st);
+        case 5: return launch_factor<5>(h, P, V, batch, list, inertia, st);
+        case 6: return launch_factor<6>(h, P, V, batch, list, inertia, st);
+        case 7: return launch_factor<7>(h, P, V, batch, list, inertia, st);
+        case 8: return launch_factor<8>(h, P, V, batch, list, inertia, st);
+        default: return fail(ATO_ERR_UNSUPPORTED, "KKT tiles");
+    }
+}
+
+int ato_kkt_solve(ato_kkt* h, int32_t batch, const int32_t* list, int64_t se, int64_t sb, double* x,
+                  void* stream) {
+    if (!h || !x || batch < 0) return fail(ATO_ERR_ARG, "bad argument");
+    if (batch == 0) return ATO_OK;
+    if (!h->d_L) return fail(ATO_ERR_STATE, "call ato_kkt_reserve() first");
+    if (!list && batch > h->cap) return fail(ATO_ERR_STATE, "ato_kkt_reserve() too small for this batch");
+    const Plan P = make_plan(h);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    switch (h->T) {
+        case 1: return launch_solve<1>(h, P, batch, list, x, se, sb, st);
+        case 2: return launch_solve<2>(h, P, batch, list, x, se, sb, st);
+        case 3: return launch_solve<3>(h, P, batch, list, x, se, sb, st);
+        case 4: return launch_solve<4>(h, P, batch, list, x, se, sb, st);
+        case 5: return launch_solve<5>(h, P, batch, list, x, se, sb, st);
+        case 6: return launch_solve<6>(h, P, batch, list, x, se, sb, st);
+        case 7: return launch_solve<7>(h, P, batch, list, x, se, sb, st);
+        case 8: return launch_solve<8>(h, P, batch, list, x, se, sb, st);
+        default: return fail(ATO_ERR_UNSUPPORTED, "KKT tiles");
+    }
+}
+
+}  // extern "C"

@@ -1,0 +1,131 @@
+'''
+ctypes / torch wrapper of the batched device KKT factorisation (include/ato_kkt.h).
+
+One DeviceKKT per problem structure and device. Values are torch tensors on the device in
+the INTERLEAVED batch layout ([element][B], the evaluation library's default), so the
+Hessian and Jacobian values written by ato_hess_eval / ato_eval are factorised in place
+without a transpose. There is no CPU fallback: without libato.so this raises.
+'''
+import ctypes
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+
+from aircraft_trajectory_optimization_amd import native
+from aircraft_trajectory_optimization_amd.solver.kkt_plan import KKTPlan
+
+_i32p = ctypes.POINTER(ctypes.c_int32)
+_i64p = ctypes.POINTER(ctypes.c_int64)
+
+
+class AtoKKTPlanDesc(ctypes.Structure):
+    ''' mirror of ato_kkt_plan_desc '''
+    _fields_ = [
+        ('n', ctypes.c_int32),
+        ('m', ctypes.c_int32),
+        ('n_stages', ctypes.c_int32),
+        ('tiles', ctypes.c_int32),
+        ('stage_ptr', _i32p),
+        ('n_own', _i32p),
+        ('pos_index', _i32p),
+        ('carry_dst', _i32p),
+        ('ent_ptr', _i32p),
+        ('ent_pos', _i32p),
+        ('ent_src', _i32p),
+        ('l_off', _i64p),
+        ('l_size', ctypes.c_int64),
+        ('piv_off', _i32p),
+    ]
+
+
+class DeviceKKT:
+    ''' staged Bunch-Kaufman LDL^T of the KKT matrix for a batch of instances on one device '''
+
+    def __init__(self, plan: KKTPlan, max_batch: int, device: Optional[torch.device] = None):
+        self.lib = native.load()
+        self.plan = plan
+        self.device = device or torch.device('cuda', torch.cuda.current_device())
+        self._keep = []
+
+        def arr(a, dt, pt):
+            a = np.ascontiguousarray(a, dtype=dt)
+            self._keep.append(a)
+            return a.ctypes.data_as(pt)
+
+        d = AtoKKTPlanDesc()
+        d.n, d.m, d.n_stages, d.tiles = plan.n, plan.m, plan.n_stages, plan.tiles
+        d.stage_ptr = arr(plan.stage_ptr, np.int32, _i32p)
+        d.n_own = arr(plan.n_own, np.int32, _i32p)
+        d.pos_index = arr(plan.pos_index, np.int32, _i32p)
+        d.carry_dst = arr(plan.carry_dst, np.int32, _i32p)
+        d.ent_ptr = arr(plan.ent_ptr, np.int32, _i32p)
+        d.ent_pos = arr(plan.ent_pos, np.int32, _i32p)
+        d.ent_src = arr(plan.ent_src.reshape(-1), np.int32, _i32p)
+        d.l_off = arr(plan.l_off, np.int64, _i64p)
+        d.l_size = plan.l_size
+        d.piv_off = arr(plan.piv_off, np.int32, _i32p)
+        self.desc = d
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            self._check(self.lib.ato_kkt_create(ctypes.byref(d), ctypes.byref(h)))
+            self.handle = h
+            self.cap = int(max_batch)
+            self._check(self.lib.ato_kkt_reserve(h, self.cap))
+        self.inertia = torch.zeros((self.cap, 3), dtype=torch.int32, device=self.device)
+
+    def _check(self, rc):
+        if rc != 0:
+            raise RuntimeError(f'libato KKT error {rc}: {self.lib.ato_last_error().decode()}')
+
+    def _list(self, idx: Optional[Sequence[int]]):
+        if idx is None:
+            return None, self.cap
+        idx = np.asarray(idx, dtype=np.int32).reshape(-1)
+        if len(idx) and (idx.min() < 0 or idx.max() >= self.cap):
+            raise ValueError(f'instance index out of range [0, {self.cap})')
+        t = torch.as_tensor(idx, device=self.device)
+        return t, len(idx)
+
+    def factor(self, H: Optional[torch.Tensor], J: torch.Tensor, dx: torch.Tensor, dr: torch.Tensor,
+               instances: Optional[Sequence[int]] = None, stream=None) -> torch.Tensor:
+        '''
+        Factorise K = [[W + diag(dx), J^T], [J, diag(dr)]] for the listed instances (all when None).
+        H [nnz_h][B] lower-CSR Hessian values (None: W = 0), J [nnz_j][B], dx [n][B], dr [m][B],
+        all fp64 interleaved with B = max_batch. Returns the inertia tensor [B][3] (device).
+        '''
+        B = self.cap
+        for t, rows in ((J, None), (dx, self.plan.n), (dr, self.plan.m)) + (((H, None),) if H is not None else ()):
+            if t.dtype != torch.float64 or t.dim() != 2 or t.shape[1] != B or not t.is_contiguous():
+                raise ValueError('KKT values must be contiguous fp64 [elements][max_batch] tensors')
+            if rows is not None and t.shape[0] != rows:
+                raise ValueError('diagonal of the wrong length')
+        lst, nb = self._list(instances)
+        st = stream if stream is not None else torch.cuda.current_stream(self.device)
+        self._check(self.lib.ato_kkt_factor(self.handle, nb, lst.data_ptr() if lst is not None else None, B, 1,
+                                            H.data_ptr() if H is not None else None, J.data_ptr(), dx.data_ptr(),
+                                            dr.data_ptr(), self.inertia.data_ptr(), st.cuda_stream))
+        self._last_list = lst
+        return self.inertia
+
+    def solve(self, x: torch.Tensor, instances: Optional[Sequence[int]] = None, stream=None) -> torch.Tensor:
+        ''' in place: x [dim][B] holds the right-hand sides (KKT order) and receives the solutions '''
+        if x.dtype != torch.float64 or x.shape != (self.plan.dim, self.cap) or not x.is_contiguous():
+            raise ValueError('x must be a contiguous fp64 [dim][max_batch] tensor')
+        lst, nb = self._list(instances)
+        st = stream if stream is not None else torch.cuda.current_stream(self.device)
+        self._check(self.lib.ato_kkt_solve(self.handle, nb, lst.data_ptr() if lst is not None else None, self.cap, 1,
+                                           x.data_ptr(), st.cuda_stream))
+        self._last_list = lst
+        return x
+
+    def close(self):
+        if getattr(self, 'handle', None):
+            self.lib.ato_kkt_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # pylint: disable=broad-except
+            pass

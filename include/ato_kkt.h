@@ -1,0 +1,76 @@
+/*
+ * ato_kkt.h -- batched factorisation and solve of the interior-point KKT system on the
+ * device (part of libato.so).
+ *
+ * What it replaces. IPOPT, called by the reference through
+ *     ca.nlpsol('solver', 'ipopt', ...)   drone3d/raceline/base_raceline.py:752-799
+ * factorises its augmented system with MUMPS (or HSL MA97, :765-782) on every iteration
+ * and reads the inertia from that factorisation; that is most of the reference's
+ * `ipopt_time` (base_raceline.py:182-189). Here the same system
+ *
+ *     K = [ W + diag_x   J^T    ]      W: Lagrangian Hessian (lower CSR, ato_hess_sparsity)
+ *         [ J            diag_r ]      J: constraint Jacobian  (CSR, ato_sparsity)
+ *
+ * is factorised for a BATCH of instances at once, one workgroup per instance, with a staged
+ * symmetric-indefinite LDL^T: the KKT indices are ordered by interval (stage), each stage's
+ * augmented block (its own variables and rows, the next stage's coupling rows and the border
+ * rows) is held in registers, its own positions are eliminated with Bunch-Kaufman pivoting,
+ * and the trailing Schur complement is carried to the next stage. The inertia (n+, n-, n0)
+ * of K is returned per instance -- what IPOPT's inertia correction needs.
+ *
+ * The structure tables come from solver/kkt_plan.py (host analysis of the two sparsity
+ * patterns). All value pointers are DEVICE pointers; element e of instance b of every value
+ * array (H, J, diag_x, diag_r, x) is at [e * stride_elem + b * stride_inst], so both the
+ * interleaved ([e][B]: stride_elem = B, stride_inst = 1) and the instance-major layout work.
+ */
+#ifndef ATO_KKT_H
+#define ATO_KKT_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ato_kkt_plan_desc {
+    int32_t n, m;               /* variables, constraint rows (KKT dim = n + m)              */
+    int32_t n_stages;           /* intervals + 1 border pseudo-stage                         */
+    int32_t tiles;              /* 32-wide register tiles of the largest block (<= 8)         */
+    const int32_t* stage_ptr;   /* [n_stages + 1] offsets into pos_index / carry_dst          */
+    const int32_t* n_own;       /* [n_stages] eligible (own) positions of every stage         */
+    const int32_t* pos_index;   /* [P] KKT index of every augmented position                  */
+    const int32_t* carry_dst;   /* [P] trailing position -> position in the next stage, or -1 */
+    const int32_t* ent_ptr;     /* [n_stages * tiles + 1] entries of (stage, 32-row strip)    */
+    const int32_t* ent_pos;     /* [E] (pa << 16) | pb, pa >= pb                               */
+    const int32_t* ent_src;     /* [E][2] (kind << 29) | index; kind 0 H, 1 J, 2 diag_x,       *
+                                 * 3 diag_r; -1 = none. The value is the sum of both sources. */
+    const int64_t* l_off;       /* [n_stages] factor-column offset of every stage (doubles)   */
+    int64_t l_size;             /* factor-column doubles per instance                        */
+    const int32_t* piv_off;     /* [n_stages] pivot-record offset of every stage              */
+} ato_kkt_plan_desc;
+
+typedef struct ato_kkt ato_kkt;
+
+int ato_kkt_create(const ato_kkt_plan_desc* desc, ato_kkt** out);
+int ato_kkt_destroy(ato_kkt* kkt);
+
+/* Device storage of the factors of instances 0 .. max_batch-1 (about l_size doubles each). */
+int ato_kkt_reserve(ato_kkt* kkt, int32_t max_batch);
+
+/* Factorise K for `batch` instances: instance list[i] (device int32 array; NULL = 0..batch-1)
+ * is factorised into its own storage slot. H may be NULL (W = 0). inertia: device int32
+ * [max_batch][3] = (positive, negative, zero) pivots, written for the listed instances.
+ * Asynchronous on stream. */
+int ato_kkt_factor(ato_kkt* kkt, int32_t batch, const int32_t* list, int64_t stride_elem,
+                   int64_t stride_inst, const double* H, const double* J, const double* diag_x,
+                   const double* diag_r, int32_t* inertia, void* stream);
+
+/* Solve K x = rhs in place (x holds rhs on entry, KKT order: variables then rows) with the
+ * factors of the listed instances. Asynchronous on stream. */
+int ato_kkt_solve(ato_kkt* kkt, int32_t batch, const int32_t* list, int64_t stride_elem,
+                  int64_t stride_inst, double* x, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ATO_KKT_H */

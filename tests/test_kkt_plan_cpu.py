@@ -1,0 +1,56 @@
+'''
+The staged KKT plan (solver/kkt_plan.py) on CPU: the test-only numpy emulation of the device
+algorithm (tests/kkt_emulation.py: restricted Bunch-Kaufman per stage, Schur carry, compact
+factor columns) solves K x = b and reports the inertia of the dense matrix, on random
+Hessian / Jacobian values of real problem structures.
+'''
+import numpy as np
+import pytest
+
+from aircraft_trajectory_optimization_amd.solver.kkt_plan import MAX_TILES, TILE, build_plan
+from tests.helpers import HostEvaluator, product_spec, random_w, var_stages
+from tests.kkt_emulation import Factor, dense_kkt
+
+CASES = [dict(track='fig8', N=5, K=3), dict(track='race', frame='global', N=7, K=2),
+         dict(track='race', N=7, K=2, rk4=True), dict(track='race', N=6, K=4),
+         dict(track='race', model='point', use_quat=False, N=8, K=3)]
+IDS = ['fig8-colloc', 'race-global', 'race-rk4', 'race-K4', 'point']
+
+
+def random_kkt_values(spec, seed):
+    ev = HostEvaluator(spec)
+    rng = np.random.default_rng(seed)
+    w = random_w(spec, rng)
+    _, _, _, jv = ev.eval(w)
+    H = ev.hess(w, rng.standard_normal(ev.ng), 1.0)
+    dx = np.abs(rng.standard_normal(ev.nw)) + 0.1
+    dr = -(np.abs(rng.standard_normal(ev.ng)) * 1e-2 + 1e-3)
+    return ev, H, jv, dx, dr
+
+
+@pytest.mark.parametrize('cfg', CASES, ids=IDS)
+def test_plan_emulation_matches_dense(cfg):
+    spec = product_spec(**cfg)
+    ev, H, jv, dx, dr = random_kkt_values(spec, 0)
+    plan = build_plan(ev.nw, ev.ng, var_stages(spec), ev.j_row_ptr, ev.j_col, ev.h_row_ptr, ev.h_col)
+    assert plan.tiles <= MAX_TILES and plan.max_block <= plan.tiles * TILE
+    # every KKT index is own in exactly one stage
+    own = np.concatenate([plan.pos_index[plan.stage_ptr[s]:plan.stage_ptr[s] + plan.n_own[s]]
+                          for s in range(plan.n_stages)])
+    assert np.array_equal(np.sort(own), np.arange(plan.dim))
+    K = dense_kkt(plan, H, jv, dx, dr, ev.h_row_ptr, ev.h_col, ev.j_row_ptr, ev.j_col)
+    f = Factor(plan, H, jv, dx, dr)
+    rhs = np.random.default_rng(1).standard_normal(plan.dim)
+    x = f.solve(rhs)
+    assert np.abs(K @ x - rhs).max() <= 1e-8 * max(1.0, np.abs(rhs).max()) * max(1.0, np.abs(K).max())
+    eig = np.linalg.eigvalsh(K)
+    assert f.inertia == (int((eig > 0).sum()), int((eig < 0).sum()), 0)
+
+
+def test_plan_racetrack_full_size_fits_device_tiles():
+    spec = product_spec(track='race', N=50, K=4)
+    ev = HostEvaluator(spec)
+    plan = build_plan(ev.nw, ev.ng, var_stages(spec), ev.j_row_ptr, ev.j_col, ev.h_row_ptr, ev.h_col)
+    assert plan.n_stages == 51 and plan.tiles == 8
+    assert plan.max_block <= 256
+    assert (np.diff(plan.ent_ptr.reshape(-1)[::plan.tiles]) <= 4096).all()

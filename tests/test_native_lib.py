@@ -1,28 +1,33 @@
 '''
-The C-ABI library: it must exist, load, export exactly what include/ato.h declares, and
+The C-ABI library: it must exist, load, export exactly what include/*.h declare, and
 its ctypes mirror must match the header's struct layout. No compute calls (no GPU here).
 '''
 import ctypes
+import glob
 import os
 import re
 
 from aircraft_trajectory_optimization_amd import native
 
-HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'include', 'ato.h')
+HEADERS = sorted(glob.glob(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'include',
+                                        '*.h')))
 
 
 def _declared():
-    txt = open(HEADER, encoding='utf-8').read()
-    txt = re.sub(r'/\*.*?\*/', '', txt, flags=re.S)
-    return sorted(set(re.findall(r'\b(ato_[a-z0-9_]+)\s*\(', txt)))
+    names = set()
+    for h in HEADERS:
+        txt = open(h, encoding='utf-8').read()
+        txt = re.sub(r'/\*.*?\*/', '', txt, flags=re.S)
+        names |= set(re.findall(r'\b(ato_[a-z0-9_]+)\s*\(', txt))
+    return sorted(names)
 
 
 def test_library_loads_and_exports_header_symbols():
     lib = native.load()
     declared = _declared()
-    assert declared, 'no functions found in include/ato.h'
+    assert declared, 'no functions found in include/*.h'
     for name in declared:
-        assert hasattr(lib, name), f'{name} declared in ato.h but not exported'
+        assert hasattr(lib, name), f'{name} declared in include/*.h but not exported'
     assert set(declared) == set(native.EXPORTED_SYMBOLS)
     assert lib.ato_version().decode().startswith('ato 2')
 
@@ -39,3 +44,11 @@ def test_missing_library_fails_loudly(tmp_path):
     import pytest
     with pytest.raises(RuntimeError):
         native.load(str(tmp_path / 'nope.so'))
+
+
+def test_kkt_plan_desc_layout():
+    from aircraft_trajectory_optimization_amd.solver.kkt_device import AtoKKTPlanDesc
+    # 4 int32, 8 pointers, int64 l_size between them (header field order)
+    assert AtoKKTPlanDesc.stage_ptr.offset == 16
+    assert AtoKKTPlanDesc.l_size.offset == 16 + 8 * 8
+    assert ctypes.sizeof(AtoKKTPlanDesc) == 16 + 8 * 8 + 8 + 8
