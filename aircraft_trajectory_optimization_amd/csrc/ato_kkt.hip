@@ -3,9 +3,10 @@
 // drone3d/raceline/base_raceline.py:752-799, the `ipopt_time` of :182-189) for a batch of
 // independent instances; the plan tables come from solver/kkt_plan.py.
 //
-// Factor (k_kkt_factor<T>): one 1024-thread workgroup per instance walks the stages. The
+// Factor (k_kkt_factor<T>): one 512-thread workgroup per instance walks the stages. The
 // augmented block of a stage (<= 32*T positions) lives in REGISTERS: thread (ti, tj) = (tid % 32,
-// tid / 32) holds A[32 I + ti][32 J + tj] for every lower tile J <= I (T(T+1)/2 doubles).
+// tid / 32) holds A[32 I + ti][32 J + tj] and A[32 I + ti][32 J + 16 + tj] for every lower tile
+// J <= I (T(T+1) doubles; 2 waves per SIMD leave 256 VGPRs per lane).
 // Assembly goes through a 32-row LDS strip per tile row (entries scattered from the H / J /
 // diagonal arrays, plus the Schur complement carried from the previous stage). Own positions
 // are then eliminated by Bunch-Kaufman pivoting (1x1 or 2x2; candidates and the pivot search
@@ -38,10 +39,33 @@ struct ato_kkt {
     double* d_L = nullptr;           // [cap][l_size]
     int2* d_piv = nullptr;           // [cap][dim] {p | type << 16, r}
     double* d_dinv = nullptr;        // [cap][dim][3]
-    int2* d_sinfo = nullptr;         // [cap][S] {steps, stream offset of the stage}
+    int2* d_sinfo = nullptr;         // [cap][S+1] {steps, stream offset of the stage}; [S] = {total, 0}
 };
 
+#ifdef ATO_KKT_STAMPS
+// DIAGNOSTIC build only (tools/diag/kkt_stamps.py): shader-clock phase totals of block 0
+__device__ unsigned long long g_kkt_stamps[16];
+#endif
+
 namespace {
+
+#ifdef ATO_KKT_STAMPS
+__device__ __forceinline__ unsigned long long kstamp() {
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#define KST_DECL unsigned long long kst_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, kst_last = kstamp(); \
+    const bool kst_on = blockIdx.x == 0;
+#define KST(i) do { if (kst_on) { const unsigned long long t_ = kstamp(); kst_acc[i] += t_ - kst_last; kst_last = t_; } } while (0)
+#define KST_DUMP(nsteps) do { if (kst_on && threadIdx.x == 0) { for (int i_ = 0; i_ < 8; ++i_) g_kkt_stamps[i_] = kst_acc[i_]; g_kkt_stamps[8] = (nsteps); } } while (0)
+#else
+#define KST_DECL
+#define KST(i)
+#define KST_DUMP(nsteps)
+#endif
 
 int fail(int code, const std::string& m) {
     ato_internal_set_error(m);
@@ -54,9 +78,9 @@ int fail(int code, const std::string& m) {
         if (e_ != hipSuccess) return fail(ATO_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(e_)); \
     } while (0)
 
-constexpr int FT = 1024;                  // factor threads per instance
+constexpr int FT = 512;                   // factor threads per instance (16 x 32 grid)
 constexpr int ST = 256;                   // solve threads per instance
-constexpr int EPT = 4;                    // entries per thread and stage (<= 4096 per stage)
+constexpr int EPT = 8;                    // entries per thread and stage (<= 4096 per stage)
 constexpr int CH = 2048;                  // doubles per ring chunk of the solve
 constexpr int CPT = CH / ST;              // chunk doubles per thread
 constexpr double BK_ALPHA = 0.64038820320220756872767623199676;   // (1 + sqrt(17)) / 8
@@ -92,12 +116,30 @@ __device__ __forceinline__ double src_value(const Vals& v, int code, int b) {
     return p[idx * v.se + (long long)b * v.sb];
 }
 
+// bit blend a = m ? b : a on doubles through integer ops (a select of two array loads would be
+// folded into a variable-index load and push the whole register array to scratch)
+__device__ __forceinline__ double blend(double a, double b, unsigned long long m) {
+    return __longlong_as_double((__double_as_longlong(a) & ~m) | (__double_as_longlong(b) & m));
+}
+
+// live-position bit mask; every word access uses a compile-time index (no scratch)
 template <int NW>
 struct Mask {
     unsigned long long w[NW];
-    __device__ __forceinline__ bool get(int i) const { return (w[i >> 6] >> (i & 63)) & 1ull; }
-    __device__ __forceinline__ void clear(int i) { w[i >> 6] &= ~(1ull << (i & 63)); }
-    __device__ __forceinline__ void set(int i) { w[i >> 6] |= 1ull << (i & 63); }
+    __device__ __forceinline__ bool get(int i) const {
+        unsigned long long r = 0ull;
+#pragma unroll
+        for (int k = 0; k < NW; ++k) r |= (((i >> 6) == k) ? ~0ull : 0ull) & w[k];
+        return (r >> (i & 63)) & 1ull;
+    }
+    __device__ __forceinline__ void clear(int i) {
+#pragma unroll
+        for (int k = 0; k < NW; ++k) w[k] &= ~((((i >> 6) == k) ? 1ull : 0ull) << (i & 63));
+    }
+    __device__ __forceinline__ void set(int i) {
+#pragma unroll
+        for (int k = 0; k < NW; ++k) w[k] |= (((i >> 6) == k) ? 1ull : 0ull) << (i & 63);
+    }
     __device__ __forceinline__ int count() const {
         int c = 0;
 #pragma unroll
@@ -129,23 +171,58 @@ struct Mask {
     }
 };
 
-// max |v| with the smallest index on ties, over the 64 lanes of a wave (all lanes get it)
-__device__ __forceinline__ void wave_argmax(double& v, int& i) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        const double ov = __shfl_xor(v, off, 64);
-        const int oi = __shfl_xor(i, off, 64);
-        if (ov > v || (ov == v && oi < i)) {
-            v = ov;
-            i = oi;
-        }
-    }
+// LDS-only workgroup barrier: waits for this wave's LDS operations, not for its global stores
+// (the factor columns written every step are read only by the solve launch)
+__device__ __forceinline__ void lds_barrier() { __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+template <int CTRL>
+__device__ __forceinline__ unsigned dpp_u32(unsigned v) {
+    return (unsigned)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, true);
 }
 
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+    const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, true);
+    const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, true);
+    return __hiloint2double(hi, lo);
+}
+
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l),
+                            __builtin_amdgcn_readlane(__double2loint(v), l));
+}
+
+__device__ __forceinline__ double uni(double v) {   // wave-uniform copy (SGPRs)
+    return __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(v)),
+                            __builtin_amdgcn_readfirstlane(__double2loint(v)));
+}
+
+// max over the 64 lanes (all lanes active), returned as a scalar: DPP within each 16-lane row,
+// then the four row results by readlane
+__device__ __forceinline__ unsigned wave_max_u32(unsigned v) {
+    v = max(v, dpp_u32<0xB1>(v));    // quad_perm [1,0,3,2]
+    v = max(v, dpp_u32<0x4E>(v));    // quad_perm [2,3,0,1]
+    v = max(v, dpp_u32<0x141>(v));   // row_half_mirror
+    v = max(v, dpp_u32<0x140>(v));   // row_mirror
+    const unsigned r0 = __builtin_amdgcn_readlane(v, 0), r1 = __builtin_amdgcn_readlane(v, 16);
+    const unsigned r2 = __builtin_amdgcn_readlane(v, 32), r3 = __builtin_amdgcn_readlane(v, 48);
+    return max(max(r0, r1), max(r2, r3));
+}
+
+// sum over the 64 lanes in a fixed order (deterministic), returned wave-uniform
 __device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-    return v;
+    v += dpp_f64<0xB1>(v);
+    v += dpp_f64<0x4E>(v);
+    v += dpp_f64<0x141>(v);
+    v += dpp_f64<0x140>(v);
+    return (readlane_f64(v, 0) + readlane_f64(v, 16)) + (readlane_f64(v, 32) + readlane_f64(v, 48));
+}
+
+// ordering key of |v| at position i (< 512): float magnitude with the low 9 mantissa bits
+// replaced by (511 - i), so the max key is a (near-)largest entry, ties to the smallest index;
+// 0 = no candidate. The pivot tests then use the exact double value at the chosen index.
+__device__ __forceinline__ unsigned mag_key(double v, int i) {
+    return (__float_as_uint((float)fabs(v)) & 0xFFFFFE00u) | (unsigned)(511 - i);
 }
 
 constexpr int slot(int I, int J) { return I * (I + 1) / 2 + J; }
@@ -153,20 +230,26 @@ constexpr int slot(int I, int J) { return I * (I + 1) / 2 + J; }
 // ------------------------------------------------------------------------------------------
 // factorisation
 // ------------------------------------------------------------------------------------------
+// column k of the block into c[0 .. 32T): thread (ti, tj) owns rows 32I+ti and columns 32J+tj,
+// 32J+16+tj of every lower tile (I, J)
 template <int T>
-__device__ __forceinline__ void extract_column(const double (&a)[T * (T + 1) / 2], int k, int ti, int tj,
+__device__ __forceinline__ void extract_column(const double (&a)[T * (T + 1) / 2][2], int k, int ti, int tj,
                                                double* __restrict__ c) {
-    const int K = k >> 5, kk = k & 31;
+    const int K = k >> 5, kk = k & 31, kt = k & 15;
+    const unsigned long long hm = (k & 16) ? ~0ull : 0ull;
 #pragma unroll
     for (int KK = 0; KK < T; ++KK) {
         if (K == KK) {
-            if (tj == kk) {
+            if (tj == kt) {
 #pragma unroll
-                for (int I = KK; I < T; ++I) c[32 * I + ti] = a[slot(I, KK)];
+                for (int I = KK; I < T; ++I) c[32 * I + ti] = blend(a[slot(I, KK)][0], a[slot(I, KK)][1], hm);
             }
             if (ti == kk) {
 #pragma unroll
-                for (int J = 0; J < KK; ++J) c[32 * J + tj] = a[slot(KK, J)];
+                for (int J = 0; J < KK; ++J) {
+                    c[32 * J + tj] = a[slot(KK, J)][0];
+                    c[32 * J + 16 + tj] = a[slot(KK, J)][1];
+                }
             }
         }
     }
@@ -179,6 +262,7 @@ __global__ __launch_bounds__(FT) void k_kkt_factor(Plan P, Vals V, int batch, co
                                                    int* __restrict__ inertia) {
     constexpr int NP = 32 * T;
     constexpr int NW = (NP + 63) / 64;
+    constexpr int NQ = (NP + 63) / 64;
     constexpr int NS = T * (T + 1) / 2;
     constexpr int SR = NP + 1;                   // strip row stride (odd: conflict-free reads)
     extern __shared__ double smem[];
@@ -189,24 +273,26 @@ __global__ __launch_bounds__(FT) void k_kkt_factor(Plan P, Vals V, int batch, co
 
     const int bi = blockIdx.x;
     if (bi >= batch) return;
-    const int b = list ? list[bi] : bi;
+    const int b = list ? __builtin_amdgcn_readfirstlane(list[bi]) : bi;
     const int tid = threadIdx.x;
     const int ti = tid & 31, tj = tid >> 5;
     const int lane = tid & 63;
 
-    double a[NS];
+    double a[NS][2];
     double* Lb = Lst + (long long)b * P.l_size;
     int2* pv = piv + (long long)b * P.dim;
     double* dv = dinv + (long long)b * P.dim * 3;
     int npos = 0, nneg = 0, nzero = 0;
     long long loff = 0;                          // running offset in the instance's column stream
     int tq_in = 0;
+    int kst_steps = 0;
+    KST_DECL
 
     for (int s = 0; s < P.S; ++s) {
         const int p0 = P.stage_ptr[s];
         const int A = P.stage_ptr[s + 1] - p0;
         const int own = P.n_own[s];
-        // ---- prefetch this stage's entries (positions and values) into registers
+        // ---- this stage's entries (positions and values) into registers
         const int e0 = P.ent_ptr[s * T], e1 = P.ent_ptr[(s + 1) * T];
         int epos[EPT];
         double eval[EPT];
@@ -244,14 +330,18 @@ __global__ __launch_bounds__(FT) void k_kkt_factor(Plan P, Vals V, int batch, co
                 }
                 __syncthreads();
 #pragma unroll
-                for (int J = 0; J <= I; ++J) a[slot(I, J)] = strip[ti * SR + 32 * J + tj];
+                for (int J = 0; J <= I; ++J) {
+                    a[slot(I, J)][0] = strip[ti * SR + 32 * J + tj];
+                    a[slot(I, J)][1] = strip[ti * SR + 32 * J + 16 + tj];
+                }
                 __syncthreads();
             } else {
 #pragma unroll
-                for (int J = 0; J <= I; ++J) a[slot(I, J)] = 0.0;
+                for (int J = 0; J <= I; ++J) a[slot(I, J)][0] = a[slot(I, J)][1] = 0.0;
             }
         }
-        // ---- restricted Bunch-Kaufman elimination of the own positions
+        KST(0);     // assembly
+        // ---- restricted Bunch-Kaufman elimination of the own positions (all decisions scalar)
         Mask<NW> live;
         live.set_range(0, A);
         int kc = 0, steps = 0, par = 0;
@@ -263,72 +353,65 @@ __global__ __launch_bounds__(FT) void k_kkt_factor(Plan P, Vals V, int batch, co
             const int k = kc;
             double* ck = colb + (par * 2 + 0) * NP;
             double* cr = colb + (par * 2 + 1) * NP;
+            KST(7);
             extract_column<T>(a, k, ti, tj, ck);
-            __syncthreads();
-            // lambda = max_{i eligible, i != k} |A_ik|
-            double lam = -1.0;
-            int r = NP;
+            lds_barrier();
+            KST(1);     // extract + barrier
+            // lambda = max_{i eligible, i != k} |A_ik| and its index r
+            unsigned key = 0u;
 #pragma unroll
-            for (int q = 0; q < NP / 64 + (NP % 64 ? 1 : 0); ++q) {
+            for (int q = 0; q < NQ; ++q) {
                 const int i = lane + 64 * q;
-                if (i < own && i != k && live.get(i)) {
-                    const double v = fabs(ck[i]);
-                    if (v > lam || (v == lam && i < r)) {
-                        lam = v;
-                        r = i;
-                    }
-                }
+                if (i < own && i != k && live.get(i)) key = max(key, mag_key(ck[i], i));
             }
-            wave_argmax(lam, r);
-            r = __builtin_amdgcn_readfirstlane(r);
-            if (lam < 0.0) lam = 0.0;
-            const double akk = ck[k];
+            key = wave_max_u32(key);
+            const int r = key ? 511 - (int)(key & 0x1FFu) : -1;
+            const double akk = uni(ck[k]);
+            const double lam = r >= 0 ? fabs(uni(ck[r])) : 0.0;
             int type;            // 0: 1x1 at p, 1: 2x2 (k, r), 2: zero column
             int p = k;
-            double* cp = ck;
-            if (r >= own) {                 // no other eligible position: lambda = 0
+            bool use_r = false;
+            if (r < 0 || lam == 0.0) {
                 type = akk == 0.0 ? 2 : 0;
-            } else if (lam == 0.0 && akk == 0.0) {
-                type = 2;
             } else if (fabs(akk) >= BK_ALPHA * lam) {
                 type = 0;
             } else {
                 extract_column<T>(a, r, ti, tj, cr);
-                __syncthreads();
-                double sig = -1.0;
-                int dummy = 0;
+                lds_barrier();
+                unsigned key2 = 0u;
 #pragma unroll
-                for (int q = 0; q < NP / 64 + (NP % 64 ? 1 : 0); ++q) {
+                for (int q = 0; q < NQ; ++q) {
                     const int i = lane + 64 * q;
-                    if (i < own && i != r && live.get(i)) sig = fmax(sig, fabs(cr[i]));
+                    if (i < own && i != r && live.get(i)) key2 = max(key2, mag_key(cr[i], i));
                 }
-                wave_argmax(sig, dummy);
-                if (sig < 0.0) sig = 0.0;
+                key2 = wave_max_u32(key2);
+                const int j2 = key2 ? 511 - (int)(key2 & 0x1FFu) : -1;
+                const double sig = j2 >= 0 ? fabs(uni(cr[j2])) : 0.0;
+                const double arr = uni(cr[r]);
                 if (fabs(akk) * sig >= BK_ALPHA * lam * lam) {
                     type = 0;
-                } else if (fabs(cr[r]) >= BK_ALPHA * sig) {
+                } else if (fabs(arr) >= BK_ALPHA * sig) {
                     type = 0;
                     p = r;
-                    cp = cr;
+                    use_r = true;
                 } else {
                     type = 1;
                 }
             }
-            // ---- pivot record, inertia, factor columns, Schur update (decision is wave-uniform)
-            type = __builtin_amdgcn_readfirstlane(type);
-            p = __builtin_amdgcn_readfirstlane(p);
-            cp = type == 0 && p == r && p != k ? cr : ck;
+            const double* cp = use_r ? cr : ck;
+            KST(2);     // pivot search
+            // ---- pivot record, inertia, factor columns, Schur update
             double i00 = 0.0, i01 = 0.0, i11 = 0.0;
             if (type == 2) {
                 live.clear(k);
                 ++nzero;
             } else if (type == 0) {
-                const double d = cp[p];
+                const double d = uni(cp[p]);
                 i00 = 1.0 / d;
                 live.clear(p);
                 if (d > 0.0) ++npos; else ++nneg;
             } else {
-                const double A00 = ck[k], A01 = ck[r], A11 = cr[r];
+                const double A00 = akk, A01 = uni(ck[r]), A11 = uni(cr[r]);
                 const double det = A00 * A11 - A01 * A01;
                 i00 = A11 / det;
                 i01 = -A01 / det;
@@ -359,33 +442,40 @@ __global__ __launch_bounds__(FT) void k_kkt_factor(Plan P, Vals V, int batch, co
                 }
             }
             loff += (long long)nlive * ncol;
+            KST(3);     // record + factor column stores
             // Schur update: one rank-1 pass (1x1 pivot) or two (2x2 pivot: A -= lk ck^T + lr cr^T)
             const int npass = type == 0 ? 1 : type == 1 ? 2 : 0;
             for (int pass = 0; pass < npass; ++pass) {
                 const double* cc = type == 0 ? cp : (pass == 0 ? ck : cr);
                 const double fa = type == 0 ? i00 : (pass == 0 ? i00 : i01);
                 const double fb = type == 0 ? 0.0 : (pass == 0 ? i01 : i11);
-                double cj[T];
+                // no live masking: a dead row or column only ever feeds dead entries
+                double cj[T][2];
 #pragma unroll
                 for (int J = 0; J < T; ++J) {
-                    const int j = 32 * J + tj;
-                    cj[J] = live.get(j) ? cc[j] : 0.0;
+                    cj[J][0] = cc[32 * J + tj];
+                    cj[J][1] = cc[32 * J + 16 + tj];
                 }
 #pragma unroll
                 for (int I = 0; I < T; ++I) {
                     if (live.any_in_tile(I)) {
                         const int i = 32 * I + ti;
-                        const double li = live.get(i) ? (type == 0 ? cp[i] * fa : ck[i] * fa + cr[i] * fb) : 0.0;
+                        const double li = type == 0 ? cp[i] * fa : ck[i] * fa + cr[i] * fb;
 #pragma unroll
                         for (int J = 0; J <= I; ++J)
-                            if (live.any_in_tile(J)) a[slot(I, J)] = fma(-li, cj[J], a[slot(I, J)]);
+                            if (live.any_in_tile(J)) {
+                                a[slot(I, J)][0] = fma(-li, cj[J][0], a[slot(I, J)][0]);
+                                a[slot(I, J)][1] = fma(-li, cj[J][1], a[slot(I, J)][1]);
+                            }
                     }
                 }
             }
             ++steps;
+            ++kst_steps;
             par ^= 1;
+            KST(4);     // Schur update
         }
-        if (tid == 0) sinfo[(long long)b * P.S + s] = make_int2(steps, (int)lstart);
+        if (tid == 0) sinfo[(long long)b * (P.S + 1) + s] = make_int2(steps, (int)lstart);
         // ---- trailing Schur complement -> carry for the next stage
         const int tq = A - own;
         if (s + 1 < P.S) {
@@ -393,10 +483,13 @@ __global__ __launch_bounds__(FT) void k_kkt_factor(Plan P, Vals V, int batch, co
             for (int I = 0; I < T; ++I) {
 #pragma unroll
                 for (int J = 0; J <= I; ++J) {
-                    const int i = 32 * I + ti, j = 32 * J + tj;
-                    if (i >= own && i < A && j >= own && j < A) {
-                        carry[(i - own) * P.max_tq + (j - own)] = a[slot(I, J)];
-                        carry[(j - own) * P.max_tq + (i - own)] = a[slot(I, J)];
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const int i = 32 * I + ti, j = 32 * J + 16 * h + tj;
+                        if (i >= own && i < A && j >= own && j < A) {
+                            carry[(i - own) * P.max_tq + (j - own)] = a[slot(I, J)][h];
+                            carry[(j - own) * P.max_tq + (i - own)] = a[slot(I, J)][h];
+                        }
                     }
                 }
             }
@@ -405,7 +498,11 @@ __global__ __launch_bounds__(FT) void k_kkt_factor(Plan P, Vals V, int batch, co
         }
         __syncthreads();
     }
+    KST(5);
+    KST_DUMP(kst_steps);
+    (void)kst_steps;
     if (tid == 0) {
+        sinfo[(long long)b * (P.S + 1) + P.S] = make_int2((int)loff, 0);
         inertia[3 * b + 0] = npos;
         inertia[3 * b + 1] = nneg;
         inertia[3 * b + 2] = nzero;
@@ -442,17 +539,28 @@ __device__ __forceinline__ double lane_get(const double (&y)[NQ], int p) {
     const int q = p >> 6;
     double v = y[0];
 #pragma unroll
-    for (int k = 1; k < NQ; ++k) v = q == k ? y[k] : v;
-    return __shfl(v, p & 63, 64);
+    for (int k = 1; k < NQ; ++k) v = blend(v, y[k], q == k ? ~0ull : 0ull);
+    return readlane_f64(v, p & 63);
 }
 
 template <int NQ>
 __device__ __forceinline__ void lane_set(double (&y)[NQ], int p, double v, int lane) {
-    if ((p & 63) == lane) {
 #pragma unroll
-        for (int k = 0; k < NQ; ++k)
-            if ((p >> 6) == k) y[k] = v;
+    for (int k = 0; k < NQ; ++k) y[k] = blend(y[k], v, ((p & 63) == lane && (p >> 6) == k) ? ~0ull : 0ull);
+}
+
+// wave 0: stage the pivot records and inverse pivot blocks of a stage into LDS
+__device__ __forceinline__ void stage_records(const int2* __restrict__ pv, const double* __restrict__ dvp, int g0,
+                                              int steps, int lane, int2* s_piv, double* s_dinv) {
+    for (int u = lane; u < steps; u += 64) {
+        s_piv[u] = pv[g0 + u];
+        s_dinv[3 * u + 0] = dvp[3 * (g0 + u) + 0];
+        s_dinv[3 * u + 1] = dvp[3 * (g0 + u) + 1];
+        s_dinv[3 * u + 2] = dvp[3 * (g0 + u) + 2];
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 template <int T>
@@ -465,42 +573,28 @@ __global__ __launch_bounds__(ST) void k_kkt_solve(Plan P, int batch, const int* 
     constexpr int NQ = (NP + 63) / 64;
     __shared__ double ring_buf[2 * CH];
     __shared__ double cvec[2][NP];            // carried trailing values (forward) / stage vector (backward)
+    __shared__ int2 s_piv[NP];
+    __shared__ double s_dinv[3 * NP];
     __shared__ int s_done;
 
     const int bi = blockIdx.x;
     if (bi >= batch) return;
-    const int b = list ? list[bi] : bi;
+    const int b = list ? __builtin_amdgcn_readfirstlane(list[bi]) : bi;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const bool w0 = tid < 64;
     const double* Lb = Lst + (long long)b * P.l_size;
     const int2* pv = piv + (long long)b * P.dim;
     const double* dvp = dinv + (long long)b * P.dim * 3;
-    const int2* si = sinfo + (long long)b * P.S;
+    const int2* si = sinfo + (long long)b * (P.S + 1);
     double* xb = x + (long long)b * sb;
     Ring ring{ring_buf};
     double stage_r[CPT];
 
-    // total stream length
-    const int2 last = si[P.S - 1];
-    long long total = last.y;
-    {
-        // stream length of the last stage: sum over its steps of live-after counts
-        const int s = P.S - 1;
-        const int A = P.stage_ptr[s + 1] - P.stage_ptr[s];
-        int alive = A;
-        const int nst = min(max(last.x, 0), P.n_own[s]);
-        for (int t = 0; t < nst; ++t) {
-            const int2 rec = pv[P.piv_off[s] + t];
-            const int type = rec.x >> 16;
-            alive -= type == 1 ? 2 : 1;
-            total += (long long)alive * (type == 1 ? 2 : 1);
-        }
-    }
+    const long long total = min((long long)si[P.S].x, P.l_size);
     const long long nchunks = (total + CH - 1) / CH;
 
     // ===================== forward: L y = b, then y <- D^{-1} y per stage =====================
-    // wave-0 state
     double y[NQ];
     Mask<NW> live;
     int s = -1, t = 0, steps = 0, A = 0, own = 0, p0 = 0, g0 = 0;
@@ -508,7 +602,6 @@ __global__ __launch_bounds__(ST) void k_kkt_solve(Plan P, int batch, const int* 
     bool finished = false;
     if (tid == 0) s_done = 0;
     for (int i = tid; i < 2 * NP; i += ST) (&cvec[0][0])[i] = 0.0;
-    // prime chunks 0 and 1
     ring_load(Lb, total, 0, stage_r, tid);
     ring_store(ring.buf, 0, stage_r, tid);
     ring_load(Lb, total, 1, stage_r, tid);
@@ -523,12 +616,12 @@ __global__ __launch_bounds__(ST) void k_kkt_solve(Plan P, int batch, const int* 
                     // ---- close the current stage: D solve, write own, carry trailing
                     if (s >= 0) {
                         for (int u = 0; u < steps; ++u) {
-                            const int2 rec = pv[g0 + u];
-                            const int type = rec.x >> 16, pp = min(rec.x & 0xffff, NP - 1);
-                            const double d0 = dvp[3 * (g0 + u)], d1 = dvp[3 * (g0 + u) + 1],
-                                         d2 = dvp[3 * (g0 + u) + 2];
+                            const int2 rec = s_piv[u];
+                            const int type = __builtin_amdgcn_readfirstlane(rec.x >> 16);
+                            const int pp = __builtin_amdgcn_readfirstlane(min(rec.x & 0xffff, NP - 1));
+                            const double d0 = s_dinv[3 * u], d1 = s_dinv[3 * u + 1], d2 = s_dinv[3 * u + 2];
                             if (type == 1) {
-                                const int rr = min(max(rec.y, 0), NP - 1);
+                                const int rr = __builtin_amdgcn_readfirstlane(min(max(rec.y, 0), NP - 1));
                                 const double yp = lane_get<NQ>(y, pp), yr = lane_get<NQ>(y, rr);
                                 lane_set<NQ>(y, pp, d0 * yp + d1 * yr, lane);
                                 lane_set<NQ>(y, rr, d1 * yp + d2 * yr, lane);
@@ -543,15 +636,17 @@ __global__ __launch_bounds__(ST) void k_kkt_solve(Plan P, int batch, const int* 
                             if (i < own) xb[(long long)P.pos_index[p0 + i] * se] = y[q];
                         }
                         for (int i = lane; i < NP; i += 64) cvec[nb][i] = 0.0;
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                         __builtin_amdgcn_wave_barrier();
-                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
                         for (int q = 0; q < NQ; ++q) {
                             const int i = lane + 64 * q;
                             if (i >= own && i < A && s + 1 < P.S) cvec[nb][P.carry_dst[p0 + i]] = y[q];
                         }
-                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                         __builtin_amdgcn_wave_barrier();
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                     }
                     ++s;
                     if (s >= P.S) {
@@ -567,6 +662,7 @@ __global__ __launch_bounds__(ST) void k_kkt_solve(Plan P, int batch, const int* 
                     steps = min(max(inf.x, 0), own);
                     off = inf.y;
                     t = 0;
+                    stage_records(pv, dvp, g0, steps, lane, s_piv, s_dinv);
                     const int cb = s & 1;
 #pragma unroll
                     for (int q = 0; q < NQ; ++q) {
@@ -579,8 +675,10 @@ __global__ __launch_bounds__(ST) void k_kkt_solve(Plan P, int batch, const int* 
                     live.set_range(0, A);
                     continue;
                 }
-                const int2 rec = pv[g0 + t];
-                const int type = rec.x >> 16, pp = min(rec.x & 0xffff, NP - 1), rr = min(max(rec.y, 0), NP - 1);
+                const int2 rec = s_piv[t];
+                const int type = __builtin_amdgcn_readfirstlane(rec.x >> 16);
+                const int pp = __builtin_amdgcn_readfirstlane(min(rec.x & 0xffff, NP - 1));
+                const int rr = __builtin_amdgcn_readfirstlane(min(max(rec.y, 0), NP - 1));
                 Mask<NW> nl = live;
                 nl.clear(pp);
                 if (type == 1) nl.clear(rr);
@@ -614,8 +712,6 @@ __global__ __launch_bounds__(ST) void k_kkt_solve(Plan P, int batch, const int* 
         if (c + 2 > nchunks + 2) break;               // safety: never loop past the stream
     }
     __syncthreads();
-    // make the forward results (written by wave 0) visible to the whole workgroup
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
 
     // ===================== backward: L^T x = z, stages and steps in reverse =====================
     if (tid == 0) s_done = 0;
@@ -628,7 +724,6 @@ __global__ __launch_bounds__(ST) void k_kkt_solve(Plan P, int batch, const int* 
     s = P.S;
     t = -1;
     finished = false;
-    long long oend = 0;
     for (long long c = clast;; --c) {
         ring_load(Lb, total, c - 2, stage_r, tid);
         if (w0 && !finished) {
@@ -643,9 +738,9 @@ __global__ __launch_bounds__(ST) void k_kkt_solve(Plan P, int batch, const int* 
                             if (i < own) xb[(long long)P.pos_index[p0 + i] * se] = y[q];
                             if (i < A) cvec[s & 1][i] = y[q];
                         }
-                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                         __builtin_amdgcn_wave_barrier();
-                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                     }
                     --s;
                     if (s < 0) {
@@ -658,10 +753,9 @@ __global__ __launch_bounds__(ST) void k_kkt_solve(Plan P, int batch, const int* 
                     g0 = P.piv_off[s];
                     const int2 inf = si[s];
                     steps = min(max(inf.x, 0), own);
-                    // stream end of this stage = start of the next one (or total)
-                    oend = s + 1 < P.S ? (long long)si[s + 1].y : total;
-                    off = oend;
+                    off = s + 1 < P.S ? (long long)si[s + 1].y : total;   // stream end of this stage
                     t = steps - 1;
+                    stage_records(pv, dvp, g0, steps, lane, s_piv, s_dinv);
                     const int nb = (s + 1) & 1;
 #pragma unroll
                     for (int q = 0; q < NQ; ++q) {
@@ -674,8 +768,10 @@ __global__ __launch_bounds__(ST) void k_kkt_solve(Plan P, int batch, const int* 
                     live.set_range(own, A);
                     continue;
                 }
-                const int2 rec = pv[g0 + t];
-                const int type = rec.x >> 16, pp = min(rec.x & 0xffff, NP - 1), rr = min(max(rec.y, 0), NP - 1);
+                const int2 rec = s_piv[t];
+                const int type = __builtin_amdgcn_readfirstlane(rec.x >> 16);
+                const int pp = __builtin_amdgcn_readfirstlane(min(rec.x & 0xffff, NP - 1));
+                const int rr = __builtin_amdgcn_readfirstlane(min(max(rec.y, 0), NP - 1));
                 const int nlive = live.count();
                 const int ncol = type == 1 ? 2 : 1;
                 const long long o = off - (long long)nlive * ncol;
@@ -781,6 +877,13 @@ void free_storage(ato_kkt* h) {
 
 extern "C" {
 
+#ifdef ATO_KKT_STAMPS
+int ato_kkt_diag_stamps(unsigned long long* out) {
+    KKT_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_kkt_stamps), sizeof(unsigned long long) * 16));
+    return ATO_OK;
+}
+#endif
+
 int ato_kkt_create(const ato_kkt_plan_desc* d, ato_kkt** out) {
     if (!d || !out) return fail(ATO_ERR_ARG, "null argument");
     *out = nullptr;
@@ -839,7 +942,7 @@ int ato_kkt_reserve(ato_kkt* h, int32_t max_batch) {
     KKT_HIP(hipMalloc((void**)&h->d_L, sizeof(double) * (size_t)h->l_size * max_batch));
     KKT_HIP(hipMalloc((void**)&h->d_piv, sizeof(int2) * (size_t)h->dim * max_batch));
     KKT_HIP(hipMalloc((void**)&h->d_dinv, sizeof(double) * 3 * (size_t)h->dim * max_batch));
-    KKT_HIP(hipMalloc((void**)&h->d_sinfo, sizeof(int2) * (size_t)h->S * max_batch));
+    KKT_HIP(hipMalloc((void**)&h->d_sinfo, sizeof(int2) * (size_t)(h->S + 1) * max_batch));
     h->cap = max_batch;
     return ATO_OK;
 }

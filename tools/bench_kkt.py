@@ -1,0 +1,85 @@
+'''
+Time the batched device KKT factorisation and solve on the racetrack 50 x 4 structure
+(the bench workload) with KKT values from the real evaluation: Hessian of the Lagrangian at
+seeded w with random multipliers, Jacobian, barrier-like diagonals.
+
+    python tools/bench_kkt.py [--batch 512] [--reps 5]
+'''
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--batch', type=int, default=512)
+    ap.add_argument('--reps', type=int, default=5)
+    ap.add_argument('--N', type=int, default=50)
+    ap.add_argument('--K', type=int, default=4)
+    ap.add_argument('--out', default=None)
+    ap.add_argument('--track', default='race')
+    ap.add_argument('--frame', default='parametric')
+    ap.add_argument('--rk4', action='store_true')
+    a = ap.parse_args()
+    from aircraft_trajectory_optimization_amd.raceline.batched import BatchedNLP
+    from aircraft_trajectory_optimization_amd.raceline.evaluator import variable_stages
+    from aircraft_trajectory_optimization_amd.raceline.instances import seeded_instances
+    from aircraft_trajectory_optimization_amd.solver.kkt_device import DeviceKKT
+    from aircraft_trajectory_optimization_amd.solver.kkt_plan import build_plan
+    from aircraft_trajectory_optimization_amd.tracks import make_spec
+    spec = make_spec(track=a.track, frame=a.frame, N=a.N, K=a.K, rk4=a.rk4)
+    B = a.batch
+    bn = BatchedNLP(spec, B)
+    W, _, _ = seeded_instances(spec, np.arange(B))
+    bn.set_w(W)
+    bn.evaluate()
+    hrp, hcol, _ = bn.problem.hess_sparsity()
+    t0 = time.perf_counter()
+    plan = build_plan(bn.sizes[0], bn.sizes[1], variable_stages(spec), bn.row_ptr, bn.col, hrp, hcol)
+    t_plan = time.perf_counter() - t0
+    g = torch.Generator(device='cuda').manual_seed(0)
+    lam = torch.randn((bn.sizes[1], B), dtype=torch.float64, device='cuda', generator=g)
+    sig = torch.ones(B, dtype=torch.float64, device='cuda')
+    H = bn.hessian(lam, sig)
+    dx = torch.rand((plan.n, B), dtype=torch.float64, device='cuda', generator=g) + 0.1
+    dr = -(torch.rand((plan.m, B), dtype=torch.float64, device='cuda', generator=g) * 1e-2 + 1e-6)
+    kkt = DeviceKKT(plan, B)
+    rhs = torch.randn((plan.dim, B), dtype=torch.float64, device='cuda', generator=g)
+    x = rhs.clone()
+    kkt.factor(H, bn.jac, dx, dr)
+    kkt.solve(x)
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    tf, ts = [], []
+    for _ in range(a.reps):
+        x.copy_(rhs)
+        ev[0].record()
+        kkt.factor(H, bn.jac, dx, dr)
+        ev[1].record()
+        kkt.solve(x)
+        ev[2].record()
+        torch.cuda.synchronize()
+        tf.append(ev[0].elapsed_time(ev[1]))
+        ts.append(ev[1].elapsed_time(ev[2]))
+    inertia = kkt.inertia.cpu().numpy()
+    out = {'batch': B, 'N': a.N, 'K': a.K, 'dim': plan.dim, 'stages': plan.n_stages, 'max_block': plan.max_block,
+           'tiles': plan.tiles, 'plan_s': t_plan, 'factor_ms': float(np.median(tf)), 'solve_ms': float(np.median(ts)),
+           'factor_us_per_instance': float(np.median(tf)) * 1e3 / B,
+           'inertia_ok': int(((inertia[:, 0] == plan.n) & (inertia[:, 1] == plan.m)).sum()),
+           'factor_bytes_per_instance': 8 * plan.l_size,
+           'factor_us_per_step_chain': float(np.median(tf)) * 1e3 / plan.dim}
+    print(json.dumps(out))
+    if a.out:
+        json.dump(out, open(a.out, 'w'), indent=1)
+
+
+if __name__ == '__main__':
+    main()

@@ -1,0 +1,85 @@
+'''
+DIAGNOSTIC ONLY: build tools/diag/libato_kktdiag.so (the library with ato_kkt.hip compiled
+-DATO_KKT_STAMPS) and report where the factor kernel's block 0 spends its shader clocks per
+pivot step (s_memtime stamps on thread 0; barrier waits count into the phase that ends with them).
+
+    python tools/diag/kkt_stamps.py --build-only      (CPU)
+    python tools/diag/kkt_stamps.py [--K 4 --batch 64] (GPU)
+'''
+import argparse
+import ctypes
+import glob
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+LIB = os.path.join(HERE, 'libato_kktdiag.so')
+PHASES = ['assembly', 'extract+barrier', 'pivot search', 'record+L stores', 'schur update', 'tail', '-', 'loop top']
+
+
+def build():
+    from aircraft_trajectory_optimization_amd import build_native
+    build_native.build(verbose=False)
+    objs = [o for o in sorted(glob.glob(os.path.join(build_native.OBJ, '*.o'))) if not o.endswith('ato_kkt.o')]
+    src = os.path.join(build_native.CSRC, 'ato_kkt.hip')
+    obj = os.path.join(HERE, 'ato_kkt_stamps.o')
+    subprocess.check_call(['hipcc', *build_native.FLAGS, '-DATO_KKT_STAMPS', '-c', src, '-o', obj])
+    subprocess.check_call(['hipcc', '-shared', '-fPIC', f'--offload-arch={build_native.ARCH}', '-o', LIB, *objs, obj])
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--build-only', action='store_true')
+    ap.add_argument('--K', type=int, default=4)
+    ap.add_argument('--N', type=int, default=50)
+    ap.add_argument('--batch', type=int, default=64)
+    a = ap.parse_args()
+    if a.build_only:
+        build()
+        return
+    import torch
+    from aircraft_trajectory_optimization_amd import native
+    native._LIB = native.declare(ctypes.CDLL(LIB))
+    lib = native._LIB
+    lib.ato_kkt_diag_stamps.argtypes = [ctypes.c_void_p]
+    from aircraft_trajectory_optimization_amd.raceline.batched import BatchedNLP
+    from aircraft_trajectory_optimization_amd.raceline.evaluator import variable_stages
+    from aircraft_trajectory_optimization_amd.raceline.instances import seeded_instances
+    from aircraft_trajectory_optimization_amd.solver.kkt_device import DeviceKKT
+    from aircraft_trajectory_optimization_amd.solver.kkt_plan import build_plan
+    from aircraft_trajectory_optimization_amd.tracks import make_spec
+    spec = make_spec(track='race', N=a.N, K=a.K)
+    B = a.batch
+    bn = BatchedNLP(spec, B)
+    W, _, _ = seeded_instances(spec, np.arange(B))
+    bn.set_w(W)
+    bn.evaluate()
+    hrp, hcol, _ = bn.problem.hess_sparsity()
+    plan = build_plan(bn.sizes[0], bn.sizes[1], variable_stages(spec), bn.row_ptr, bn.col, hrp, hcol)
+    g = torch.Generator(device='cuda').manual_seed(0)
+    lam = torch.randn((bn.sizes[1], B), dtype=torch.float64, device='cuda', generator=g)
+    H = bn.hessian(lam, torch.ones(B, dtype=torch.float64, device='cuda'))
+    dx = torch.rand((plan.n, B), dtype=torch.float64, device='cuda', generator=g) + 0.1
+    dr = -(torch.rand((plan.m, B), dtype=torch.float64, device='cuda', generator=g) * 1e-2 + 1e-6)
+    kkt = DeviceKKT(plan, B)
+    for _ in range(2):
+        kkt.factor(H, bn.jac, dx, dr)
+    torch.cuda.synchronize()
+    out = (ctypes.c_uint64 * 16)()
+    assert lib.ato_kkt_diag_stamps(ctypes.cast(out, ctypes.c_void_p)) == 0
+    v = np.array(out[:16], dtype=np.float64)
+    steps = max(v[8], 1)
+    total = v[:8].sum()
+    print(f'K={a.K} tiles={plan.tiles} steps={int(steps)} total clocks={total:.3e} ({total / steps:.0f} per step)')
+    for i, name in enumerate(PHASES):
+        if v[i]:
+            print(f'  {name:18s} {v[i]:12.3e}  {v[i] / steps:8.0f} per step  {100 * v[i] / total:5.1f} %')
+
+
+if __name__ == '__main__':
+    main()
