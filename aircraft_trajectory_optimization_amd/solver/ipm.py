@@ -488,6 +488,10 @@ class InteriorPointSolver:
                 if not np.all(np.isfinite(res)) or np.abs(res).max(initial=0) <= 1e-10 * scale:
                     break
                 x = x + base(res)
+            res = rhs - Kc @ x
+            # IPOPT (residual_ratio_singular): a solve refinement cannot bring below 1e-5 of the
+            # right-hand side is treated like a singular matrix (larger perturbation)
+            self._last_solve_ok = bool(np.all(np.isfinite(res)) and np.abs(res).max(initial=0) <= 1e-5 * scale)
             return x
         return solve, inertia
 
@@ -522,7 +526,7 @@ class InteriorPointSolver:
                 r_y = rhs_y.copy()
                 r_y[iin] += rhs_s / Ds_tot
                 sol = solve_k(np.concatenate([rhs_x, r_y]))
-                if np.all(np.isfinite(sol)):
+                if np.all(np.isfinite(sol)) and self._last_solve_ok:
                     dx, dy = sol[:n], sol[n:]
                     ds = (rhs_s + dy[iin]) / Ds_tot
                     if inertia is None:

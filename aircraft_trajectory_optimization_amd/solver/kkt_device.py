@@ -95,11 +95,14 @@ class DeviceKKT:
         all fp64 interleaved with B = max_batch. Returns the inertia tensor [B][3] (device).
         '''
         B = self.cap
+        J, dx, dr = J.contiguous(), dx.contiguous(), dr.contiguous()
+        H = H.contiguous() if H is not None else None
         for t, rows in ((J, None), (dx, self.plan.n), (dr, self.plan.m)) + (((H, None),) if H is not None else ()):
-            if t.dtype != torch.float64 or t.dim() != 2 or t.shape[1] != B or not t.is_contiguous():
-                raise ValueError('KKT values must be contiguous fp64 [elements][max_batch] tensors')
+            if t.dtype != torch.float64 or t.dim() != 2 or t.shape[1] != B or t.device != self.device:
+                raise ValueError('KKT values must be fp64 [elements][max_batch] tensors on the KKT device')
             if rows is not None and t.shape[0] != rows:
                 raise ValueError('diagonal of the wrong length')
+        self._keep_vals = (H, J, dx, dr)      # alive until the (asynchronous) factorisation has read them
         lst, nb = self._list(instances)
         st = stream if stream is not None else torch.cuda.current_stream(self.device)
         self._check(self.lib.ato_kkt_factor(self.handle, nb, lst.data_ptr() if lst is not None else None, B, 1,
@@ -110,8 +113,9 @@ class DeviceKKT:
 
     def solve(self, x: torch.Tensor, instances: Optional[Sequence[int]] = None, stream=None) -> torch.Tensor:
         ''' in place: x [dim][B] holds the right-hand sides (KKT order) and receives the solutions '''
-        if x.dtype != torch.float64 or x.shape != (self.plan.dim, self.cap) or not x.is_contiguous():
-            raise ValueError('x must be a contiguous fp64 [dim][max_batch] tensor')
+        if x.dtype != torch.float64 or x.shape != (self.plan.dim, self.cap) or not x.is_contiguous() or \
+                x.device != self.device:
+            raise ValueError('x must be a contiguous fp64 [dim][max_batch] tensor on the KKT device')
         lst, nb = self._list(instances)
         st = stream if stream is not None else torch.cuda.current_stream(self.device)
         self._check(self.lib.ato_kkt_solve(self.handle, nb, lst.data_ptr() if lst is not None else None, self.cap, 1,
