@@ -39,7 +39,9 @@ def parse():
     ap.add_argument('--layout', choices=['interleaved', 'instance'], default='interleaved')
     ap.add_argument('--cpu-seconds', type=float, default=15.0, help='budget of the oracle CPU baseline')
     ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--no-solve', action='store_true', help='skip the single-instance interior-point solve')
+    ap.add_argument('--no-solve', action='store_true', help='skip the interior-point solves (batched and single)')
+    ap.add_argument('--solve-batch', type=int, default=512, help='instances of the batched interior-point solve')
+    ap.add_argument('--solve-max-iter', type=int, default=200)
     ap.add_argument('--traffic-json', default=os.path.join(ROOT, 'profiles', 'traffic_latest.json'))
     return ap.parse_args()
 
@@ -65,34 +67,21 @@ def cpu_baseline(spec_kwargs, W, budget_s):
                       f'dense J + f + grad f, numpy fp64, single thread, {dt:.1f} s'}
 
 
-def single_solve(dev):
+def batched_solve(B, max_iter):
     '''
-    BASELINE config 2: the racetrack 50x4 drone NLP solved to IPOPT tolerance for ONE instance,
-    every evaluation (g, J, f, grad f, Lagrangian Hessian) on the GPU, the interior-point
-    iteration and its KKT factorisation on the host (warm-started from the point-mass solve as
-    race.py's use_ws does). Reported beside the batched evaluation throughput; the batched
-    on-device KKT is the next step.
+    The SQP (interior-point) iteration itself, batched: BASELINE config 3 shape (racetrack 50 x 4
+    drone, B instances on one GPU, fp64). Instance 0 is race.py's use_ws start (point-mass warm
+    start); the others are seeded perturbations of it (raceline/batch_instances.py). Every
+    evaluation, Hessian, KKT factorisation (ato_kkt_factor) and solve runs on the device; the
+    lockstep iteration logic is torch on the device. Instance 0 is also solved by the
+    single-instance host-KKT solver: lap_time_err_instance0_vs_host_s compares the two (the
+    CasADi/IPOPT lap time itself is unpinned: IPOPT is not reachable here).
     '''
-    from aircraft_trajectory_optimization_amd.raceline.evaluator import DeviceEvaluator
-    from aircraft_trajectory_optimization_amd.solver.ipm import InteriorPointSolver, IPMOptions
-    from aircraft_trajectory_optimization_amd.tracks import make_spec, make_warm_spec
-    kw = dict(track='race', frame='parametric', N=50, K=4)
-    pspec = make_spec(model='point', use_quat=False, **kw)
-    pev = DeviceEvaluator(pspec, device=dev)
-    t0 = time.perf_counter()
-    pres = InteriorPointSolver(pev, pspec.lbw, pspec.ubw, pev.lbg, pev.ubg, IPMOptions(max_iter=1000)).solve(pspec.w0)
-    t_ws = time.perf_counter() - t0
-    spec = make_warm_spec(pres.x, **kw)
-    ev = DeviceEvaluator(spec, device=dev)
-    t0 = time.perf_counter()
-    res = InteriorPointSolver(ev, spec.lbw, spec.ubw, ev.lbg, ev.ubg, IPMOptions(max_iter=1000)).solve(spec.w0)
-    t = time.perf_counter() - t0
-    return {'workload': 'racetrack_parametric_esp_drone_colloc_N50_K4 (single instance, point-mass warm start)',
-            'status': res.status, 'iterations': res.iters, 'lap_time_s': float(res.x[:spec.N].sum()),
-            'solve_s': t, 'iterations_per_s': res.iters / t, 'feval_s': ev.feval_time,
-            'warm_start': {'status': pres.status, 'iterations': pres.iters, 'solve_s': t_ws,
-                           'lap_time_s': float(pres.x[:pspec.N].sum())},
-            'lap_time_vs_casadi': 'unpinned (no IPOPT reachable here)'}
+    from tools.solve_batched import run
+    out = run(B, max_iter, host_ref=True)
+    out['lap_time_vs_casadi'] = 'unpinned (no IPOPT reachable here); vs the single-instance solver: see ' \
+                                'lap_time_err_instance0_vs_host_s'
+    return out
 
 
 def main():
@@ -188,7 +177,7 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             out['cpu_baseline'] = cpu_baseline(spec_kwargs, W, args.cpu_seconds)
         if world == 1 and not args.no_solve:
-            out['solve'] = single_solve(dev)
+            out['sqp'] = batched_solve(args.solve_batch, args.solve_max_iter)
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()
