@@ -17,8 +17,10 @@ single-instance solver would make:
   * filter line search with switching / Armijo conditions and second-order corrections; every
     trial point of every instance is evaluated in one batched ato_eval
 
-Not carried over: the feasibility-restoration phase. An instance whose line search fails
-stops with status 'restoration_failed' (the single-instance solver.ipm handles that case).
+  * feasibility restoration (IPOPT's min ||c||_1 phase, as solver/ipm.py): the instances whose
+    line search fails run a nested batched solve of the restoration NLP over (x, p, n); the
+    elastic variables p, n are eliminated from its KKT system (_RestorationKKT), so it is
+    factorised by the same device LDL^T with modified row diagonals
 
 Interfaces (duck-typed so tests can substitute CPU stand-ins):
   evaluator: n, m, batch, device, j_row_ptr, j_col, h_row_ptr, h_col, lbg, ubg,
@@ -35,9 +37,10 @@ import torch
 
 from aircraft_trajectory_optimization_amd.solver.ipm import INF, IPMOptions
 
-RUNNING, OPTIMAL, ACCEPTABLE, MAX_ITER, LS_FAILED, KKT_FAILED = range(6)
+RUNNING, OPTIMAL, ACCEPTABLE, MAX_ITER, LS_FAILED, KKT_FAILED, STOPPED, INACTIVE = range(8)
 STATUS_NAMES = {RUNNING: 'running', OPTIMAL: 'optimal', ACCEPTABLE: 'acceptable', MAX_ITER: 'max_iter',
-                LS_FAILED: 'restoration_failed', KKT_FAILED: 'kkt_failure'}
+                LS_FAILED: 'restoration_failed', KKT_FAILED: 'kkt_failure', STOPPED: 'stopped',
+                INACTIVE: 'inactive'}
 FILTER_MAX = 256
 
 
@@ -117,13 +120,16 @@ class BatchedInteriorPoint:
         self.lbx0, self.ubx0 = per_inst(lbx), per_inst(ubx)
         if self.lbx0.shape != (n, B):
             raise ValueError('lbx / ubx must be [n], [n, B] or [B, n]')
-        lbg, ubg = np.asarray(ev.lbg, float), np.asarray(ev.ubg, float)
-        eq = lbg == ubg
+        lbg = ev.lbg.cpu().numpy() if torch.is_tensor(ev.lbg) else np.asarray(ev.lbg, float)
+        ubg = ev.ubg.cpu().numpy() if torch.is_tensor(ev.ubg) else np.asarray(ev.ubg, float)
+        eq = (lbg == ubg) if lbg.ndim == 1 else (lbg[:, 0] == ubg[:, 0])
+        if lbg.ndim == 1:               # shared by every instance
+            lbg, ubg = lbg[:, None], ubg[:, None]
         self.ieq = t(np.nonzero(eq)[0], torch.long)
         self.iin = t(np.nonzero(~eq)[0], torch.long)
         self.mi = int((~eq).sum())
-        self.lbg0 = t(np.where(lbg <= -INF, -np.inf, lbg))[:, None]
-        self.ubg0 = t(np.where(ubg >= INF, np.inf, ubg))[:, None]
+        self.lbg0 = t(np.where(lbg <= -INF, -np.inf, lbg))
+        self.ubg0 = t(np.where(ubg >= INF, np.inf, ubg))
         self.jr = t(np.repeat(np.arange(m), np.diff(ev.j_row_ptr)), torch.long)
         self.jc = t(np.asarray(ev.j_col), torch.long)
         hr = np.repeat(np.arange(n), np.diff(ev.h_row_ptr))
@@ -359,8 +365,15 @@ class BatchedInteriorPoint:
         return dxs, ds, dy, dw_out, ok_all, ctx
 
     # ------------------------------------------------------------------ solve
-    def solve(self, X0) -> BatchedIPMResult:
+    def solve(self, X0, mu0: Optional[torch.Tensor] = None, active: Optional[torch.Tensor] = None,
+              stop_check=None, allow_restoration: bool = True, progress: int = 0) -> BatchedIPMResult:
+        '''
+        X0 [n, B] (or [B, n]). active: instances to iterate (default all); mu0: initial barrier
+        per instance; stop_check(x) -> [B] bool ends an instance with status 'stopped' (the
+        restoration phase's return test).
+        '''
         o = self.o
+        self._progress = progress
         n, m, B, dev = self.n, self.m, self.B, self.dev
         x = torch.as_tensor(np.asarray(X0, float) if not torch.is_tensor(X0) else X0, dtype=torch.float64,
                             device=dev)
@@ -384,6 +397,7 @@ class BatchedInteriorPoint:
         sf, sg = self.sf, self.sg
         lbg = torch.where(torch.isfinite(self.lbg0), self.lbg0 * sg, torch.full_like(sg, -np.inf))
         ubg = torch.where(torch.isfinite(self.ubg0), self.ubg0 * sg, torch.full_like(sg, np.inf))
+        self.lbg_s, self.ubg_s = lbg, ubg
         self.c_rhs = lbg[self.ieq]
         self.dL, self.dU = self._relax(lbg[self.iin], ubg[self.iin])
         self.xL, self.xU = self._relax(self.lbx0, self.ubx0)
@@ -401,10 +415,12 @@ class BatchedInteriorPoint:
         zu = self.hxu.double() * o.bound_mult_init_val
         vl = self.hsl.double() * o.bound_mult_init_val
         vu = self.hsu.double() * o.bound_mult_init_val
-        act = torch.ones(B, dtype=torch.bool, device=dev)
+        act = torch.ones(B, dtype=torch.bool, device=dev) if active is None else active.clone()
         Js = jv * sg[self.jr]
         y = self._ls_multipliers(Js, gf, zl, zu, vl, vu, act)
         mu = torch.full((B,), o.mu_init, dtype=torch.float64, device=dev)
+        if mu0 is not None:
+            mu = torch.where(act, mu0, mu)
         tau = torch.clamp(1.0 - mu, min=o.tau_min)
         theta0 = self._resid(g, s).abs().sum(0)
         self.theta_max = o.theta_max_fact * torch.clamp(theta0, min=1.0)
@@ -413,7 +429,11 @@ class BatchedInteriorPoint:
         nf = torch.zeros(B, dtype=torch.long, device=dev)
         dwl = torch.zeros(B, dtype=torch.float64, device=dev)
         n_acc = torch.zeros(B, dtype=torch.long, device=dev)
-        status = torch.full((B,), RUNNING, dtype=torch.long, device=dev)
+        status = torch.where(act, torch.full((B,), RUNNING, dtype=torch.long, device=dev),
+                             torch.full((B,), INACTIVE, dtype=torch.long, device=dev))
+        n_resto = torch.zeros(B, dtype=torch.long, device=dev)
+        own = torch.zeros(B, dtype=torch.long, device=dev)          # iterations done per instance
+        waiting = torch.zeros(B, dtype=torch.bool, device=dev)      # frozen until the next restoration batch
         iters = torch.zeros(B, dtype=torch.long, device=dev)
         history = []
 
@@ -426,13 +446,17 @@ class BatchedInteriorPoint:
             F[rows, pos] = torch.where(mask[:, None], entry, cur)
             nf = torch.where(mask, torch.clamp(nf + 1, max=FILTER_MAX), nf)
 
-        for it in range(o.max_iter + 1):
-            iters = torch.where(act, torch.full_like(iters, it), iters)
+        for it in range(3 * o.max_iter + 3):
+            iters = torch.where(act, own, iters)
             Js = jv * sg[self.jr]
             dual_x = gf + self._JTy(Js, y) - zl + zu
             E0, du, pr, co = self._errors(dual_x, g, x, s, y, zl, zu, vl, vu, 0.0)
             pr_uns = (self._resid(g, s) / sg).abs().amax(0)
             history.append(torch.stack([f / sf, pr, du, mu, E0]))
+            if stop_check is not None:
+                stp = act & (own > 0) & stop_check(x)
+                status = torch.where(stp, torch.full_like(status, STOPPED), status)
+                act = act & ~stp
             conv = act & (E0 <= o.tol) & (du / sf <= o.dual_inf_tol) & (pr_uns <= o.constr_viol_tol) & \
                 (co <= o.compl_inf_tol)
             status = torch.where(conv, torch.full_like(status, OPTIMAL), status)
@@ -441,129 +465,178 @@ class BatchedInteriorPoint:
             accd = act & (n_acc >= o.acceptable_iter)
             status = torch.where(accd, torch.full_like(status, ACCEPTABLE), status)
             act = act & ~accd
-            if it == o.max_iter:
-                status = torch.where(act, torch.full_like(status, MAX_ITER), status)
-                act = act & False
-            if not bool(act.any()):
+            mx = act & (own >= o.max_iter)
+            status = torch.where(mx, torch.full_like(status, MAX_ITER), status)
+            act = act & ~mx
+            if not bool(act.any()) and not bool(waiting.any()):
                 break
-            # ---- barrier update (monotone), per instance
-            for _ in range(100):
-                Emu = self._errors(dual_x, g, x, s, y, zl, zu, vl, vu, mu)[0]
-                upd = act & (Emu <= o.kappa_eps * mu) & (mu > o.tol / 10)
-                if not bool(upd.any()):
-                    break
-                mu_new = torch.clamp(torch.minimum(o.kappa_mu * mu, mu ** o.theta_mu), min=o.tol / 10)
-                mu = torch.where(upd, mu_new, mu)
-                tau = torch.where(upd, torch.clamp(1.0 - mu, min=o.tau_min), tau)
-                nf = torch.where(upd, torch.zeros_like(nf), nf)
-            # ---- Newton step
-            W = self.ev.hess(x, y * sg, sf)
-            self.stats['hess'] += 1
-            a, b, c, d = self._slacks(x, s)
-            Sx = torch.where(self.hxl, zl / a, 0.0) + torch.where(self.hxu, zu / b, 0.0)
-            Ss = torch.where(self.hsl, vl / c, 0.0) + torch.where(self.hsu, vu / d, 0.0)
-            gx, gs = self._grad_phi(gf, x, s, mu)
-            r = self._resid(g, s)
-            rhs_x = -(gx + self._JTy(Js, y))
-            rhs_s = -(gs - y[self.iin])
-            rhs_y = -r
-            dx, ds, dy, delta_w, ok, ctx = self._kkt_step(W, Js, Sx, Ss, rhs_x, rhs_s, rhs_y, mu, dwl, act)
-            kfail = act & ~ok
-            status = torch.where(kfail, torch.full_like(status, KKT_FAILED), status)
-            act = act & ok
-            dwl = torch.where(act & (delta_w > 0), delta_w, dwl)
-            # ---- bound multiplier steps, fraction to the boundary
-            dzl = torch.where(self.hxl, mu / a - zl - zl / a * dx, 0.0)
-            dzu = torch.where(self.hxu, mu / b - zu + zu / b * dx, 0.0)
-            dvl = torch.where(self.hsl, mu / c - vl - vl / c * ds, 0.0)
-            dvu = torch.where(self.hsu, mu / d - vu + vu / d * ds, 0.0)
-            alpha_max = torch.minimum(torch.minimum(self._ftb(a, dx, self.hxl, tau), self._ftb(b, -dx, self.hxu, tau)),
-                                      torch.minimum(self._ftb(c, ds, self.hsl, tau), self._ftb(d, -ds, self.hsu, tau)))
-            alpha_z = torch.minimum(torch.minimum(self._ftb(zl, dzl, self.hxl, tau), self._ftb(zu, dzu, self.hxu, tau)),
-                                    torch.minimum(self._ftb(vl, dvl, self.hsl, tau), self._ftb(vu, dvu, self.hsu, tau)))
-            # ---- filter line search, all instances in lockstep
-            theta = r.abs().sum(0)
-            phi = self._phi(f, x, s, mu)
-            gphi_d = (gx * dx).sum(0) + (gs * ds).sum(0)
-            neg = gphi_d < 0
-            mgd = torch.clamp(-gphi_d, min=1e-300)
-            t1 = o.gamma_phi * theta / mgd
-            t2 = o.delta * theta ** o.s_theta / mgd ** o.s_phi
-            amin = torch.where(neg & (theta <= self.theta_min),
-                               torch.clamp(torch.minimum(t1, t2), max=o.gamma_theta),
-                               torch.where(neg, torch.clamp(t1, max=o.gamma_theta), torch.full_like(t1, o.gamma_theta)))
-            alpha_min = o.alpha_min_frac * amin
-            alpha = alpha_max.clone()
-            pend = act.clone()
-            first = torch.ones(B, dtype=torch.bool, device=dev)
-            # accepted trial state
-            xn, sn, fn, gn, gfn, jvn = x.clone(), s.clone(), f.clone(), g.clone(), gf.clone(), jv.clone()
-            an, dyn = torch.zeros_like(alpha), dy.clone()
-            armn = torch.zeros(B, dtype=torch.bool, device=dev)
+            stepping = act.clone()
+            resto = torch.zeros(B, dtype=torch.bool, device=dev)
+            if progress and it % progress == 0:
+                import sys
+                print(f'[batched ipm{" resto" if stop_check is not None else ""}] iter {it}: '
+                      f'{int(act.sum())} active, {int((status == OPTIMAL).sum())} optimal', file=sys.stderr, flush=True)
+            if bool(act.any()):
+                # ---- barrier update (monotone), per instance
+                for _ in range(100):
+                    Emu = self._errors(dual_x, g, x, s, y, zl, zu, vl, vu, mu)[0]
+                    upd = act & (Emu <= o.kappa_eps * mu) & (mu > o.tol / 10)
+                    if not bool(upd.any()):
+                        break
+                    mu_new = torch.clamp(torch.minimum(o.kappa_mu * mu, mu ** o.theta_mu), min=o.tol / 10)
+                    mu = torch.where(upd, mu_new, mu)
+                    tau = torch.where(upd, torch.clamp(1.0 - mu, min=o.tau_min), tau)
+                    nf = torch.where(upd, torch.zeros_like(nf), nf)
+                # ---- Newton step
+                W = self.ev.hess(x, y * sg, sf)
+                self.stats['hess'] += 1
+                a, b, c, d = self._slacks(x, s)
+                Sx = torch.where(self.hxl, zl / a, 0.0) + torch.where(self.hxu, zu / b, 0.0)
+                Ss = torch.where(self.hsl, vl / c, 0.0) + torch.where(self.hsu, vu / d, 0.0)
+                gx, gs = self._grad_phi(gf, x, s, mu)
+                r = self._resid(g, s)
+                rhs_x = -(gx + self._JTy(Js, y))
+                rhs_s = -(gs - y[self.iin])
+                rhs_y = -r
+                dx, ds, dy, delta_w, ok, ctx = self._kkt_step(W, Js, Sx, Ss, rhs_x, rhs_s, rhs_y, mu, dwl, act)
+                kfail = act & ~ok
+                status = torch.where(kfail, torch.full_like(status, KKT_FAILED), status)
+                act = act & ok
+                dwl = torch.where(act & (delta_w > 0), delta_w, dwl)
+                # ---- bound multiplier steps, fraction to the boundary
+                dzl = torch.where(self.hxl, mu / a - zl - zl / a * dx, 0.0)
+                dzu = torch.where(self.hxu, mu / b - zu + zu / b * dx, 0.0)
+                dvl = torch.where(self.hsl, mu / c - vl - vl / c * ds, 0.0)
+                dvu = torch.where(self.hsu, mu / d - vu + vu / d * ds, 0.0)
+                alpha_max = torch.minimum(torch.minimum(self._ftb(a, dx, self.hxl, tau), self._ftb(b, -dx, self.hxu, tau)),
+                                          torch.minimum(self._ftb(c, ds, self.hsl, tau), self._ftb(d, -ds, self.hsu, tau)))
+                alpha_z = torch.minimum(torch.minimum(self._ftb(zl, dzl, self.hxl, tau), self._ftb(zu, dzu, self.hxu, tau)),
+                                        torch.minimum(self._ftb(vl, dvl, self.hsl, tau), self._ftb(vu, dvu, self.hsu, tau)))
+                # ---- filter line search, all instances in lockstep
+                theta = r.abs().sum(0)
+                phi = self._phi(f, x, s, mu)
+                gphi_d = (gx * dx).sum(0) + (gs * ds).sum(0)
+                neg = gphi_d < 0
+                mgd = torch.clamp(-gphi_d, min=1e-300)
+                t1 = o.gamma_phi * theta / mgd
+                t2 = o.delta * theta ** o.s_theta / mgd ** o.s_phi
+                amin = torch.where(neg & (theta <= self.theta_min),
+                                   torch.clamp(torch.minimum(t1, t2), max=o.gamma_theta),
+                                   torch.where(neg, torch.clamp(t1, max=o.gamma_theta), torch.full_like(t1, o.gamma_theta)))
+                alpha_min = o.alpha_min_frac * amin
+                alpha = alpha_max.clone()
+                pend = act.clone()
+                resto = torch.zeros(B, dtype=torch.bool, device=dev)
+                first = torch.ones(B, dtype=torch.bool, device=dev)
+                # accepted trial state
+                xn, sn, fn, gn, gfn, jvn = x.clone(), s.clone(), f.clone(), g.clone(), gf.clone(), jv.clone()
+                an, dyn = torch.zeros_like(alpha), dy.clone()
+                armn = torch.zeros(B, dtype=torch.bool, device=dev)
 
-            def take(mask, al, xt, st, ft, gt, gft, jvt, arm, dyt):
-                nonlocal xn, sn, fn, gn, gfn, jvn, an, dyn, armn
-                m2 = mask[None, :]
-                xn = torch.where(m2, xt, xn)
-                sn = torch.where(m2, st, sn)
-                fn = torch.where(mask, ft, fn)
-                gn = torch.where(m2, gt, gn)
-                gfn = torch.where(m2, gft, gfn)
-                jvn = torch.where(m2, jvt, jvn)
-                an = torch.where(mask, al, an)
-                dyn = torch.where(m2, dyt, dyn)
-                armn = torch.where(mask, arm, armn)
+                def take(mask, al, xt, st, ft, gt, gft, jvt, arm, dyt):
+                    nonlocal xn, sn, fn, gn, gfn, jvn, an, dyn, armn
+                    m2 = mask[None, :]
+                    xn = torch.where(m2, xt, xn)
+                    sn = torch.where(m2, st, sn)
+                    fn = torch.where(mask, ft, fn)
+                    gn = torch.where(m2, gt, gn)
+                    gfn = torch.where(m2, gft, gfn)
+                    jvn = torch.where(m2, jvt, jvn)
+                    an = torch.where(mask, al, an)
+                    dyn = torch.where(m2, dyt, dyn)
+                    armn = torch.where(mask, arm, armn)
 
-            for _ls in range(200):
-                failed = pend & ~(alpha >= alpha_min)
-                if bool(failed.any()):
-                    status = torch.where(failed, torch.full_like(status, LS_FAILED), status)
-                    act = act & ~failed
-                    pend = pend & ~failed
-                if not bool(pend.any()):
-                    break
-                xt = x + alpha * dx
-                st = s + alpha * ds
-                ft, gt, gft, jvt = self._eval(xt)
-                rt = self._resid(gt, st)
-                tht = rt.abs().sum(0)
-                pht = self._phi(ft, xt, st, mu)
-                okt, armt = self._accept(theta, phi, gphi_d, alpha, tht, pht, F, nf)
-                okt = okt & pend
-                take(okt, alpha, xt, st, ft, gt, gft, jvt, armt, dy)
-                pend = pend & ~okt
-                soc = pend & first & (tht >= theta)
-                if bool(soc.any()):
-                    got = self._soc(soc, ctx, rhs_x, rhs_s, x, s, alpha, r, rt, theta, phi, gphi_d, F, nf, tau,
-                                    (a, b, c, d), mu, take)
-                    pend = pend & ~got
-                first = first & False
-                alpha = torch.where(pend, alpha * 0.5, alpha)
-            # ---- accept
-            add_filter(act & ~armn, theta, phi)
-            m2 = act[None, :]
-            x = torch.where(m2, xn, x)
-            s = torch.where(m2, sn, s)
-            f = torch.where(act, fn, f)
-            g = torch.where(m2, gn, g)
-            gf = torch.where(m2, gfn, gf)
-            jv = torch.where(m2, jvn, jv)
-            y = torch.where(m2, y + an * dyn, y)
-            az = torch.where(act, alpha_z, torch.zeros_like(alpha_z))
-            zl, zu = zl + az * dzl, zu + az * dzu
-            vl, vu = vl + az * dvl, vu + az * dvu
-            a, b, c, d = self._slacks(x, s)
-            ks = o.kappa_sigma
-            zl = torch.where(self.hxl, torch.minimum(torch.maximum(zl, mu / (ks * a)), ks * mu / a), 0.0)
-            zu = torch.where(self.hxu, torch.minimum(torch.maximum(zu, mu / (ks * b)), ks * mu / b), 0.0)
-            vl = torch.where(self.hsl, torch.minimum(torch.maximum(vl, mu / (ks * c)), ks * mu / c), 0.0)
-            vu = torch.where(self.hsu, torch.minimum(torch.maximum(vu, mu / (ks * d)), ks * mu / d), 0.0)
+                for _ls in range(200):
+                    failed = pend & ~(alpha >= alpha_min)
+                    if bool(failed.any()):
+                        if allow_restoration:
+                            resto = resto | failed
+                        else:
+                            status = torch.where(failed, torch.full_like(status, LS_FAILED), status)
+                            act = act & ~failed
+                        pend = pend & ~failed
+                    if not bool(pend.any()):
+                        break
+                    xt = x + alpha * dx
+                    st = s + alpha * ds
+                    ft, gt, gft, jvt = self._eval(xt)
+                    rt = self._resid(gt, st)
+                    tht = rt.abs().sum(0)
+                    pht = self._phi(ft, xt, st, mu)
+                    okt, armt = self._accept(theta, phi, gphi_d, alpha, tht, pht, F, nf)
+                    okt = okt & pend
+                    take(okt, alpha, xt, st, ft, gt, gft, jvt, armt, dy)
+                    pend = pend & ~okt
+                    soc = pend & first & (tht >= theta)
+                    if bool(soc.any()):
+                        got = self._soc(soc, ctx, rhs_x, rhs_s, x, s, alpha, r, rt, theta, phi, gphi_d, F, nf, tau,
+                                        (a, b, c, d), mu, take)
+                        pend = pend & ~got
+                    first = first & False
+                    alpha = torch.where(pend, alpha * 0.5, alpha)
+                # ---- accept
+                upd = act & ~resto
+                add_filter(upd & ~armn, theta, phi)
+                m2 = upd[None, :]
+                x = torch.where(m2, xn, x)
+                s = torch.where(m2, sn, s)
+                f = torch.where(upd, fn, f)
+                g = torch.where(m2, gn, g)
+                gf = torch.where(m2, gfn, gf)
+                jv = torch.where(m2, jvn, jv)
+                y = torch.where(m2, y + an * dyn, y)
+                az = torch.where(upd, alpha_z, torch.zeros_like(alpha_z))
+                zl, zu = zl + az * dzl, zu + az * dzu
+                vl, vu = vl + az * dvl, vu + az * dvu
+                a, b, c, d = self._slacks(x, s)
+                ks = o.kappa_sigma
+                zl = torch.where(self.hxl, torch.minimum(torch.maximum(zl, mu / (ks * a)), ks * mu / a), 0.0)
+                zu = torch.where(self.hxu, torch.minimum(torch.maximum(zu, mu / (ks * b)), ks * mu / b), 0.0)
+                vl = torch.where(self.hsl, torch.minimum(torch.maximum(vl, mu / (ks * c)), ks * mu / c), 0.0)
+                vu = torch.where(self.hsu, torch.minimum(torch.maximum(vu, mu / (ks * d)), ks * mu / d), 0.0)
+            own = own + stepping.long()
+            # ---- feasibility restoration: instances whose line search failed wait (frozen) and are
+            # restored together, so one nested batched solve serves many of them
+            waiting = waiting | resto
+            act = act & ~resto
+            n_act, n_wait = int(act.sum()), int(waiting.sum())
+            if n_wait and (n_act == 0 or n_wait >= max(1, n_act // 8) or it % 10 == 9):
+                R = waiting.clone()
+                waiting = waiting & False
+                can = R & (n_resto < o.max_resto)
+                cant = R & ~can
+                status = torch.where(cant, torch.full_like(status, LS_FAILED), status)
+                if bool(can.any()):
+                    n_resto = n_resto + can.long()
+                    theta_w = self._resid(g, s).abs().sum(0)
+                    phi_w = self._phi(f, x, s, mu)
+                    add_filter(can, theta_w, phi_w)
+                    xr, okr = self._restore(can, x, g, mu, theta_w, F, nf)
+                    bad = can & ~okr
+                    status = torch.where(bad, torch.full_like(status, LS_FAILED), status)
+                    if bool(okr.any()):
+                        r2 = okr[None, :]
+                        x = torch.where(r2, xr, x)
+                        fe, ge, gfe, jve = self._eval(x)
+                        f = torch.where(okr, fe, f)
+                        g = torch.where(r2, ge, g)
+                        gf = torch.where(r2, gfe, gf)
+                        jv = torch.where(r2, jve, jv)
+                        s = torch.where(r2, self._push(g[self.iin], self.dL, self.dU), s)
+                        a, b, c, d = self._slacks(x, s)
+                        zl = torch.where(r2, torch.where(self.hxl, mu / a, 0.0), zl)
+                        zu = torch.where(r2, torch.where(self.hxu, mu / b, 0.0), zu)
+                        vl = torch.where(r2, torch.where(self.hsl, mu / c, 0.0), vl)
+                        vu = torch.where(r2, torch.where(self.hsu, mu / d, 0.0), vu)
+                        y = torch.where(r2, self._ls_multipliers(jv * sg[self.jr], gf, zl, zu, vl, vu, okr), y)
+                        act = act | okr
 
         if o.honor_original_bounds:
             x = torch.minimum(torch.maximum(x, self.lbx0), self.ubx0)
         fu, _, _, _ = self.ev.eval(x)
         st = status.cpu().numpy()
         self.history = torch.stack(history).cpu().numpy() if history else np.zeros((0, 5, B))
+        self.stats['restorations'] = self.stats.get('restorations', 0) + int(n_resto.sum())
         return BatchedIPMResult(x=x, f=fu, lam_g=y * sg / sf, lam_x=(zu - zl) / sf,
                                 status=[STATUS_NAMES[int(v)] for v in st], iters=iters.cpu().numpy(),
                                 stats=dict(self.stats))
@@ -602,3 +675,153 @@ class BatchedInteriorPoint:
             theta_old = tht
             c_soc = am * c_soc + rt2
         return got
+
+    # ------------------------------------------------------------------ feasibility restoration
+    def _restore(self, R, x, g, mu, theta, F, nf):
+        ''' IPOPT's restoration phase on the scaled problem for the instances in R (solver/ipm.py
+        _restore, batched): returns (new x [n, B], success mask) '''
+        o = self.o
+        n, m, B, dev = self.n, self.m, self.B, self.dev
+        rho = o.resto_penalty
+        viol = g - torch.minimum(torch.maximum(g, self.lbg_s), self.ubg_s)
+        mu_r = torch.maximum(mu, viol.abs().amax(0))
+        a_ = (mu_r - rho * viol) / (2 * rho)
+        nn = a_ + torch.sqrt(a_ * a_ + mu_r * viol / (2 * rho))
+        pp = viol + nn
+        rev = _RestorationEvaluator(self.ev, self.sg, x, torch.sqrt(mu), rho, self.lbg_s, self.ubg_s)
+        Xr0 = torch.cat([x, pp, nn])
+        lbx = torch.cat([self.lbx0, torch.zeros((2 * m, B), dtype=torch.float64, device=dev)])
+        ubx = torch.cat([self.ubx0, torch.full((2 * m, B), np.inf, dtype=torch.float64, device=dev)])
+        ro = IPMOptions(**{**o.__dict__, 'nlp_scaling': False, 'max_iter': 3000})
+        sub = BatchedInteriorPoint(rev, _RestorationKKT(self.kkt, rev), lbx.cpu().numpy(), ubx.cpu().numpy(), ro)
+        theta_start = theta
+
+        def accept(xr):
+            xo = xr[:n]
+            f2, g2, _, _ = self._eval(xo)
+            s2 = self._push(g2[self.iin], self.dL, self.dU)
+            th = self._resid(g2, s2).abs().sum(0)
+            ph = self._phi(f2, xo, s2, mu)
+            k = torch.arange(F.shape[1], device=dev)
+            valid = k[None, :] < nf[:, None]
+            in_f = (valid & (th[:, None] >= F[:, :, 0]) & (ph[:, None] >= F[:, :, 1])).any(1)
+            return (th <= o.resto_kappa * theta_start) & ~in_f
+
+        res = sub.solve(Xr0, mu0=mu_r, active=R, stop_check=accept, allow_restoration=False,
+                        progress=self._progress)
+        for k2, v in sub.stats.items():
+            if k2 != 'restorations':
+                self.stats[k2] = self.stats.get(k2, 0) + v
+        ok = R & torch.as_tensor(np.array([st == 'stopped' for st in res.status]), device=dev)
+        return torch.minimum(torch.maximum(res.x[:n], self.xL), self.xU), ok
+
+
+class _RestorationEvaluator:
+    '''
+    Restoration NLP over (x, p, n) on the scaled rows of the base evaluator, per instance
+    (solver/ipm.py _RestorationEvaluator on [element][instance] tensors):
+        min  rho sum(p + n) + zeta/2 |D_R (x - x_r)|^2   s.t.  sg * g(x) - p + n  in scaled bounds
+    Jacobian rows [sg_i J_i, -1 (p_i), +1 (n_i)]; Hessian = base constraint Hessian (sigma = 0)
+    plus zeta D_R^2 on the x diagonal (pattern: base pattern plus the full x diagonal).
+    '''
+
+    def __init__(self, base, sg, x_ref, zeta, rho, lbg_s, ubg_s):
+        n, m, B = base.n, base.m, base.batch
+        dev = base.device
+        self.base, self.sg, self.x_ref, self.zeta, self.rho = base, sg, x_ref.clone(), zeta, rho
+        self.n0, self.m, self.n, self.batch, self.device = n, m, n + 2 * m, B, dev
+        self.dr2 = torch.clamp(1.0 / torch.clamp(self.x_ref.abs(), min=1e-300), max=1.0) ** 2
+        cnt = np.diff(np.asarray(base.j_row_ptr))
+        self.j_row_ptr = np.concatenate([[0], np.cumsum(cnt + 2)]).astype(np.int64)
+        rows = np.repeat(np.arange(m), cnt)
+        pos_orig = np.arange(len(base.j_col)) + 2 * rows
+        col = np.empty(int(self.j_row_ptr[-1]), np.int64)
+        col[pos_orig] = base.j_col
+        pe = self.j_row_ptr[1:] - 2
+        col[pe], col[pe + 1] = n + np.arange(m), n + m + np.arange(m)
+        self.j_col = col
+        self.pos_orig = torch.as_tensor(pos_orig, device=dev)
+        self.pe = torch.as_tensor(pe, device=dev)
+        self.jrow_orig = torch.as_tensor(rows, device=dev)
+        hr = np.repeat(np.arange(n), np.diff(np.asarray(base.h_row_ptr)))
+        hc = np.asarray(base.h_col)
+        dkeys = np.arange(n) * n + np.arange(n)
+        keys = np.unique(np.concatenate([hr * n + hc, dkeys]))
+        r2, c2 = keys // n, keys % n
+        self.h_row_ptr = np.concatenate([np.searchsorted(r2, np.arange(n)), [len(keys)],
+                                         np.full(2 * m, len(keys))]).astype(np.int64)
+        self.h_col = c2
+        self.nnz_h = len(keys)
+        self.h_map = torch.as_tensor(np.searchsorted(keys, hr * n + hc), device=dev)
+        self.h_diag = torch.as_tensor(np.searchsorted(keys, dkeys), device=dev)
+        self.diag_new = torch.as_tensor(~np.isin(dkeys, hr * n + hc), device=dev)
+        self.lbg, self.ubg = lbg_s, ubg_s
+
+    def eval(self, X):
+        n, m, B = self.n0, self.m, self.batch
+        x, p, nn = X[:n], X[n:n + m], X[n + m:]
+        f, g, gf, jv = self.base.eval(x)
+        d = x - self.x_ref
+        fr = self.rho * (p.sum(0) + nn.sum(0)) + 0.5 * self.zeta * (self.dr2 * d * d).sum(0)
+        gr = self.sg * g - p + nn
+        gfr = torch.cat([self.zeta * self.dr2 * d,
+                         torch.full((2 * m, B), self.rho, dtype=torch.float64, device=self.device)])
+        jr = torch.empty((len(self.j_col), B), dtype=torch.float64, device=self.device)
+        jr[self.pos_orig] = jv * self.sg[self.jrow_orig]
+        jr[self.pe] = -1.0
+        jr[self.pe + 1] = 1.0
+        return fr, gr, gfr, jr
+
+    def hess(self, X, lam, sigma):
+        H0 = self.base.hess(X[:self.n0].contiguous(), (lam * self.sg).contiguous(), torch.zeros_like(sigma))
+        h = torch.zeros((self.nnz_h, self.batch), dtype=torch.float64, device=self.device)
+        h[self.h_map] = H0
+        h[self.h_diag] += sigma * self.zeta * self.dr2
+        return h
+
+
+class _RestorationKKT:
+    '''
+    KKT system of the restoration NLP through the base factorisation: p_i and n_i appear only in
+    row i (coefficients -1, +1) with diagonal Hessian entries dp, dn > 0, so they are eliminated:
+        row diagonal  dr - 1/dp - 1/dn,  right-hand side  ry + rp/dp - rn/dn,
+        p = (rp + y) / dp,  n = (rn - y) / dn,
+    and each eliminated variable adds one eigenvalue of its own sign (Haynsworth).
+    '''
+
+    def __init__(self, base_kkt, rev: _RestorationEvaluator):
+        self.k, self.rev = base_kkt, rev
+        m, B, dev = rev.m, rev.batch, rev.device
+        self.dp = torch.ones((m, B), dtype=torch.float64, device=dev)
+        self.dn = torch.ones((m, B), dtype=torch.float64, device=dev)
+
+    def _mask(self, instances):
+        rv = self.rev
+        mask = torch.zeros(rv.batch, dtype=torch.bool, device=rv.device)
+        mask[torch.as_tensor(np.asarray(instances, dtype=np.int64), device=rv.device)] = True
+        return mask
+
+    def factor(self, H, J, dx, dr, instances):
+        rv = self.rev
+        n, m = rv.n0, rv.m
+        Hb = H[rv.h_map] if H is not None else None
+        dxb = dx[:n] + torch.where(rv.diag_new[:, None], H[rv.h_diag], 0.0) if H is not None else dx[:n]
+        dp, dn = dx[n:n + m], dx[n + m:]
+        mask = self._mask(instances)[None, :]
+        self.dp = torch.where(mask, dp, self.dp)
+        self.dn = torch.where(mask, dn, self.dn)
+        inertia = self.k.factor(Hb, J[rv.pos_orig], dxb, dr - 1.0 / dp - 1.0 / dn, instances).clone()
+        inertia[:, 0] += ((dp > 0).sum(0) + (dn > 0).sum(0)).to(inertia.dtype)
+        inertia[:, 1] += ((dp < 0).sum(0) + (dn < 0).sum(0)).to(inertia.dtype)
+        return inertia
+
+    def solve(self, x, instances):
+        rv = self.rev
+        n, m = rv.n0, rv.m
+        rx, rp, rn, ry = x[:n], x[n:n + m], x[n + m:n + 2 * m], x[n + 2 * m:]
+        xb = torch.cat([rx, ry + rp / self.dp - rn / self.dn]).contiguous()
+        self.k.solve(xb, instances)
+        y = xb[n:]
+        new = torch.cat([xb[:n], (rp + y) / self.dp, (rn - y) / self.dn, y])
+        x.copy_(torch.where(self._mask(instances)[None, :], new, x))
+        return x

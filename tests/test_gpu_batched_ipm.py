@@ -53,3 +53,24 @@ def test_batched_device_racetrack_drone_warm_start():
     assert res.status[0] == 'optimal', res.status
     assert abs(laps[0] - ref.x[:spec.N].sum()) <= 1e-6, (laps[0], ref.x[:spec.N].sum())
     assert sum(s == 'optimal' for s in res.status) >= B - 1, res.status
+
+
+def test_batched_device_restoration_matches_single_instance():
+    ''' drone cold starts that need IPOPT's feasibility restoration (race N=5, K=2): the batched
+    restoration phase reproduces the single-instance solver on instance 1 and every instance
+    converges '''
+    from aircraft_trajectory_optimization_amd.solver.batched_ipm import device_solver
+    from aircraft_trajectory_optimization_amd.tracks import make_spec
+    spec = make_spec(track='race', N=5, K=2)
+    B = 2
+    rng = np.random.default_rng(0)
+    W = np.repeat(spec.w0[None], B, axis=0)
+    W[1, :spec.N] *= 1 + 0.1 * rng.uniform(-1, 1, spec.N)
+    opts = IPMOptions(max_iter=300)
+    res = device_solver(spec, B, spec.lbw, spec.ubw, opts).solve(W)
+    assert res.stats['restorations'] > 0
+    assert all(s == 'optimal' for s in res.status), res.status
+    ref = _host_solve(spec, W[1], spec.lbw, spec.ubw, opts)
+    assert ref.status == 'optimal' and ref.stats['restorations'] > 0
+    assert abs(int(res.iters[1]) - ref.iters) <= 2
+    assert abs(float(res.x[:spec.N, 1].sum()) - ref.x[:spec.N].sum()) <= 1e-6

@@ -35,7 +35,7 @@ def run(B, max_iter, N=50, K=4, track='race', host_ref=True):
     t_setup = time.perf_counter() - t0
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    res = solver.solve(W)
+    res = solver.solve(W, progress=10)
     torch.cuda.synchronize()
     t_solve = time.perf_counter() - t0
     laps = res.x[:spec.N].sum(0).cpu().numpy()
