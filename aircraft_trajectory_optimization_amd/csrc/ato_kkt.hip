@@ -81,7 +81,7 @@ int fail(int code, const std::string& m) {
 constexpr int FT = 512;                   // factor threads per instance (16 x 32 grid)
 constexpr int ST = 256;                   // solve threads per instance
 constexpr int EPT = 8;                    // entries per thread and stage (<= 4096 per stage)
-constexpr int CH = 2048;                  // doubles per ring chunk of the solve
+constexpr int CH = 4096;                  // doubles per ring chunk of the solve (2 x 32 KB LDS ring)
 constexpr int CPT = CH / ST;              // chunk doubles per thread
 constexpr double BK_ALPHA = 0.64038820320220756872767623199676;   // (1 + sqrt(17)) / 8
 constexpr int SRC_SHIFT = 29;
@@ -342,8 +342,13 @@ __global__ __launch_bounds__(FT) void k_kkt_factor(Plan P, Vals V, int batch, co
         }
         KST(0);     // assembly
         // ---- restricted Bunch-Kaufman elimination of the own positions (all decisions scalar)
-        Mask<NW> live;
+        Mask<NW> live;                // scalar copy: candidate scan, tile skipping
         live.set_range(0, A);
+        bool lvq[NQ];                 // per lane: position lane + 64 q live
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) lvq[q] = lane + 64 * q < A;
+        bool lvt = tid < A;           // per thread: its factor-column position tid live ...
+        int cit = tid;                // ... and its index among the live positions
         int kc = 0, steps = 0, par = 0;
         const int g0 = P.piv_off[s];
         const long long lstart = loff;
@@ -362,7 +367,7 @@ __global__ __launch_bounds__(FT) void k_kkt_factor(Plan P, Vals V, int batch, co
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
                 const int i = lane + 64 * q;
-                if (i < own && i != k && live.get(i)) key = max(key, mag_key(ck[i], i));
+                if (i < own && i != k && lvq[q]) key = max(key, mag_key(ck[i], i));
             }
             key = wave_max_u32(key);
             const int r = key ? 511 - (int)(key & 0x1FFu) : -1;
@@ -382,7 +387,7 @@ __global__ __launch_bounds__(FT) void k_kkt_factor(Plan P, Vals V, int batch, co
 #pragma unroll
                 for (int q = 0; q < NQ; ++q) {
                     const int i = lane + 64 * q;
-                    if (i < own && i != r && live.get(i)) key2 = max(key2, mag_key(cr[i], i));
+                    if (i < own && i != r && lvq[q]) key2 = max(key2, mag_key(cr[i], i));
                 }
                 key2 = wave_max_u32(key2);
                 const int j2 = key2 ? 511 - (int)(key2 & 0x1FFu) : -1;
@@ -424,14 +429,25 @@ __global__ __launch_bounds__(FT) void k_kkt_factor(Plan P, Vals V, int batch, co
             }
             const int nlive = live.count();
             const int ncol = type == 1 ? 2 : 1;
+            {
+                const int e1 = type == 1 ? k : (type == 2 ? k : p);
+                const int e2 = type == 1 ? r : -1;
+                lvt = lvt && tid != e1 && tid != e2;
+                cit -= (tid > e1 ? 1 : 0) + (e2 >= 0 && tid > e2 ? 1 : 0);
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) {
+                    const int i = lane + 64 * q;
+                    lvq[q] = lvq[q] && i != e1 && i != e2;
+                }
+            }
             if (tid == 0) {
                 pv[g0 + steps] = make_int2((type == 1 ? k : p) | (type << 16), type == 1 ? r : -1);
                 dv[3 * (g0 + steps) + 0] = i00;
                 dv[3 * (g0 + steps) + 1] = i01;
                 dv[3 * (g0 + steps) + 2] = i11;
             }
-            if (tid < A && live.get(tid)) {
-                const int ci = live.below(tid);
+            if (lvt) {
+                const int ci = cit;
                 if (type == 0) {
                     Lb[loff + ci] = cp[tid] * i00;
                 } else if (type == 1) {
@@ -596,7 +612,9 @@ __global__ __launch_bounds__(ST) void k_kkt_solve(Plan P, int batch, const int* 
 
     // ===================== forward: L y = b, then y <- D^{-1} y per stage =====================
     double y[NQ];
-    Mask<NW> live;
+    bool lv[NQ];          // position lane + 64 q live (wave 0)
+    int ci[NQ];           // live positions below it (its index in a compact factor column)
+    int nlive = 0;
     int s = -1, t = 0, steps = 0, A = 0, own = 0, p0 = 0, g0 = 0;
     long long off = 0;
     bool finished = false;
@@ -672,34 +690,39 @@ __global__ __launch_bounds__(ST) void k_kkt_solve(Plan P, int batch, const int* 
                         if (i < A) v += cvec[cb][i];
                         y[q] = v;
                     }
-                    live.set_range(0, A);
+#pragma unroll
+                    for (int q = 0; q < NQ; ++q) {
+                        const int i = lane + 64 * q;
+                        lv[q] = i < A;
+                        ci[q] = min(i, A);
+                    }
+                    nlive = A;
                     continue;
                 }
                 const int2 rec = s_piv[t];
                 const int type = __builtin_amdgcn_readfirstlane(rec.x >> 16);
                 const int pp = __builtin_amdgcn_readfirstlane(min(rec.x & 0xffff, NP - 1));
                 const int rr = __builtin_amdgcn_readfirstlane(min(max(rec.y, 0), NP - 1));
-                Mask<NW> nl = live;
-                nl.clear(pp);
-                if (type == 1) nl.clear(rr);
-                const int nlive = nl.count();
                 const int ncol = type == 1 ? 2 : 1;
-                if (off + (long long)nlive * ncol > limit) break;     // column not resident yet
+                const int nl_after = nlive - ncol;
+                if (off + (long long)nl_after * ncol > limit) break;     // column not resident yet
                 const double zp = lane_get<NQ>(y, pp);
                 const double zr = type == 1 ? lane_get<NQ>(y, rr) : 0.0;
 #pragma unroll
                 for (int q = 0; q < NQ; ++q) {
                     const int i = lane + 64 * q;
-                    if (i < A && nl.get(i)) {
-                        const int ci = nl.below(i);
-                        if (type == 1)
-                            y[q] -= ring.at(off + 2 * ci) * zp + ring.at(off + 2 * ci + 1) * zr;
+                    const bool two = type == 1;
+                    lv[q] = lv[q] && i != pp && !(two && i == rr);
+                    ci[q] -= (i > pp ? 1 : 0) + (two && i > rr ? 1 : 0);
+                    if (lv[q]) {
+                        if (two)
+                            y[q] -= ring.at(off + 2 * ci[q]) * zp + ring.at(off + 2 * ci[q] + 1) * zr;
                         else
-                            y[q] -= ring.at(off + ci) * zp;
+                            y[q] -= ring.at(off + ci[q]) * zp;
                     }
                 }
-                off += (long long)nlive * ncol;
-                live = nl;
+                off += (long long)nl_after * ncol;
+                nlive = nl_after;
                 ++t;
             }
             if (finished && lane == 0) s_done = 1;
@@ -765,39 +788,48 @@ __global__ __launch_bounds__(ST) void k_kkt_solve(Plan P, int batch, const int* 
                         else if (i < A) v = cvec[nb][P.carry_dst[p0 + i]];
                         y[q] = v;
                     }
-                    live.set_range(own, A);
+#pragma unroll
+                    for (int q = 0; q < NQ; ++q) {
+                        const int i = lane + 64 * q;
+                        lv[q] = i >= own && i < A;
+                        ci[q] = min(max(i - own, 0), A - own);
+                    }
+                    nlive = A - own;
                     continue;
                 }
                 const int2 rec = s_piv[t];
                 const int type = __builtin_amdgcn_readfirstlane(rec.x >> 16);
                 const int pp = __builtin_amdgcn_readfirstlane(min(rec.x & 0xffff, NP - 1));
                 const int rr = __builtin_amdgcn_readfirstlane(min(max(rec.y, 0), NP - 1));
-                const int nlive = live.count();
                 const int ncol = type == 1 ? 2 : 1;
                 const long long o = off - (long long)nlive * ncol;
                 if (o < lower) break;                             // column not resident yet
+                const bool two = type == 1;
                 double sp = 0.0, sr = 0.0;
 #pragma unroll
                 for (int q = 0; q < NQ; ++q) {
-                    const int i = lane + 64 * q;
-                    if (i < A && live.get(i)) {
-                        const int ci = live.below(i);
-                        if (type == 1) {
-                            sp += ring.at(o + 2 * ci) * y[q];
-                            sr += ring.at(o + 2 * ci + 1) * y[q];
+                    if (lv[q]) {
+                        if (two) {
+                            sp += ring.at(o + 2 * ci[q]) * y[q];
+                            sr += ring.at(o + 2 * ci[q] + 1) * y[q];
                         } else {
-                            sp += ring.at(o + ci) * y[q];
+                            sp += ring.at(o + ci[q]) * y[q];
                         }
                     }
                 }
                 sp = wave_sum(sp);
                 lane_set<NQ>(y, pp, lane_get<NQ>(y, pp) - sp, lane);
-                live.set(pp);
-                if (type == 1) {
+                if (two) {
                     sr = wave_sum(sr);
                     lane_set<NQ>(y, rr, lane_get<NQ>(y, rr) - sr, lane);
-                    live.set(rr);
                 }
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) {
+                    const int i = lane + 64 * q;
+                    lv[q] = lv[q] || i == pp || (two && i == rr);
+                    ci[q] += (i > pp ? 1 : 0) + (two && i > rr ? 1 : 0);
+                }
+                nlive += ncol;
                 off = o;
                 --t;
             }

@@ -47,24 +47,44 @@ def parse():
 
 
 def cpu_baseline(spec_kwargs, W, budget_s):
-    ''' the numpy oracle (tests-only code) timed on a bounded sample of the same workload '''
-    from tests.helpers import oracle_nlp
+    '''
+    SURVEY 8(d): the build's C++ CPU twin of ato_eval -- the same segment programs compiled with
+    g++ -O3 (tests/native/hostcheck.cpp, OpenMP over instances) -- timed on the host cores of the
+    same box on the same instances: one thread and all threads of this process' share
+    (OMP_NUM_THREADS). The numpy restatement (oracle, complex-step Jacobian) is reported beside it.
+    The reference's CasADi/IPOPT path cannot run anywhere in this pipeline.
+    '''
+    from tests.helpers import HostCheck, oracle_nlp
+    from aircraft_trajectory_optimization_amd.tracks import make_spec
+    hc = HostCheck(make_spec(**spec_kwargs).native_spec())
+    threads = max(1, int(os.environ.get('OMP_NUM_THREADS', os.cpu_count() or 1)))
+
+    def rate(nthreads, budget):
+        out = None
+        n, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < budget:
+            out = hc.eval_threads(W, nthreads, out)
+            n += W.shape[0]
+        return n / (time.perf_counter() - t0), n
+
+    r1, n1 = rate(1, budget_s / 3)
+    rT, nT = rate(threads, budget_s / 3)
     nlp = oracle_nlp(**spec_kwargs)
-    t0 = time.perf_counter()
-    n = 0
-    while n < W.shape[0]:
-        w = W[n]
+    t0, k = time.perf_counter(), 0
+    while k < 3:
+        w = W[k]
         nlp.g(w)
         nlp.jac_dense(w)
         nlp.f(w)
         nlp.grad_f(w)
-        n += 1
-        if time.perf_counter() - t0 > budget_s:
-            break
-    dt = time.perf_counter() - t0
-    return {'value': n / dt, 'unit': 'evals/s', 'cores': 1, 'kind': 'port',
-            'sample': f'{n} instances of the same 50x4x13 racetrack workload: oracle g + complex-step '
-                      f'dense J + f + grad f, numpy fp64, single thread, {dt:.1f} s'}
+        k += 1
+    r_np = k / (time.perf_counter() - t0)
+    return {'value': rT, 'unit': 'evals/s', 'cores': threads, 'kind': 'port',
+            'single_thread_value': r1, 'numpy_oracle_value': r_np,
+            'sample': f'C++ twin of ato_eval (g++ -O3 -march=x86-64-v3, OpenMP): {nT} evaluations on '
+                      f'{threads} threads and {n1} on 1 thread of the same {W.shape[0]} seeded 50x4x13 '
+                      f'racetrack instances (g, dg/dw, f, grad f), about {budget_s / 3:.0f} s each; numpy oracle '
+                      f'(complex-step dense J) {k} instances'}
 
 
 def batched_solve(B, max_iter):

@@ -68,7 +68,9 @@ def build_hostcheck(force=False):
     if not force and os.path.exists(HOSTCHECK_LIB) and \
             os.path.getmtime(HOSTCHECK_LIB) >= max(os.path.getmtime(s) for s in srcs):
         return HOSTCHECK_LIB
-    subprocess.check_call(['g++', '-std=c++20', '-O2', '-fPIC', '-shared', '-o', HOSTCHECK_LIB, HOSTCHECK_SRC])
+    # x86-64-v3 (AVX2), not -march=native: the library is built here and also runs on the GPU box's host
+    subprocess.check_call(['g++', '-std=c++20', '-O3', '-march=x86-64-v3', '-fopenmp', '-fPIC', '-shared', '-o',
+                           HOSTCHECK_LIB, HOSTCHECK_SRC])
     return HOSTCHECK_LIB
 
 
@@ -81,6 +83,7 @@ class HostCheck:
         lib.atoh_create.argtypes = [ctypes.POINTER(native.AtoProblemDesc), ctypes.POINTER(vp)]
         lib.atoh_last_error.restype = ctypes.c_char_p
         lib.atoh_eval.argtypes = [vp, ctypes.c_int, vp, vp, vp, vp, vp]
+        lib.atoh_eval_threads.argtypes = [vp, ctypes.c_int, vp, vp, vp, vp, vp, ctypes.c_int]
         lib.atoh_destroy.argtypes = [vp]
         lib.atoh_sizes.argtypes = [vp] + [ctypes.POINTER(ctypes.c_int32)] * 3
         lib.atoh_sparsity.argtypes = [vp, vp, vp]
@@ -117,6 +120,19 @@ class HostCheck:
         if rc != 0:
             raise RuntimeError(self.lib.atoh_last_error().decode())
         return g, J, f, gf
+
+    def eval_threads(self, W, nthreads, out=None):
+        ''' W (B, nw) -> the same outputs as eval, instances over nthreads OpenMP threads '''
+        W = np.ascontiguousarray(np.atleast_2d(W), dtype=np.float64)
+        B = W.shape[0]
+        if out is None:
+            out = (np.zeros((B, self.ng)), np.zeros((B, self.nnz)), np.zeros(B), np.zeros((B, self.nw)))
+        g, J, f, gf = out
+        rc = self.lib.atoh_eval_threads(self.h, B, W.ctypes.data, g.ctypes.data, J.ctypes.data, f.ctypes.data,
+                                        gf.ctypes.data, int(nthreads))
+        if rc != 0:
+            raise RuntimeError(self.lib.atoh_last_error().decode())
+        return out
 
     def hess_pattern(self):
         nnz, nc = ctypes.c_int32(), ctypes.c_int32()

@@ -123,6 +123,39 @@ int atoh_eval(const atoh_handle* h, int B, const double* w, double* g, double* J
     return 0;
 }
 
+// the same evaluation with the instances spread over nthreads OpenMP threads (CPU baseline)
+int atoh_eval_threads(const atoh_handle* h, int B, const double* w, double* g, double* J, double* f, double* gf,
+                      int nthreads) {
+    const ato::ProbD& p = h->L.p;
+    bool ok = true;
+#pragma omp parallel num_threads(nthreads)
+    {
+        std::vector<double> fpart(p.N);
+        bool lok = ato::with_model(p, [&]<class M>() {
+#pragma omp for schedule(static)
+            for (int b = 0; b < B; ++b) {
+                HostW<double> W{w + (long)b * p.nw, 1};
+                HostSink<double> s{J ? J + (long)b * p.nnz : nullptr, g ? g + (long)b * p.ng : nullptr, 1, 1, 0, 0};
+                const ato::GradOut<double> go{gf + (long)b * p.nw, 1, fpart.data(), 1};
+                for (int u = 0; u < p.n_units; ++u) {
+                    const int32_t* ut = p.units + 4 * u;
+                    ato::run_unit<M, double, 0, true, true>(p, ut[0], ut[1], ut[2], W, s, go);
+                }
+                f[b] = ato::reduce_cost(fpart.data(), 1, p.N);
+            }
+        });
+        if (!lok) {
+#pragma omp critical
+            ok = false;
+        }
+    }
+    if (!ok) {
+        last_err = "unsupported model";
+        return -1;
+    }
+    return 0;
+}
+
 int atoh_hess_sparsity(atoh_handle* h, int32_t* nnz, int32_t* n_colors) {
     if (!h->hess) {
         std::string e = h->HL.build(h->L);

@@ -31,7 +31,7 @@ for s in $STEPS; do
     case $s in
         tests) run pytest_gpu 600 python -m pytest tests -m gpu -q -x -p no:cacheprovider ;;
         smoke) run smoke 300 python -c 'import __graft_entry__ as g; g.smoke()' ;;
-        bench) run bench 400 python bench.py --steps 50 --warmup 10 ;;
+        bench) run bench 900 python bench.py --steps 50 --warmup 10 ;;
         bench32) run bench_f32 300 python bench.py --steps 50 --warmup 10 --dtype f32 --no-cpu-baseline --no-solve ;;
         benchim) run bench_im 300 python bench.py --steps 50 --warmup 10 --layout instance --no-cpu-baseline --no-solve ;;
         benchbig) run bench_b4096 300 python bench.py --steps 20 --warmup 5 --batch 4096 --no-cpu-baseline --no-solve ;;
