@@ -61,10 +61,12 @@ __device__ __forceinline__ unsigned long long kstamp() {
     const bool kst_on = blockIdx.x == 0;
 #define KST(i) do { if (kst_on) { const unsigned long long t_ = kstamp(); kst_acc[i] += t_ - kst_last; kst_last = t_; } } while (0)
 #define KST_DUMP(nsteps) do { if (kst_on && threadIdx.x == 0) { for (int i_ = 0; i_ < 8; ++i_) g_kkt_stamps[i_] = kst_acc[i_]; g_kkt_stamps[8] = (nsteps); } } while (0)
+#define KST_DUMP2(nsteps) do { if (kst_on && threadIdx.x == 0) { for (int i_ = 0; i_ < 4; ++i_) g_kkt_stamps[10 + i_] = kst_acc[i_]; g_kkt_stamps[14] = (nsteps); } } while (0)
 #else
 #define KST_DECL
 #define KST(i)
 #define KST_DUMP(nsteps)
+#define KST_DUMP2(nsteps)
 #endif
 
 int fail(int code, const std::string& m) {
@@ -608,6 +610,8 @@ __global__ __launch_bounds__(ST) void k_kkt_solve(Plan P, int batch, const int* 
     double stage_r[CPT];
 
     const long long total = min((long long)si[P.S].x, P.l_size);
+    int kst_steps = 0;
+    KST_DECL
     const long long nchunks = (total + CH - 1) / CH;
 
     // ===================== forward: L y = b, then y <- D^{-1} y per stage =====================
@@ -697,6 +701,7 @@ __global__ __launch_bounds__(ST) void k_kkt_solve(Plan P, int batch, const int* 
                         ci[q] = min(i, A);
                     }
                     nlive = A;
+                    KST(0);
                     continue;
                 }
                 const int2 rec = s_piv[t];
@@ -708,22 +713,24 @@ __global__ __launch_bounds__(ST) void k_kkt_solve(Plan P, int batch, const int* 
                 if (off + (long long)nl_after * ncol > limit) break;     // column not resident yet
                 const double zp = lane_get<NQ>(y, pp);
                 const double zr = type == 1 ? lane_get<NQ>(y, rr) : 0.0;
+                // branch-free: every lane reads (dead positions read a harmless ring word)
+                const bool two = type == 1;
 #pragma unroll
                 for (int q = 0; q < NQ; ++q) {
                     const int i = lane + 64 * q;
-                    const bool two = type == 1;
                     lv[q] = lv[q] && i != pp && !(two && i == rr);
                     ci[q] -= (i > pp ? 1 : 0) + (two && i > rr ? 1 : 0);
-                    if (lv[q]) {
-                        if (two)
-                            y[q] -= ring.at(off + 2 * ci[q]) * zp + ring.at(off + 2 * ci[q] + 1) * zr;
-                        else
-                            y[q] -= ring.at(off + ci[q]) * zp;
-                    }
+                    const int idx = two ? 2 * ci[q] : ci[q];
+                    const double l0 = ring.at(off + idx);
+                    const double l1 = ring.at(off + idx + 1);
+                    const double upd = two ? l0 * zp + l1 * zr : l0 * zp;
+                    y[q] = lv[q] ? y[q] - upd : y[q];
                 }
                 off += (long long)nl_after * ncol;
                 nlive = nl_after;
                 ++t;
+                ++kst_steps;
+                KST(1);
             }
             if (finished && lane == 0) s_done = 1;
         }
@@ -732,6 +739,7 @@ __global__ __launch_bounds__(ST) void k_kkt_solve(Plan P, int batch, const int* 
         if (done) break;
         ring_store(ring.buf, c + 2, stage_r, tid);
         __syncthreads();
+        KST(2);
         if (c + 2 > nchunks + 2) break;               // safety: never loop past the stream
     }
     __syncthreads();
@@ -795,6 +803,7 @@ __global__ __launch_bounds__(ST) void k_kkt_solve(Plan P, int batch, const int* 
                         ci[q] = min(max(i - own, 0), A - own);
                     }
                     nlive = A - own;
+                    KST(0);
                     continue;
                 }
                 const int2 rec = s_piv[t];
@@ -808,14 +817,10 @@ __global__ __launch_bounds__(ST) void k_kkt_solve(Plan P, int batch, const int* 
                 double sp = 0.0, sr = 0.0;
 #pragma unroll
                 for (int q = 0; q < NQ; ++q) {
-                    if (lv[q]) {
-                        if (two) {
-                            sp += ring.at(o + 2 * ci[q]) * y[q];
-                            sr += ring.at(o + 2 * ci[q] + 1) * y[q];
-                        } else {
-                            sp += ring.at(o + ci[q]) * y[q];
-                        }
-                    }
+                    const int idx = two ? 2 * ci[q] : ci[q];
+                    const double yv = lv[q] ? y[q] : 0.0;
+                    sp += ring.at(o + idx) * yv;
+                    sr += two ? ring.at(o + idx + 1) * yv : 0.0;
                 }
                 sp = wave_sum(sp);
                 lane_set<NQ>(y, pp, lane_get<NQ>(y, pp) - sp, lane);
@@ -832,6 +837,8 @@ __global__ __launch_bounds__(ST) void k_kkt_solve(Plan P, int batch, const int* 
                 nlive += ncol;
                 off = o;
                 --t;
+                ++kst_steps;
+                KST(1);
             }
             if (finished && lane == 0) s_done = 1;
         }
@@ -839,8 +846,12 @@ __global__ __launch_bounds__(ST) void k_kkt_solve(Plan P, int batch, const int* 
         if (s_done != 0) break;
         ring_store(ring.buf, c - 2, stage_r, tid);
         __syncthreads();
+        KST(2);
         if (c < -2) break;                                // safety
     }
+    KST(3);
+    KST_DUMP2(kst_steps);
+    (void)kst_steps;
 }
 
 template <int T>

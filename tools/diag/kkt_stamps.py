@@ -69,6 +69,8 @@ def main():
     kkt = DeviceKKT(plan, B)
     for _ in range(2):
         kkt.factor(H, bn.jac, dx, dr)
+    x = torch.randn((plan.dim, B), dtype=torch.float64, device='cuda', generator=g)
+    kkt.solve(x)
     torch.cuda.synchronize()
     out = (ctypes.c_uint64 * 16)()
     assert lib.ato_kkt_diag_stamps(ctypes.cast(out, ctypes.c_void_p)) == 0
@@ -79,6 +81,11 @@ def main():
     for i, name in enumerate(PHASES):
         if v[i]:
             print(f'  {name:18s} {v[i]:12.3e}  {v[i] / steps:8.0f} per step  {100 * v[i] / total:5.1f} %')
+    w = np.array(out[10:16], dtype=np.float64)
+    st2 = max(w[4], 1)
+    print(f'solve: steps={int(st2)} total clocks={w[:4].sum():.3e}')
+    for i, name in enumerate(['stage open/close', 'sweep steps', 'chunk barriers+stores', 'tail']):
+        print(f'  {name:22s} {w[i]:12.3e}  {w[i] / st2:8.0f} per step')
 
 
 if __name__ == '__main__':
