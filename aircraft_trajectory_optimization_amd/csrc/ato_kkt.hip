@@ -229,6 +229,16 @@ __device__ __forceinline__ unsigned mag_key(double v, int i) {
 
 constexpr int slot(int I, int J) { return I * (I + 1) / 2 + J; }
 
+// value of position p (= lane p % 64, register p / 64) of a per-lane array, wave-uniform
+template <int NQ>
+__device__ __forceinline__ double lane_pick(const double (&v)[NQ], int p) {
+    const int q = p >> 6;
+    double x = v[0];
+#pragma unroll
+    for (int k = 1; k < NQ; ++k) x = blend(x, v[k], q == k ? ~0ull : 0ull);
+    return readlane_f64(x, p & 63);
+}
+
 // ------------------------------------------------------------------------------------------
 // factorisation
 // ------------------------------------------------------------------------------------------
@@ -365,17 +375,21 @@ __global__ __launch_bounds__(FT) void k_kkt_factor(Plan P, Vals V, int batch, co
             lds_barrier();
             KST(1);     // extract + barrier
             // lambda = max_{i eligible, i != k} |A_ik| and its index r
+            // every lane keeps its column values: A_kk and lambda come back by readlane, not LDS
             unsigned key = 0u;
+            double cv[NQ];
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
                 const int i = lane + 64 * q;
-                if (i < own && i != k && lvq[q]) key = max(key, mag_key(ck[i], i));
+                cv[q] = ck[i];
+                if (i < own && i != k && lvq[q]) key = max(key, mag_key(cv[q], i));
             }
             key = wave_max_u32(key);
             const int r = key ? 511 - (int)(key & 0x1FFu) : -1;
-            const double akk = uni(ck[k]);
-            const double lam = r >= 0 ? fabs(uni(ck[r])) : 0.0;
+            const double akk = lane_pick<NQ>(cv, k);
+            const double lam = r >= 0 ? fabs(lane_pick<NQ>(cv, r)) : 0.0;
             int type;            // 0: 1x1 at p, 1: 2x2 (k, r), 2: zero column
+            double arr = 0.0;    // A_rr (when column r was extracted)
             int p = k;
             bool use_r = false;
             if (r < 0 || lam == 0.0) {
@@ -386,15 +400,17 @@ __global__ __launch_bounds__(FT) void k_kkt_factor(Plan P, Vals V, int batch, co
                 extract_column<T>(a, r, ti, tj, cr);
                 lds_barrier();
                 unsigned key2 = 0u;
+                double cw[NQ];
 #pragma unroll
                 for (int q = 0; q < NQ; ++q) {
                     const int i = lane + 64 * q;
-                    if (i < own && i != r && lvq[q]) key2 = max(key2, mag_key(cr[i], i));
+                    cw[q] = cr[i];
+                    if (i < own && i != r && lvq[q]) key2 = max(key2, mag_key(cw[q], i));
                 }
                 key2 = wave_max_u32(key2);
                 const int j2 = key2 ? 511 - (int)(key2 & 0x1FFu) : -1;
-                const double sig = j2 >= 0 ? fabs(uni(cr[j2])) : 0.0;
-                const double arr = uni(cr[r]);
+                const double sig = j2 >= 0 ? fabs(lane_pick<NQ>(cw, j2)) : 0.0;
+                arr = lane_pick<NQ>(cw, r);
                 if (fabs(akk) * sig >= BK_ALPHA * lam * lam) {
                     type = 0;
                 } else if (fabs(arr) >= BK_ALPHA * sig) {
@@ -413,12 +429,12 @@ __global__ __launch_bounds__(FT) void k_kkt_factor(Plan P, Vals V, int batch, co
                 live.clear(k);
                 ++nzero;
             } else if (type == 0) {
-                const double d = uni(cp[p]);
+                const double d = use_r ? arr : akk;
                 i00 = 1.0 / d;
                 live.clear(p);
                 if (d > 0.0) ++npos; else ++nneg;
             } else {
-                const double A00 = akk, A01 = uni(ck[r]), A11 = uni(cr[r]);
+                const double A00 = akk, A01 = lane_pick<NQ>(cv, r), A11 = arr;
                 const double det = A00 * A11 - A01 * A01;
                 i00 = A11 / det;
                 i01 = -A01 / det;
@@ -474,17 +490,22 @@ __global__ __launch_bounds__(FT) void k_kkt_factor(Plan P, Vals V, int batch, co
                     cj[J][0] = cc[32 * J + tj];
                     cj[J][1] = cc[32 * J + 16 + tj];
                 }
+                // row factors of all tiles first (their LDS reads overlap), then the tiles of
+                // live row blocks; dead column tiles are updated too (harmless, no selects)
+                double li[T];
+#pragma unroll
+                for (int I = 0; I < T; ++I) {
+                    const int i = 32 * I + ti;
+                    li[I] = type == 0 ? cp[i] * fa : ck[i] * fa + cr[i] * fb;
+                }
 #pragma unroll
                 for (int I = 0; I < T; ++I) {
                     if (live.any_in_tile(I)) {
-                        const int i = 32 * I + ti;
-                        const double li = type == 0 ? cp[i] * fa : ck[i] * fa + cr[i] * fb;
 #pragma unroll
-                        for (int J = 0; J <= I; ++J)
-                            if (live.any_in_tile(J)) {
-                                a[slot(I, J)][0] = fma(-li, cj[J][0], a[slot(I, J)][0]);
-                                a[slot(I, J)][1] = fma(-li, cj[J][1], a[slot(I, J)][1]);
-                            }
+                        for (int J = 0; J <= I; ++J) {
+                            a[slot(I, J)][0] = fma(-li[I], cj[J][0], a[slot(I, J)][0]);
+                            a[slot(I, J)][1] = fma(-li[I], cj[J][1], a[slot(I, J)][1]);
+                        }
                     }
                 }
             }
