@@ -464,7 +464,11 @@ __global__ __launch_bounds__(FT) void k_kkt_factor(Plan P, Vals V, int batch, co
                 dv[3 * (g0 + steps) + 1] = i01;
                 dv[3 * (g0 + steps) + 2] = i11;
             }
+#ifdef ATO_KKT_EXP_NOSTORE
+            if (false) {              // DIAGNOSTIC experiment: no factor-column stores
+#else
             if (lvt) {
+#endif
                 const int ci = cit;
                 if (type == 0) {
                     Lb[loff + ci] = cp[tid] * i00;
@@ -478,7 +482,11 @@ __global__ __launch_bounds__(FT) void k_kkt_factor(Plan P, Vals V, int batch, co
             loff += (long long)nlive * ncol;
             KST(3);     // record + factor column stores
             // Schur update: one rank-1 pass (1x1 pivot) or two (2x2 pivot: A -= lk ck^T + lr cr^T)
+#ifdef ATO_KKT_EXP_NOUPD
+            const int npass = 0;      // DIAGNOSTIC experiment: no Schur update (wrong results)
+#else
             const int npass = type == 0 ? 1 : type == 1 ? 2 : 0;
+#endif
             for (int pass = 0; pass < npass; ++pass) {
                 const double* cc = type == 0 ? cp : (pass == 0 ? ck : cr);
                 const double fa = type == 0 ? i00 : (pass == 0 ? i00 : i01);
