@@ -229,6 +229,21 @@ __device__ __forceinline__ unsigned mag_key(double v, int i) {
 
 constexpr int slot(int I, int J) { return I * (I + 1) / 2 + J; }
 
+// rows 32I + ti (I < T) of a column held as v[q] = c[lane + 64q]: lanes 0-31 of v[q] hold tile 2q,
+// lanes 32-63 tile 2q + 1, and a self v_permlane32_swap broadcasts each half to the whole wave
+// (no LDS round trip for the row factors of the Schur update)
+template <int T, int NQ>
+__device__ __forceinline__ void column_rows(const double (&v)[NQ], double (&x)[T]) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        const uint2 u = __builtin_bit_cast(uint2, v[q]);
+        const auto lo = __builtin_amdgcn_permlane32_swap(u.x, u.x, false, false);
+        const auto hi = __builtin_amdgcn_permlane32_swap(u.y, u.y, false, false);
+        if (2 * q < T) x[2 * q] = __builtin_bit_cast(double, make_uint2(lo[0], hi[0]));
+        if (2 * q + 1 < T) x[2 * q + 1] = __builtin_bit_cast(double, make_uint2(lo[1], hi[1]));
+    }
+}
+
 // value of position p (= lane p % 64, register p / 64) of a per-lane array, wave-uniform
 template <int NQ>
 __device__ __forceinline__ double lane_pick(const double (&v)[NQ], int p) {
@@ -392,6 +407,9 @@ __global__ __launch_bounds__(FT) void k_kkt_factor(Plan P, Vals V, int batch, co
             double arr = 0.0;    // A_rr (when column r was extracted)
             int p = k;
             bool use_r = false;
+            double cw[NQ];       // column r (when extracted), same lane layout as cv
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) cw[q] = 0.0;
             if (r < 0 || lam == 0.0) {
                 type = akk == 0.0 ? 2 : 0;
             } else if (fabs(akk) >= BK_ALPHA * lam) {
@@ -400,7 +418,6 @@ __global__ __launch_bounds__(FT) void k_kkt_factor(Plan P, Vals V, int batch, co
                 extract_column<T>(a, r, ti, tj, cr);
                 lds_barrier();
                 unsigned key2 = 0u;
-                double cw[NQ];
 #pragma unroll
                 for (int q = 0; q < NQ; ++q) {
                     const int i = lane + 64 * q;
@@ -421,7 +438,6 @@ __global__ __launch_bounds__(FT) void k_kkt_factor(Plan P, Vals V, int batch, co
                     type = 1;
                 }
             }
-            const double* cp = use_r ? cr : ck;
             KST(2);     // pivot search
             // ---- pivot record, inertia, factor columns, Schur update
             double i00 = 0.0, i01 = 0.0, i11 = 0.0;
@@ -436,9 +452,10 @@ __global__ __launch_bounds__(FT) void k_kkt_factor(Plan P, Vals V, int batch, co
             } else {
                 const double A00 = akk, A01 = lane_pick<NQ>(cv, r), A11 = arr;
                 const double det = A00 * A11 - A01 * A01;
-                i00 = A11 / det;
-                i01 = -A01 / det;
-                i11 = A00 / det;
+                const double rdet = 1.0 / det;
+                i00 = A11 * rdet;
+                i01 = -A01 * rdet;
+                i11 = A00 * rdet;
                 live.clear(k);
                 live.clear(r);
                 if (det < 0.0) { ++npos; ++nneg; }
@@ -464,48 +481,70 @@ __global__ __launch_bounds__(FT) void k_kkt_factor(Plan P, Vals V, int batch, co
                 dv[3 * (g0 + steps) + 1] = i01;
                 dv[3 * (g0 + steps) + 2] = i11;
             }
+            // row factors of the thread's rows 32I + ti: l0 = rows of L's first column, l1 of the
+            // second (2x2 pivot); A -= l0 c0^T (+ l1 cr^T), c0 = column p (1x1) or k (2x2)
+            double l0[T], l1[T];
+            {
+                double xk[T], xr[T];
+                column_rows<T, NQ>(cv, xk);
+                column_rows<T, NQ>(cw, xr);
+                if (type == 1) {
+#pragma unroll
+                    for (int I = 0; I < T; ++I) {
+                        l0[I] = xk[I] * i00 + xr[I] * i01;
+                        l1[I] = xk[I] * i01 + xr[I] * i11;
+                    }
+                } else {
+#pragma unroll
+                    for (int I = 0; I < T; ++I) {
+                        l0[I] = (use_r ? xr[I] : xk[I]) * i00;
+                        l1[I] = 0.0;
+                    }
+                }
+            }
 #ifdef ATO_KKT_EXP_NOSTORE
             if (false) {              // DIAGNOSTIC experiment: no factor-column stores
 #else
             if (lvt) {
 #endif
+                // position tid = row 32 tj + ti of the thread: its factor entries are l0[tj], l1[tj]
+                double v0 = l0[0], v1 = l1[0];
+#pragma unroll
+                for (int I = 1; I < T; ++I) {
+                    const unsigned long long m = tj == I ? ~0ull : 0ull;
+                    v0 = blend(v0, l0[I], m);
+                    v1 = blend(v1, l1[I], m);
+                }
                 const int ci = cit;
                 if (type == 0) {
-                    Lb[loff + ci] = cp[tid] * i00;
+                    Lb[loff + ci] = v0;
                 } else if (type == 1) {
-                    Lb[loff + 2 * ci] = ck[tid] * i00 + cr[tid] * i01;
-                    Lb[loff + 2 * ci + 1] = ck[tid] * i01 + cr[tid] * i11;
+                    Lb[loff + 2 * ci] = v0;
+                    Lb[loff + 2 * ci + 1] = v1;
                 } else {
                     Lb[loff + ci] = 0.0;
                 }
             }
             loff += (long long)nlive * ncol;
             KST(3);     // record + factor column stores
-            // Schur update: one rank-1 pass (1x1 pivot) or two (2x2 pivot: A -= lk ck^T + lr cr^T)
+            // Schur update: one rank-1 pass (1x1 pivot) or two (2x2 pivot); tiles of dead rows are
+            // skipped, dead column tiles are updated too (harmless, no per-tile branches)
 #ifdef ATO_KKT_EXP_NOUPD
             const int npass = 0;      // DIAGNOSTIC experiment: no Schur update (wrong results)
 #else
             const int npass = type == 0 ? 1 : type == 1 ? 2 : 0;
 #endif
             for (int pass = 0; pass < npass; ++pass) {
-                const double* cc = type == 0 ? cp : (pass == 0 ? ck : cr);
-                const double fa = type == 0 ? i00 : (pass == 0 ? i00 : i01);
-                const double fb = type == 0 ? 0.0 : (pass == 0 ? i01 : i11);
-                // no live masking: a dead row or column only ever feeds dead entries
+                const double* cc = pass == 1 ? cr : (use_r ? cr : ck);
                 double cj[T][2];
 #pragma unroll
                 for (int J = 0; J < T; ++J) {
                     cj[J][0] = cc[32 * J + tj];
                     cj[J][1] = cc[32 * J + 16 + tj];
                 }
-                // row factors of all tiles first (their LDS reads overlap), then the tiles of
-                // live row blocks; dead column tiles are updated too (harmless, no selects)
                 double li[T];
 #pragma unroll
-                for (int I = 0; I < T; ++I) {
-                    const int i = 32 * I + ti;
-                    li[I] = type == 0 ? cp[i] * fa : ck[i] * fa + cr[i] * fb;
-                }
+                for (int I = 0; I < T; ++I) li[I] = pass == 1 ? l1[I] : l0[I];
 #pragma unroll
                 for (int I = 0; I < T; ++I) {
                     if (live.any_in_tile(I)) {
