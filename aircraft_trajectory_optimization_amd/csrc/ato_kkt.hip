@@ -508,17 +508,16 @@ __global__ __launch_bounds__(FT) void k_kkt_factor(Plan P, Vals V, int batch, co
             if (lvt) {
 #endif
                 // position tid = row 32 tj + ti of the thread: its factor entries are l0[tj], l1[tj]
-                double v0 = l0[0], v1 = l1[0];
+                double v0 = l0[0];
 #pragma unroll
-                for (int I = 1; I < T; ++I) {
-                    const unsigned long long m = tj == I ? ~0ull : 0ull;
-                    v0 = blend(v0, l0[I], m);
-                    v1 = blend(v1, l1[I], m);
-                }
+                for (int I = 1; I < T; ++I) v0 = blend(v0, l0[I], tj == I ? ~0ull : 0ull);
                 const int ci = cit;
                 if (type == 0) {
                     Lb[loff + ci] = v0;
                 } else if (type == 1) {
+                    double v1 = l1[0];
+#pragma unroll
+                    for (int I = 1; I < T; ++I) v1 = blend(v1, l1[I], tj == I ? ~0ull : 0ull);
                     Lb[loff + 2 * ci] = v0;
                     Lb[loff + 2 * ci + 1] = v1;
                 } else {
