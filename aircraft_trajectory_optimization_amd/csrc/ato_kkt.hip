@@ -571,7 +571,9 @@ __global__ __launch_bounds__(FT) void k_kkt_factor(Plan P, Vals V, int batch, co
 #pragma unroll
                     for (int h = 0; h < 2; ++h) {
                         const int i = 32 * I + ti, j = 32 * J + 16 * h + tj;
-                        if (i >= own && i < A && j >= own && j < A) {
+                        // diagonal tiles hold both (i, j) and (j, i), which differ by rounding:
+                        // only the lower one writes (one writer per carry entry, deterministic)
+                        if (i >= own && i < A && j >= own && j < A && (I != J || i >= j)) {
                             carry[(i - own) * P.max_tq + (j - own)] = a[slot(I, J)][h];
                             carry[(j - own) * P.max_tq + (i - own)] = a[slot(I, J)][h];
                         }

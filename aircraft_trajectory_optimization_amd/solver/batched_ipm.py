@@ -137,21 +137,35 @@ class BatchedInteriorPoint:
         self.hr, self.hc = t(hr, torch.long), t(hc, torch.long)
         off = np.nonzero(hr != hc)[0]
         self.hoff, self.hr_off, self.hc_off = t(off, torch.long), t(hr[off], torch.long), t(hc[off], torch.long)
+        # deterministic sparse products: entries grouped by output row, summed in a fixed order
+        # per segment (segment_reduce), not by atomics (index_add_), so that a batched solve is
+        # reproducible run to run
+        jr_np, jc_np = np.repeat(np.arange(m), np.diff(ev.j_row_ptr)), np.asarray(ev.j_col)
+        self.j_len = t(np.diff(ev.j_row_ptr), torch.long)
+        pc = np.argsort(jc_np, kind='stable')
+        self.jt_src, self.jt_row = t(pc, torch.long), t(jr_np[pc], torch.long)
+        self.jt_len = t(np.bincount(jc_np, minlength=n), torch.long)
+        w_row = np.concatenate([hr, hc[off]])
+        w_col = np.concatenate([hc, hr[off]])
+        w_src = np.concatenate([np.arange(len(hr)), off])
+        pw = np.argsort(w_row, kind='stable')
+        self.w_src, self.w_col = t(w_src[pw], torch.long), t(w_col[pw], torch.long)
+        self.w_len = t(np.bincount(w_row, minlength=n), torch.long)
         self.stats = {'factorizations': 0, 'solves': 0, 'evals': 0, 'hess': 0}
 
     # ------------------------------------------------------------------ sparse products
+    @staticmethod
+    def _segsum(vals, lengths):
+        return torch.segment_reduce(vals, 'sum', lengths=lengths, axis=0, unsafe=True)
+
     def _Jx(self, Js, v):
-        out = torch.zeros((self.m, self.B), dtype=torch.float64, device=self.dev)
-        return out.index_add_(0, self.jr, Js * v[self.jc])
+        return self._segsum(Js * v[self.jc], self.j_len)
 
     def _JTy(self, Js, y):
-        out = torch.zeros((self.n, self.B), dtype=torch.float64, device=self.dev)
-        return out.index_add_(0, self.jc, Js * y[self.jr])
+        return self._segsum(Js[self.jt_src] * y[self.jt_row], self.jt_len)
 
     def _Wx(self, H, v):
-        out = torch.zeros((self.n, self.B), dtype=torch.float64, device=self.dev)
-        out.index_add_(0, self.hr, H * v[self.hc])
-        return out.index_add_(0, self.hc_off, H[self.hoff] * v[self.hr_off])
+        return self._segsum(H[self.w_src] * v[self.w_col], self.w_len)
 
     def _Kmul(self, H, Js, dx, dr, v):
         vx, vy = v[:self.n], v[self.n:]

@@ -77,6 +77,25 @@ def test_device_kkt_instance_list_and_refactor():
     assert np.abs(K @ x2[:, 2] - rhs.cpu().numpy()[:, 2]).max() <= 1e-8 * np.abs(K).max()
 
 
+def test_device_kkt_is_deterministic():
+    ''' repeated factorisations and solves of the same values are bitwise identical (every carried
+    Schur entry has one writer; the diagonal tiles' upper copies differ from the lower ones by rounding) '''
+    from aircraft_trajectory_optimization_amd.solver.kkt_device import DeviceKKT
+    spec = product_spec(track='race', N=6, K=4)
+    vals = [random_kkt_values(spec, seed) for seed in range(8)]
+    ev = vals[0][0]
+    plan = build_plan(ev.nw, ev.ng, var_stages(spec), ev.j_row_ptr, ev.j_col, ev.h_row_ptr, ev.h_col)
+    kkt = DeviceKKT(plan, 8)
+    H, J = _dev([v[1] for v in vals]), _dev([v[2] for v in vals])
+    dx, dr = _dev([v[3] for v in vals]), _dev([v[4] for v in vals])
+    rhs = torch.as_tensor(np.random.default_rng(5).standard_normal((plan.dim, 8)), device='cuda').contiguous()
+    outs = []
+    for _ in range(4):
+        kkt.factor(H, J, dx, dr)
+        outs.append(kkt.solve(rhs.clone()).clone())
+    assert all(torch.equal(outs[0], o) for o in outs[1:])
+
+
 def test_device_kkt_racetrack_full_size():
     ''' 50 x 4 racetrack (the bench structure): inertia and solution against the host block LDL^T '''
     from aircraft_trajectory_optimization_amd.solver.kkt_device import DeviceKKT
