@@ -689,6 +689,7 @@ __global__ __launch_bounds__(ST) void k_kkt_solve(Plan P, int batch, const int* 
     int ci[NQ];           // live positions below it (its index in a compact factor column)
     int nlive = 0;
     int s = -1, t = 0, steps = 0, A = 0, own = 0, p0 = 0, g0 = 0;
+    int2 rec_nx = make_int2(0, -1);   // pivot record of step t, read one step ahead (off the y chain)
     long long off = 0;
     bool finished = false;
     if (tid == 0) s_done = 0;
@@ -754,6 +755,7 @@ __global__ __launch_bounds__(ST) void k_kkt_solve(Plan P, int batch, const int* 
                     off = inf.y;
                     t = 0;
                     stage_records(pv, dvp, g0, steps, lane, s_piv, s_dinv);
+                    rec_nx = s_piv[0];
                     const int cb = s & 1;
 #pragma unroll
                     for (int q = 0; q < NQ; ++q) {
@@ -773,13 +775,14 @@ __global__ __launch_bounds__(ST) void k_kkt_solve(Plan P, int batch, const int* 
                     KST(0);
                     continue;
                 }
-                const int2 rec = s_piv[t];
+                const int2 rec = rec_nx;
                 const int type = __builtin_amdgcn_readfirstlane(rec.x >> 16);
                 const int pp = __builtin_amdgcn_readfirstlane(min(rec.x & 0xffff, NP - 1));
                 const int rr = __builtin_amdgcn_readfirstlane(min(max(rec.y, 0), NP - 1));
                 const int ncol = type == 1 ? 2 : 1;
                 const int nl_after = nlive - ncol;
                 if (off + (long long)nl_after * ncol > limit) break;     // column not resident yet
+                rec_nx = s_piv[min(t + 1, NP - 1)];
                 const double zp = lane_get<NQ>(y, pp);
                 const double zr = type == 1 ? lane_get<NQ>(y, rr) : 0.0;
                 // branch-free: every lane reads (dead positions read a harmless ring word)
@@ -856,6 +859,7 @@ __global__ __launch_bounds__(ST) void k_kkt_solve(Plan P, int batch, const int* 
                     off = s + 1 < P.S ? (long long)si[s + 1].y : total;   // stream end of this stage
                     t = steps - 1;
                     stage_records(pv, dvp, g0, steps, lane, s_piv, s_dinv);
+                    rec_nx = s_piv[max(t, 0)];
                     const int nb = (s + 1) & 1;
 #pragma unroll
                     for (int q = 0; q < NQ; ++q) {
@@ -875,13 +879,14 @@ __global__ __launch_bounds__(ST) void k_kkt_solve(Plan P, int batch, const int* 
                     KST(0);
                     continue;
                 }
-                const int2 rec = s_piv[t];
+                const int2 rec = rec_nx;
                 const int type = __builtin_amdgcn_readfirstlane(rec.x >> 16);
                 const int pp = __builtin_amdgcn_readfirstlane(min(rec.x & 0xffff, NP - 1));
                 const int rr = __builtin_amdgcn_readfirstlane(min(max(rec.y, 0), NP - 1));
                 const int ncol = type == 1 ? 2 : 1;
                 const long long o = off - (long long)nlive * ncol;
                 if (o < lower) break;                             // column not resident yet
+                rec_nx = s_piv[max(t - 1, 0)];
                 const bool two = type == 1;
                 double sp = 0.0, sr = 0.0;
 #pragma unroll
