@@ -783,20 +783,25 @@ __global__ __launch_bounds__(ST) void k_kkt_solve(Plan P, int batch, const int* 
                 const int nl_after = nlive - ncol;
                 if (off + (long long)nl_after * ncol > limit) break;     // column not resident yet
                 rec_nx = s_piv[min(t + 1, NP - 1)];
-                const double zp = lane_get<NQ>(y, pp);
-                const double zr = type == 1 ? lane_get<NQ>(y, rr) : 0.0;
-                // branch-free: every lane reads (dead positions read a harmless ring word)
+                // branch-free: every lane reads (dead positions read a harmless ring word); all the
+                // column reads are issued before y is touched, so one LDS round trip per step
                 const bool two = type == 1;
+                double c0[NQ], c1[NQ];
 #pragma unroll
                 for (int q = 0; q < NQ; ++q) {
                     const int i = lane + 64 * q;
                     lv[q] = lv[q] && i != pp && !(two && i == rr);
                     ci[q] -= (i > pp ? 1 : 0) + (two && i > rr ? 1 : 0);
                     const int idx = two ? 2 * ci[q] : ci[q];
-                    const double l0 = ring.at(off + idx);
-                    const double l1 = ring.at(off + idx + 1);
-                    const double upd = two ? l0 * zp + l1 * zr : l0 * zp;
-                    y[q] = lv[q] ? y[q] - upd : y[q];
+                    c0[q] = ring.at(off + idx);
+                    c1[q] = ring.at(off + idx + 1);
+                }
+                const double zp = lane_get<NQ>(y, pp);
+                const double zr = two ? lane_get<NQ>(y, rr) : 0.0;
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) {
+                    const double upd = two ? c0[q] * zp + c1[q] * zr : c0[q] * zp;
+                    y[q] = blend(y[q], y[q] - upd, lv[q] ? ~0ull : 0ull);
                 }
                 off += (long long)nl_after * ncol;
                 nlive = nl_after;
