@@ -893,13 +893,19 @@ __global__ __launch_bounds__(ST) void k_kkt_solve(Plan P, int batch, const int* 
                 if (o < lower) break;                             // column not resident yet
                 rec_nx = s_piv[max(t - 1, 0)];
                 const bool two = type == 1;
-                double sp = 0.0, sr = 0.0;
+                double c0[NQ], c1[NQ];     // all column reads first: one LDS round trip per step
 #pragma unroll
                 for (int q = 0; q < NQ; ++q) {
                     const int idx = two ? 2 * ci[q] : ci[q];
-                    const double yv = lv[q] ? y[q] : 0.0;
-                    sp += ring.at(o + idx) * yv;
-                    sr += two ? ring.at(o + idx + 1) * yv : 0.0;
+                    c0[q] = ring.at(o + idx);
+                    c1[q] = ring.at(o + idx + 1);
+                }
+                double sp = 0.0, sr = 0.0;
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) {
+                    const double yv = blend(0.0, y[q], lv[q] ? ~0ull : 0ull);
+                    sp += c0[q] * yv;
+                    sr += two ? c1[q] * yv : 0.0;
                 }
                 sp = wave_sum(sp);
                 lane_set<NQ>(y, pp, lane_get<NQ>(y, pp) - sp, lane);
