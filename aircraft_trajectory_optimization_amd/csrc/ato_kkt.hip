@@ -900,12 +900,14 @@ __global__ __launch_bounds__(ST) void k_kkt_solve(Plan P, int batch, const int* 
                     c0[q] = ring.at(o + idx);
                     c1[q] = ring.at(o + idx + 1);
                 }
+                // the PRODUCT is masked, not the operand: a dead lane reads an arbitrary ring word
+                // (possibly Inf / NaN), and 0 * Inf would poison the sum
                 double sp = 0.0, sr = 0.0;
 #pragma unroll
                 for (int q = 0; q < NQ; ++q) {
-                    const double yv = blend(0.0, y[q], lv[q] ? ~0ull : 0ull);
-                    sp += c0[q] * yv;
-                    sr += two ? c1[q] * yv : 0.0;
+                    const unsigned long long mq = lv[q] ? ~0ull : 0ull;
+                    sp += blend(0.0, c0[q] * y[q], mq);
+                    sr += two ? blend(0.0, c1[q] * y[q], mq) : 0.0;
                 }
                 sp = wave_sum(sp);
                 lane_set<NQ>(y, pp, lane_get<NQ>(y, pp) - sp, lane);

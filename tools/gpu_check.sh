@@ -20,6 +20,8 @@ run() {  # run <name> <seconds> <cmd...>
     timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
     local rc=$?
     echo "[gpu_check] $(date +%T) end $name rc=$rc" | tee -a "$OUT/steps.log"
+    # keep the summaries only: full traces would push gpurun_out/ past its 64 MiB copy-back limit
+    find "$OUT" \( -name '*_trace.csv' -o -name '*.db' -o -name '*.rocpd' \) -delete 2>/dev/null
     case $rc in
         0) ;;
         124|137|134|139|136|135) echo "[gpu_check] crash-like exit, stopping" | tee -a "$OUT/steps.log"; exit $rc ;;
@@ -46,6 +48,12 @@ for s in $STEPS; do
                    python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-solve
                run pmc_tcc 400 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d "$OUT/pmc_tcc" -o run -- \
                    python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-solve ;;
+        kkt)   run kkt_b512 200 python tools/bench_kkt.py --batch 512 --out "$OUT/kkt_b512.json"
+               run kkt_b64 200 python tools/bench_kkt.py --batch 64 --out "$OUT/kkt_b64.json"
+               run kkt_b1 200 python tools/bench_kkt.py --batch 1 --out "$OUT/kkt_b1.json" ;;
+        solve) run solve_b512 600 python tools/solve_batched.py --batch 512 --max-iter 200 --no-host --out "$OUT/solve_b512.json" ;;
+        solveprof) run solveprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/solveprof" -o run -- \
+                   python tools/solve_batched.py --batch 512 --max-iter 60 --no-host --out "$OUT/solveprof.json" ;;
         listpmc) run listpmc 120 rocprofv3 -L ;;
         mbpmc) run mb_fetch 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/mb_fetch" -o run -- ./tools/mb_store
                run mb_write 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/mb_write" -o run -- ./tools/mb_store ;;
