@@ -1,27 +1,31 @@
-// ato_kkt.hip -- batched staged LDL^T factorisation and solve of the interior-point KKT system
-// (include/ato_kkt.h). Replaces IPOPT's MUMPS / MA97 factorisation (ref:
+// ato_kkt.hip -- batched multifrontal LDL^T factorisation and solve of the interior-point KKT
+// system (include/ato_kkt.h). Replaces IPOPT's MUMPS / MA97 factorisation (ref:
 // drone3d/raceline/base_raceline.py:752-799, the `ipopt_time` of :182-189) for a batch of
-// independent instances; the plan tables come from solver/kkt_plan.py.
+// independent instances; the plan tables (fronts, levels, extend-add maps) come from
+// solver/kkt_plan.py.
 //
-// Factor (k_kkt_factor<T>): one 512-thread workgroup per instance walks the stages. The
-// augmented block of a stage (<= 32*T positions) lives in REGISTERS: thread (ti, tj) = (tid % 32,
-// tid / 32) holds A[32 I + ti][32 J + tj] and A[32 I + ti][32 J + 16 + tj] for every lower tile
-// J <= I (T(T+1) doubles; 2 waves per SIMD leave 256 VGPRs per lane).
-// Assembly goes through a 32-row LDS strip per tile row (entries scattered from the H / J /
-// diagonal arrays, plus the Schur complement carried from the previous stage). Own positions
-// are then eliminated by Bunch-Kaufman pivoting (1x1 or 2x2; candidates and the pivot search
-// restricted to own positions): the pivot column(s) are copied to LDS by their owners, every
-// wave reduces the same max / argmax, and every thread applies the rank-1 / rank-2 update to
-// its tiles (tiles without live rows are skipped). The factor columns are written compactly
-// (live positions only, physical order) into one contiguous stream per instance, with a pivot
-// record and the inverse pivot block per step. The trailing block (next stage's coupling rows +
-// border) goes to LDS and is added into the next stage's assembly.
+// Factor (k_front_factor<T>): one 512-thread workgroup per (front, instance) of a level. The
+// front's block (<= 32*T positions) lives in REGISTERS: thread (ti, tj) = (tid % 32, tid / 32)
+// holds A[32 I + ti][32 J + tj] and A[32 I + ti][32 J + 16 + tj] for every lower tile J <= I
+// (T(T+1) doubles). The original entries are assembled through a 32-row LDS strip per tile
+// row; the children's contribution blocks are then added in registers (extend-add through an
+// LDS position map, children in a fixed order). Own positions are eliminated by Bunch-Kaufman
+// pivoting (1x1 or 2x2; candidates and the pivot search restricted to own positions): the
+// pivot column(s) are copied to LDS by their owners, every wave reduces the same max /
+// argmax, and every thread applies the rank-1 / rank-2 update to its tiles (tiles without
+// live rows are skipped). The factor columns are written compactly (live positions only,
+// physical order) into the front's slice of the instance's stream, with a pivot record and
+// the inverse pivot block per step. The trailing block (the Schur complement) is the front's
+// contribution block, written to HBM for the parent's launch.
 //
-// Solve (k_kkt_solve<T>): one 256-thread workgroup per instance. Wave 0 runs the forward
-// (L y = b), D and backward (L^T x = z) sweeps with the stage vector in registers (4 positions
-// per lane); all four waves stream the factor columns through a two-slot LDS ring so that
-// the sweep reads LDS only.
+// Solve: k_front_fwd<T> (levels upwards: L y = b and the D solve of the own positions; the
+// trailing part of y is the front's contribution to its parent's right-hand side) and
+// k_front_bwd<T> (levels downwards: L^T x = z; the trailing values are final already). One
+// 256-thread workgroup per (front, instance): wave 0 sweeps with the front vector in
+// registers (4 positions per lane), all four waves stream the factor columns through a
+// two-slot LDS ring so that the sweep reads LDS only.
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <string>
 #include <vector>
 #include <cstdint>
@@ -31,43 +35,24 @@
 void ato_internal_set_error(const std::string& msg);   // ato_capi.hip: ato_last_error()
 
 struct ato_kkt {
-    int n = 0, m = 0, dim = 0, S = 0, T = 0, max_tq = 0, max_ent = 0;
-    int64_t l_size = 0;
-    int32_t *d_stage_ptr = nullptr, *d_n_own = nullptr, *d_pos_index = nullptr, *d_carry_dst = nullptr;
-    int32_t *d_ent_ptr = nullptr, *d_ent_pos = nullptr, *d_ent_src = nullptr, *d_piv_off = nullptr;
+    int n = 0, m = 0, dim = 0, F = 0, L = 0, max_ent = 0;
+    int64_t l_size = 0, cb_size = 0;
+    int32_t sc_size = 0;
+    std::vector<int32_t> level_ptr, level_tiles;
+    int32_t *d_pos_ptr = nullptr, *d_n_own = nullptr, *d_pos_index = nullptr, *d_parent_pos = nullptr;
+    int32_t *d_child_ptr = nullptr, *d_child_list = nullptr, *d_ent_ptr = nullptr, *d_ent_pos = nullptr;
+    int32_t *d_ent_src = nullptr, *d_piv_off = nullptr, *d_sc_off = nullptr;
+    int64_t *d_l_off = nullptr, *d_cb_off = nullptr;
     int32_t cap = 0;                 // instances with factor storage
     double* d_L = nullptr;           // [cap][l_size]
+    double* d_cb = nullptr;          // [cap][cb_size] contribution blocks
+    double* d_sc = nullptr;          // [cap][sc_size] solve contributions
     int2* d_piv = nullptr;           // [cap][dim] {p | type << 16, r}
     double* d_dinv = nullptr;        // [cap][dim][3]
-    int2* d_sinfo = nullptr;         // [cap][S+1] {steps, stream offset of the stage}; [S] = {total, 0}
+    int2* d_sinfo = nullptr;         // [cap][F] {steps, used stream length of the front}
 };
 
-#ifdef ATO_KKT_STAMPS
-// DIAGNOSTIC build only (tools/diag/kkt_stamps.py): shader-clock phase totals of block 0
-__device__ unsigned long long g_kkt_stamps[16];
-#endif
-
 namespace {
-
-#ifdef ATO_KKT_STAMPS
-__device__ __forceinline__ unsigned long long kstamp() {
-    unsigned long long t;
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-    __builtin_amdgcn_sched_barrier(0);
-    return t;
-}
-#define KST_DECL unsigned long long kst_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, kst_last = kstamp(); \
-    const bool kst_on = blockIdx.x == 0;
-#define KST(i) do { if (kst_on) { const unsigned long long t_ = kstamp(); kst_acc[i] += t_ - kst_last; kst_last = t_; } } while (0)
-#define KST_DUMP(nsteps) do { if (kst_on && threadIdx.x == 0) { for (int i_ = 0; i_ < 8; ++i_) g_kkt_stamps[i_] = kst_acc[i_]; g_kkt_stamps[8] = (nsteps); } } while (0)
-#define KST_DUMP2(nsteps) do { if (kst_on && threadIdx.x == 0) { for (int i_ = 0; i_ < 4; ++i_) g_kkt_stamps[10 + i_] = kst_acc[i_]; g_kkt_stamps[14] = (nsteps); } } while (0)
-#else
-#define KST_DECL
-#define KST(i)
-#define KST_DUMP(nsteps)
-#define KST_DUMP2(nsteps)
-#endif
 
 int fail(int code, const std::string& m) {
     ato_internal_set_error(m);
@@ -80,25 +65,32 @@ int fail(int code, const std::string& m) {
         if (e_ != hipSuccess) return fail(ATO_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(e_)); \
     } while (0)
 
-constexpr int FT = 512;                   // factor threads per instance (16 x 32 grid)
-constexpr int ST = 256;                   // solve threads per instance
-constexpr int EPT = 8;                    // entries per thread and stage (<= 4096 per stage)
+constexpr int FT = 512;                   // factor threads per (front, instance) (16 x 32 grid)
+constexpr int ST = 256;                   // solve threads per (front, instance)
+constexpr int EPT = 8;                    // entries per thread and front (<= 4096 per front)
 constexpr int CH = 4096;                  // doubles per ring chunk of the solve (2 x 32 KB LDS ring)
 constexpr int CPT = CH / ST;              // chunk doubles per thread
+constexpr int MAXT = 8;                   // strips per front in ent_ptr
 constexpr double BK_ALPHA = 0.64038820320220756872767623199676;   // (1 + sqrt(17)) / 8
 constexpr int SRC_SHIFT = 29;
 
 struct Plan {
-    int n, m, dim, S, max_tq;
-    const int* stage_ptr;
+    int n, m, dim, F;
+    const int* pos_ptr;
     const int* n_own;
     const int* pos_index;
-    const int* carry_dst;
+    const int* parent_pos;
+    const int* child_ptr;
+    const int* child_list;
     const int* ent_ptr;
     const int* ent_pos;
     const int2* ent_src;
+    const long long* l_off;
     const int* piv_off;
-    long long l_size;
+    const long long* cb_off;
+    const int* sc_off;
+    long long l_size, cb_size;
+    int sc_size;
 };
 
 struct Vals {
@@ -138,25 +130,10 @@ struct Mask {
 #pragma unroll
         for (int k = 0; k < NW; ++k) w[k] &= ~((((i >> 6) == k) ? 1ull : 0ull) << (i & 63));
     }
-    __device__ __forceinline__ void set(int i) {
-#pragma unroll
-        for (int k = 0; k < NW; ++k) w[k] |= (((i >> 6) == k) ? 1ull : 0ull) << (i & 63);
-    }
     __device__ __forceinline__ int count() const {
         int c = 0;
 #pragma unroll
         for (int k = 0; k < NW; ++k) c += __popcll(w[k]);
-        return c;
-    }
-    // live positions strictly below i
-    __device__ __forceinline__ int below(int i) const {
-        int c = 0;
-        const int wi = i >> 6;
-#pragma unroll
-        for (int k = 0; k < NW; ++k) {
-            if (k < wi) c += __popcll(w[k]);
-            else if (k == wi) c += __popcll(w[k] & ((1ull << (i & 63)) - 1ull));
-        }
         return c;
     }
     __device__ __forceinline__ bool any_in_tile(int I) const {   // positions 32I .. 32I+31
@@ -174,7 +151,7 @@ struct Mask {
 };
 
 // LDS-only workgroup barrier: waits for this wave's LDS operations, not for its global stores
-// (the factor columns written every step are read only by the solve launch)
+// (the factor columns written every step are read only by later launches)
 __device__ __forceinline__ void lds_barrier() { __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 template <int CTRL>
@@ -192,11 +169,6 @@ __device__ __forceinline__ double dpp_f64(double v) {
 __device__ __forceinline__ double readlane_f64(double v, int l) {
     return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l),
                             __builtin_amdgcn_readlane(__double2loint(v), l));
-}
-
-__device__ __forceinline__ double uni(double v) {   // wave-uniform copy (SGPRs)
-    return __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(v)),
-                            __builtin_amdgcn_readfirstlane(__double2loint(v)));
 }
 
 // max over the 64 lanes (all lanes active), returned as a scalar: DPP within each 16-lane row,
@@ -254,6 +226,12 @@ __device__ __forceinline__ double lane_pick(const double (&v)[NQ], int p) {
     return readlane_f64(x, p & 63);
 }
 
+template <int NQ>
+__device__ __forceinline__ void lane_set(double (&y)[NQ], int p, double v, int lane) {
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) y[k] = blend(y[k], v, ((p & 63) == lane && (p >> 6) == k) ? ~0ull : 0ull);
+}
+
 // ------------------------------------------------------------------------------------------
 // factorisation
 // ------------------------------------------------------------------------------------------
@@ -282,11 +260,20 @@ __device__ __forceinline__ void extract_column(const double (&a)[T * (T + 1) / 2
     }
 }
 
+__global__ void k_inertia_zero(int batch, const int* __restrict__ list, int* __restrict__ inertia) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= batch) return;
+    const int b = list ? list[i] : i;
+    inertia[3 * b + 0] = 0;
+    inertia[3 * b + 1] = 0;
+    inertia[3 * b + 2] = 0;
+}
+
 template <int T>
-__global__ __launch_bounds__(FT) void k_kkt_factor(Plan P, Vals V, int batch, const int* __restrict__ list,
-                                                   double* __restrict__ Lst, int2* __restrict__ piv,
-                                                   double* __restrict__ dinv, int2* __restrict__ sinfo,
-                                                   int* __restrict__ inertia) {
+__global__ __launch_bounds__(FT) void k_front_factor(Plan P, Vals V, int f0, int batch, const int* __restrict__ list,
+                                                     double* __restrict__ Lst, int2* __restrict__ piv,
+                                                     double* __restrict__ dinv, int2* __restrict__ sinfo,
+                                                     double* __restrict__ CB, int* __restrict__ inertia) {
     constexpr int NP = 32 * T;
     constexpr int NW = (NP + 63) / 64;
     constexpr int NQ = (NP + 63) / 64;
@@ -295,312 +282,302 @@ __global__ __launch_bounds__(FT) void k_kkt_factor(Plan P, Vals V, int batch, co
     extern __shared__ double smem[];
     double* strip = smem;                        // [32][SR]
     double* colb = strip + 32 * SR;              // [2 parity][2 (k, r)][NP]
-    double* carry = colb + 4 * NP;               // [max_tq][max_tq]
-    int* cdst = reinterpret_cast<int*>(carry + P.max_tq * P.max_tq);   // [max_tq]
+    int* inv = reinterpret_cast<int*>(colb + 4 * NP);   // [NP] position -> child trailing index
 
-    const int bi = blockIdx.x;
+    const int f = f0 + blockIdx.x;
+    const int bi = blockIdx.y;
     if (bi >= batch) return;
     const int b = list ? __builtin_amdgcn_readfirstlane(list[bi]) : bi;
     const int tid = threadIdx.x;
     const int ti = tid & 31, tj = tid >> 5;
     const int lane = tid & 63;
 
+    const int p0 = P.pos_ptr[f];
+    const int A = P.pos_ptr[f + 1] - p0;
+    const int own = P.n_own[f];
     double a[NS][2];
-    double* Lb = Lst + (long long)b * P.l_size;
-    int2* pv = piv + (long long)b * P.dim;
-    double* dv = dinv + (long long)b * P.dim * 3;
+    double* Lb = Lst + (long long)b * P.l_size + P.l_off[f];
+    int2* pv = piv + (long long)b * P.dim + P.piv_off[f];
+    double* dv = dinv + ((long long)b * P.dim + P.piv_off[f]) * 3;
     int npos = 0, nneg = 0, nzero = 0;
-    long long loff = 0;                          // running offset in the instance's column stream
-    int tq_in = 0;
-    int kst_steps = 0;
-    KST_DECL
+    long long loff = 0;                          // running offset in the front's column stream
 
-    for (int s = 0; s < P.S; ++s) {
-        const int p0 = P.stage_ptr[s];
-        const int A = P.stage_ptr[s + 1] - p0;
-        const int own = P.n_own[s];
-        // ---- this stage's entries (positions and values) into registers
-        const int e0 = P.ent_ptr[s * T], e1 = P.ent_ptr[(s + 1) * T];
-        int epos[EPT];
-        double eval[EPT];
+    // ---- original entries (positions and values) into registers
+    const int e0 = P.ent_ptr[f * MAXT], e1 = P.ent_ptr[(f + 1) * MAXT];
+    int epos[EPT];
+    double eval[EPT];
 #pragma unroll
-        for (int q = 0; q < EPT; ++q) {
-            const int e = e0 + tid + q * FT;
-            epos[q] = -1;
-            eval[q] = 0.0;
-            if (e < e1) {
-                epos[q] = P.ent_pos[e];
-                const int2 sc = P.ent_src[e];
-                eval[q] = src_value(V, sc.x, b) + src_value(V, sc.y, b);
-            }
+    for (int q = 0; q < EPT; ++q) {
+        const int e = e0 + tid + q * FT;
+        epos[q] = -1;
+        eval[q] = 0.0;
+        if (e < e1) {
+            epos[q] = P.ent_pos[e];
+            const int2 sc = P.ent_src[e];
+            eval[q] = src_value(V, sc.x, b) + src_value(V, sc.y, b);
         }
-        // ---- assemble strip by strip
+    }
+    // ---- assemble strip by strip
 #pragma unroll
-        for (int I = 0; I < T; ++I) {
-            if (32 * I < A) {
-                for (int i = tid; i < 32 * SR; i += FT) strip[i] = 0.0;
-                __syncthreads();
+    for (int I = 0; I < T; ++I) {
+        if (32 * I < A) {
+            for (int i = tid; i < 32 * SR; i += FT) strip[i] = 0.0;
+            __syncthreads();
 #pragma unroll
-                for (int q = 0; q < EPT; ++q) {
-                    const int pa = epos[q] >> 16, pb = epos[q] & 0xffff;
-                    if (epos[q] >= 0 && (pa >> 5) == I) {
-                        strip[(pa & 31) * SR + pb] = eval[q];
-                        if ((pb >> 5) == I && pa != pb) strip[(pb & 31) * SR + pa] = eval[q];
-                    }
+            for (int q = 0; q < EPT; ++q) {
+                const int pa = epos[q] >> 16, pb = epos[q] & 0xffff;
+                if (epos[q] >= 0 && (pa >> 5) == I) {
+                    strip[(pa & 31) * SR + pb] = eval[q];
+                    if ((pb >> 5) == I && pa != pb) strip[(pb & 31) * SR + pa] = eval[q];
                 }
-                __syncthreads();
-                // carry-in: Schur complement of the previous stage (full symmetric tq x tq)
-                for (int e = tid; e < tq_in * tq_in; e += FT) {
-                    const int q1 = e / tq_in, q2 = e - q1 * tq_in;
-                    const int d1 = cdst[q1], d2 = cdst[q2];
-                    if ((d1 >> 5) == I) strip[(d1 & 31) * SR + d2] += carry[q1 * P.max_tq + q2];
-                }
-                __syncthreads();
-#pragma unroll
-                for (int J = 0; J <= I; ++J) {
-                    a[slot(I, J)][0] = strip[ti * SR + 32 * J + tj];
-                    a[slot(I, J)][1] = strip[ti * SR + 32 * J + 16 + tj];
-                }
-                __syncthreads();
-            } else {
-#pragma unroll
-                for (int J = 0; J <= I; ++J) a[slot(I, J)][0] = a[slot(I, J)][1] = 0.0;
             }
+            __syncthreads();
+#pragma unroll
+            for (int J = 0; J <= I; ++J) {
+                a[slot(I, J)][0] = strip[ti * SR + 32 * J + tj];
+                a[slot(I, J)][1] = strip[ti * SR + 32 * J + 16 + tj];
+            }
+            __syncthreads();
+        } else {
+#pragma unroll
+            for (int J = 0; J <= I; ++J) a[slot(I, J)][0] = a[slot(I, J)][1] = 0.0;
         }
-        KST(0);     // assembly
-        // ---- restricted Bunch-Kaufman elimination of the own positions (all decisions scalar)
-        Mask<NW> live;                // scalar copy: candidate scan, tile skipping
-        live.set_range(0, A);
-        bool lvq[NQ];                 // per lane: position lane + 64 q live
+    }
+    // ---- extend-add of the children's contribution blocks (fixed child order: deterministic)
+    for (int ci = P.child_ptr[f]; ci < P.child_ptr[f + 1]; ++ci) {
+        const int c = P.child_list[ci];
+        const int pc = P.pos_ptr[c], oc = P.n_own[c];
+        const int tqc = P.pos_ptr[c + 1] - pc - oc;
+        const int* pm = P.parent_pos + pc + oc;
+        const double* cbc = CB + (long long)b * P.cb_size + P.cb_off[c];
+        for (int i = tid; i < NP; i += FT) inv[i] = -1;
+        __syncthreads();
+        for (int q = tid; q < tqc; q += FT) inv[pm[q]] = q;
+        __syncthreads();
+        int qr[T];
 #pragma unroll
-        for (int q = 0; q < NQ; ++q) lvq[q] = lane + 64 * q < A;
-        bool lvt = tid < A;           // per thread: its factor-column position tid live ...
-        int cit = tid;                // ... and its index among the live positions
-        int kc = 0, steps = 0, par = 0;
-        const int g0 = P.piv_off[s];
-        const long long lstart = loff;
-        while (true) {
-            while (kc < own && !live.get(kc)) ++kc;
-            if (kc >= own) break;
-            const int k = kc;
-            double* ck = colb + (par * 2 + 0) * NP;
-            double* cr = colb + (par * 2 + 1) * NP;
-            KST(7);
-            extract_column<T>(a, k, ti, tj, ck);
-            lds_barrier();
-            KST(1);     // extract + barrier
-            // lambda = max_{i eligible, i != k} |A_ik| and its index r
-            // every lane keeps its column values: A_kk and lambda come back by readlane, not LDS
-            unsigned key = 0u;
-            double cv[NQ];
+        for (int I = 0; I < T; ++I) qr[I] = inv[32 * I + ti];
 #pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                const int i = lane + 64 * q;
-                cv[q] = ck[i];
-                if (i < own && i != k && lvq[q]) key = max(key, mag_key(cv[q], i));
+        for (int J = 0; J < T; ++J) {
+            const int q0 = inv[32 * J + tj], q1 = inv[32 * J + 16 + tj];
+#pragma unroll
+            for (int I = J; I < T; ++I) {
+                if (qr[I] >= 0 && q0 >= 0) a[slot(I, J)][0] += cbc[(long long)qr[I] * tqc + q0];
+                if (qr[I] >= 0 && q1 >= 0) a[slot(I, J)][1] += cbc[(long long)qr[I] * tqc + q1];
             }
-            key = wave_max_u32(key);
-            const int r = key ? 511 - (int)(key & 0x1FFu) : -1;
-            const double akk = lane_pick<NQ>(cv, k);
-            const double lam = r >= 0 ? fabs(lane_pick<NQ>(cv, r)) : 0.0;
-            int type;            // 0: 1x1 at p, 1: 2x2 (k, r), 2: zero column
-            double arr = 0.0;    // A_rr (when column r was extracted)
-            int p = k;
-            bool use_r = false;
-            double cw[NQ];       // column r (when extracted), same lane layout as cv
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) cw[q] = 0.0;
-            if (r < 0 || lam == 0.0) {
-                type = akk == 0.0 ? 2 : 0;
-            } else if (fabs(akk) >= BK_ALPHA * lam) {
-                type = 0;
-            } else {
-                extract_column<T>(a, r, ti, tj, cr);
-                lds_barrier();
-                unsigned key2 = 0u;
-#pragma unroll
-                for (int q = 0; q < NQ; ++q) {
-                    const int i = lane + 64 * q;
-                    cw[q] = cr[i];
-                    if (i < own && i != r && lvq[q]) key2 = max(key2, mag_key(cw[q], i));
-                }
-                key2 = wave_max_u32(key2);
-                const int j2 = key2 ? 511 - (int)(key2 & 0x1FFu) : -1;
-                const double sig = j2 >= 0 ? fabs(lane_pick<NQ>(cw, j2)) : 0.0;
-                arr = lane_pick<NQ>(cw, r);
-                if (fabs(akk) * sig >= BK_ALPHA * lam * lam) {
-                    type = 0;
-                } else if (fabs(arr) >= BK_ALPHA * sig) {
-                    type = 0;
-                    p = r;
-                    use_r = true;
-                } else {
-                    type = 1;
-                }
-            }
-            KST(2);     // pivot search
-            // ---- pivot record, inertia, factor columns, Schur update
-            double i00 = 0.0, i01 = 0.0, i11 = 0.0;
-            if (type == 2) {
-                live.clear(k);
-                ++nzero;
-            } else if (type == 0) {
-                const double d = use_r ? arr : akk;
-                i00 = 1.0 / d;
-                live.clear(p);
-                if (d > 0.0) ++npos; else ++nneg;
-            } else {
-                const double A00 = akk, A01 = lane_pick<NQ>(cv, r), A11 = arr;
-                const double det = A00 * A11 - A01 * A01;
-                const double rdet = 1.0 / det;
-                i00 = A11 * rdet;
-                i01 = -A01 * rdet;
-                i11 = A00 * rdet;
-                live.clear(k);
-                live.clear(r);
-                if (det < 0.0) { ++npos; ++nneg; }
-                else if (A00 + A11 > 0.0) npos += 2;
-                else nneg += 2;
-            }
-            const int nlive = live.count();
-            const int ncol = type == 1 ? 2 : 1;
-            {
-                const int e1 = type == 1 ? k : (type == 2 ? k : p);
-                const int e2 = type == 1 ? r : -1;
-                lvt = lvt && tid != e1 && tid != e2;
-                cit -= (tid > e1 ? 1 : 0) + (e2 >= 0 && tid > e2 ? 1 : 0);
-#pragma unroll
-                for (int q = 0; q < NQ; ++q) {
-                    const int i = lane + 64 * q;
-                    lvq[q] = lvq[q] && i != e1 && i != e2;
-                }
-            }
-            if (tid == 0) {
-                pv[g0 + steps] = make_int2((type == 1 ? k : p) | (type << 16), type == 1 ? r : -1);
-                dv[3 * (g0 + steps) + 0] = i00;
-                dv[3 * (g0 + steps) + 1] = i01;
-                dv[3 * (g0 + steps) + 2] = i11;
-            }
-            // row factors of the thread's rows 32I + ti: l0 = rows of L's first column, l1 of the
-            // second (2x2 pivot); A -= l0 c0^T (+ l1 cr^T), c0 = column p (1x1) or k (2x2)
-            double l0[T], l1[T];
-            {
-                double xk[T], xr[T];
-                column_rows<T, NQ>(cv, xk);
-                column_rows<T, NQ>(cw, xr);
-                if (type == 1) {
-#pragma unroll
-                    for (int I = 0; I < T; ++I) {
-                        l0[I] = xk[I] * i00 + xr[I] * i01;
-                        l1[I] = xk[I] * i01 + xr[I] * i11;
-                    }
-                } else {
-#pragma unroll
-                    for (int I = 0; I < T; ++I) {
-                        l0[I] = (use_r ? xr[I] : xk[I]) * i00;
-                        l1[I] = 0.0;
-                    }
-                }
-            }
-#ifdef ATO_KKT_EXP_NOSTORE
-            if (false) {              // DIAGNOSTIC experiment: no factor-column stores
-#else
-            if (lvt) {
-#endif
-                // position tid = row 32 tj + ti of the thread: its factor entries are l0[tj], l1[tj]
-                double v0 = l0[0];
-#pragma unroll
-                for (int I = 1; I < T; ++I) v0 = blend(v0, l0[I], tj == I ? ~0ull : 0ull);
-                const int ci = cit;
-                if (type == 0) {
-                    Lb[loff + ci] = v0;
-                } else if (type == 1) {
-                    double v1 = l1[0];
-#pragma unroll
-                    for (int I = 1; I < T; ++I) v1 = blend(v1, l1[I], tj == I ? ~0ull : 0ull);
-                    Lb[loff + 2 * ci] = v0;
-                    Lb[loff + 2 * ci + 1] = v1;
-                } else {
-                    Lb[loff + ci] = 0.0;
-                }
-            }
-            loff += (long long)nlive * ncol;
-            KST(3);     // record + factor column stores
-            // Schur update: one rank-1 pass (1x1 pivot) or two (2x2 pivot); tiles of dead rows are
-            // skipped, dead column tiles are updated too (harmless, no per-tile branches)
-#ifdef ATO_KKT_EXP_NOUPD
-            const int npass = 0;      // DIAGNOSTIC experiment: no Schur update (wrong results)
-#else
-            const int npass = type == 0 ? 1 : type == 1 ? 2 : 0;
-#endif
-            for (int pass = 0; pass < npass; ++pass) {
-                const double* cc = pass == 1 ? cr : (use_r ? cr : ck);
-                double cj[T][2];
-#pragma unroll
-                for (int J = 0; J < T; ++J) {
-                    cj[J][0] = cc[32 * J + tj];
-                    cj[J][1] = cc[32 * J + 16 + tj];
-                }
-                double li[T];
-#pragma unroll
-                for (int I = 0; I < T; ++I) li[I] = pass == 1 ? l1[I] : l0[I];
-#pragma unroll
-                for (int I = 0; I < T; ++I) {
-                    if (live.any_in_tile(I)) {
-#pragma unroll
-                        for (int J = 0; J <= I; ++J) {
-                            a[slot(I, J)][0] = fma(-li[I], cj[J][0], a[slot(I, J)][0]);
-                            a[slot(I, J)][1] = fma(-li[I], cj[J][1], a[slot(I, J)][1]);
-                        }
-                    }
-                }
-            }
-            ++steps;
-            ++kst_steps;
-            par ^= 1;
-            KST(4);     // Schur update
-        }
-        if (tid == 0) sinfo[(long long)b * (P.S + 1) + s] = make_int2(steps, (int)lstart);
-        // ---- trailing Schur complement -> carry for the next stage
-        const int tq = A - own;
-        if (s + 1 < P.S) {
-#pragma unroll
-            for (int I = 0; I < T; ++I) {
-#pragma unroll
-                for (int J = 0; J <= I; ++J) {
-#pragma unroll
-                    for (int h = 0; h < 2; ++h) {
-                        const int i = 32 * I + ti, j = 32 * J + 16 * h + tj;
-                        // diagonal tiles hold both (i, j) and (j, i), which differ by rounding:
-                        // only the lower one writes (one writer per carry entry, deterministic)
-                        if (i >= own && i < A && j >= own && j < A && (I != J || i >= j)) {
-                            carry[(i - own) * P.max_tq + (j - own)] = a[slot(I, J)][h];
-                            carry[(j - own) * P.max_tq + (i - own)] = a[slot(I, J)][h];
-                        }
-                    }
-                }
-            }
-            if (tid < tq) cdst[tid] = P.carry_dst[p0 + own + tid];
-            tq_in = tq;
         }
         __syncthreads();
     }
-    KST(5);
-    KST_DUMP(kst_steps);
-    (void)kst_steps;
+    // ---- restricted Bunch-Kaufman elimination of the own positions (all decisions scalar)
+    Mask<NW> live;                // scalar copy: candidate scan, tile skipping
+    live.set_range(0, A);
+    bool lvq[NQ];                 // per lane: position lane + 64 q live
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) lvq[q] = lane + 64 * q < A;
+    bool lvt = tid < A;           // per thread: its factor-column position tid live ...
+    int cit = tid;                // ... and its index among the live positions
+    int kc = 0, steps = 0, par = 0;
+    while (true) {
+        while (kc < own && !live.get(kc)) ++kc;
+        if (kc >= own) break;
+        const int k = kc;
+        double* ck = colb + (par * 2 + 0) * NP;
+        double* cr = colb + (par * 2 + 1) * NP;
+        extract_column<T>(a, k, ti, tj, ck);
+        lds_barrier();
+        // lambda = max_{i eligible, i != k} |A_ik| and its index r
+        // every lane keeps its column values: A_kk and lambda come back by readlane, not LDS
+        unsigned key = 0u;
+        double cv[NQ];
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int i = lane + 64 * q;
+            cv[q] = ck[i];
+            if (i < own && i != k && lvq[q]) key = max(key, mag_key(cv[q], i));
+        }
+        key = wave_max_u32(key);
+        const int r = key ? 511 - (int)(key & 0x1FFu) : -1;
+        const double akk = lane_pick<NQ>(cv, k);
+        const double lam = r >= 0 ? fabs(lane_pick<NQ>(cv, r)) : 0.0;
+        int type;            // 0: 1x1 at p, 1: 2x2 (k, r), 2: zero column
+        double arr = 0.0;    // A_rr (when column r was extracted)
+        int p = k;
+        bool use_r = false;
+        double cw[NQ];       // column r (when extracted), same lane layout as cv
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) cw[q] = 0.0;
+        if (r < 0 || lam == 0.0) {
+            type = akk == 0.0 ? 2 : 0;
+        } else if (fabs(akk) >= BK_ALPHA * lam) {
+            type = 0;
+        } else {
+            extract_column<T>(a, r, ti, tj, cr);
+            lds_barrier();
+            unsigned key2 = 0u;
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const int i = lane + 64 * q;
+                cw[q] = cr[i];
+                if (i < own && i != r && lvq[q]) key2 = max(key2, mag_key(cw[q], i));
+            }
+            key2 = wave_max_u32(key2);
+            const int j2 = key2 ? 511 - (int)(key2 & 0x1FFu) : -1;
+            const double sig = j2 >= 0 ? fabs(lane_pick<NQ>(cw, j2)) : 0.0;
+            arr = lane_pick<NQ>(cw, r);
+            if (fabs(akk) * sig >= BK_ALPHA * lam * lam) {
+                type = 0;
+            } else if (fabs(arr) >= BK_ALPHA * sig) {
+                type = 0;
+                p = r;
+                use_r = true;
+            } else {
+                type = 1;
+            }
+        }
+        // ---- pivot record, inertia, factor columns, Schur update
+        double i00 = 0.0, i01 = 0.0, i11 = 0.0;
+        if (type == 2) {
+            live.clear(k);
+            ++nzero;
+        } else if (type == 0) {
+            const double d = use_r ? arr : akk;
+            i00 = 1.0 / d;
+            live.clear(p);
+            if (d > 0.0) ++npos; else ++nneg;
+        } else {
+            const double A00 = akk, A01 = lane_pick<NQ>(cv, r), A11 = arr;
+            const double det = A00 * A11 - A01 * A01;
+            const double rdet = 1.0 / det;
+            i00 = A11 * rdet;
+            i01 = -A01 * rdet;
+            i11 = A00 * rdet;
+            live.clear(k);
+            live.clear(r);
+            if (det < 0.0) { ++npos; ++nneg; }
+            else if (A00 + A11 > 0.0) npos += 2;
+            else nneg += 2;
+        }
+        const int nlive = live.count();
+        const int ncol = type == 1 ? 2 : 1;
+        {
+            const int e1p = type == 1 ? k : (type == 2 ? k : p);
+            const int e2p = type == 1 ? r : -1;
+            lvt = lvt && tid != e1p && tid != e2p;
+            cit -= (tid > e1p ? 1 : 0) + (e2p >= 0 && tid > e2p ? 1 : 0);
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const int i = lane + 64 * q;
+                lvq[q] = lvq[q] && i != e1p && i != e2p;
+            }
+        }
+        if (tid == 0) {
+            pv[steps] = make_int2((type == 1 ? k : p) | (type << 16), type == 1 ? r : -1);
+            dv[3 * steps + 0] = i00;
+            dv[3 * steps + 1] = i01;
+            dv[3 * steps + 2] = i11;
+        }
+        // row factors of the thread's rows 32I + ti: l0 = rows of L's first column, l1 of the
+        // second (2x2 pivot); A -= l0 c0^T (+ l1 cr^T), c0 = column p (1x1) or k (2x2)
+        double l0[T], l1[T];
+        {
+            double xk[T], xr[T];
+            column_rows<T, NQ>(cv, xk);
+            column_rows<T, NQ>(cw, xr);
+            if (type == 1) {
+#pragma unroll
+                for (int I = 0; I < T; ++I) {
+                    l0[I] = xk[I] * i00 + xr[I] * i01;
+                    l1[I] = xk[I] * i01 + xr[I] * i11;
+                }
+            } else {
+#pragma unroll
+                for (int I = 0; I < T; ++I) {
+                    l0[I] = (use_r ? xr[I] : xk[I]) * i00;
+                    l1[I] = 0.0;
+                }
+            }
+        }
+        if (lvt) {
+            // position tid = row 32 tj + ti of the thread: its factor entries are l0[tj], l1[tj]
+            double v0 = l0[0];
+#pragma unroll
+            for (int I = 1; I < T; ++I) v0 = blend(v0, l0[I], tj == I ? ~0ull : 0ull);
+            const int ci = cit;
+            if (type == 0) {
+                Lb[loff + ci] = v0;
+            } else if (type == 1) {
+                double v1 = l1[0];
+#pragma unroll
+                for (int I = 1; I < T; ++I) v1 = blend(v1, l1[I], tj == I ? ~0ull : 0ull);
+                Lb[loff + 2 * ci] = v0;
+                Lb[loff + 2 * ci + 1] = v1;
+            } else {
+                Lb[loff + ci] = 0.0;
+            }
+        }
+        loff += (long long)nlive * ncol;
+        // Schur update: one rank-1 pass (1x1 pivot) or two (2x2 pivot); tiles of dead rows are
+        // skipped, dead column tiles are updated too (harmless, no per-tile branches)
+        const int npass = type == 0 ? 1 : type == 1 ? 2 : 0;
+        for (int pass = 0; pass < npass; ++pass) {
+            const double* cc = pass == 1 ? cr : (use_r ? cr : ck);
+            double cj[T][2];
+#pragma unroll
+            for (int J = 0; J < T; ++J) {
+                cj[J][0] = cc[32 * J + tj];
+                cj[J][1] = cc[32 * J + 16 + tj];
+            }
+            double li[T];
+#pragma unroll
+            for (int I = 0; I < T; ++I) li[I] = pass == 1 ? l1[I] : l0[I];
+#pragma unroll
+            for (int I = 0; I < T; ++I) {
+                if (live.any_in_tile(I)) {
+#pragma unroll
+                    for (int J = 0; J <= I; ++J) {
+                        a[slot(I, J)][0] = fma(-li[I], cj[J][0], a[slot(I, J)][0]);
+                        a[slot(I, J)][1] = fma(-li[I], cj[J][1], a[slot(I, J)][1]);
+                    }
+                }
+            }
+        }
+        ++steps;
+        par ^= 1;
+    }
     if (tid == 0) {
-        sinfo[(long long)b * (P.S + 1) + P.S] = make_int2((int)loff, 0);
-        inertia[3 * b + 0] = npos;
-        inertia[3 * b + 1] = nneg;
-        inertia[3 * b + 2] = nzero;
+        sinfo[(long long)b * P.F + f] = make_int2(steps, (int)loff);
+        atomicAdd(&inertia[3 * b + 0], npos);
+        atomicAdd(&inertia[3 * b + 1], nneg);
+        atomicAdd(&inertia[3 * b + 2], nzero);
+    }
+    // ---- trailing Schur complement -> contribution block of the parent (HBM)
+    const int tq = A - own;
+    if (tq > 0) {
+        double* cb = CB + (long long)b * P.cb_size + P.cb_off[f];
+#pragma unroll
+        for (int I = 0; I < T; ++I) {
+#pragma unroll
+            for (int J = 0; J <= I; ++J) {
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int i = 32 * I + ti, j = 32 * J + 16 * h + tj;
+                    // diagonal tiles hold both (i, j) and (j, i), which differ by rounding:
+                    // only the lower one writes (one writer per entry, deterministic)
+                    if (i >= own && i < A && j >= own && j < A && (I != J || i >= j)) {
+                        cb[(long long)(i - own) * tq + (j - own)] = a[slot(I, J)][h];
+                        cb[(long long)(j - own) * tq + (i - own)] = a[slot(I, J)][h];
+                    }
+                }
+            }
+        }
     }
 }
 
 // ------------------------------------------------------------------------------------------
 // solve
 // ------------------------------------------------------------------------------------------
-// Stream of factor columns through a two-slot LDS ring. Forward: chunks 0, 1, 2, ... of
-// [0, total); backward: the same chunks in reverse. Chunk c lives in slot c & 1.
+// Stream of the front's factor columns through a two-slot LDS ring. Forward: chunks 0, 1, 2,
+// ... of [0, total); backward: the same chunks in reverse. Chunk c lives in slot c & 1.
 struct Ring {
     double* buf;           // [2][CH]
     __device__ __forceinline__ double at(long long off) const { return buf[off & (2 * CH - 1)]; }
@@ -630,151 +607,116 @@ __device__ __forceinline__ double lane_get(const double (&y)[NQ], int p) {
     return readlane_f64(v, p & 63);
 }
 
-template <int NQ>
-__device__ __forceinline__ void lane_set(double (&y)[NQ], int p, double v, int lane) {
-#pragma unroll
-    for (int k = 0; k < NQ; ++k) y[k] = blend(y[k], v, ((p & 63) == lane && (p >> 6) == k) ? ~0ull : 0ull);
-}
-
-// wave 0: stage the pivot records and inverse pivot blocks of a stage into LDS
-__device__ __forceinline__ void stage_records(const int2* __restrict__ pv, const double* __restrict__ dvp, int g0,
-                                              int steps, int lane, int2* s_piv, double* s_dinv) {
-    for (int u = lane; u < steps; u += 64) {
-        s_piv[u] = pv[g0 + u];
-        s_dinv[3 * u + 0] = dvp[3 * (g0 + u) + 0];
-        s_dinv[3 * u + 1] = dvp[3 * (g0 + u) + 1];
-        s_dinv[3 * u + 2] = dvp[3 * (g0 + u) + 2];
-    }
+__device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// the front's pivot records and inverse pivot blocks into LDS (all threads), then a barrier
+__device__ __forceinline__ void stage_records(const int2* __restrict__ pv, const double* __restrict__ dvp,
+                                              int steps, int tid, int2* s_piv, double* s_dinv) {
+    for (int u = tid; u < steps; u += ST) {
+        s_piv[u] = pv[u];
+        s_dinv[3 * u + 0] = dvp[3 * u + 0];
+        s_dinv[3 * u + 1] = dvp[3 * u + 1];
+        s_dinv[3 * u + 2] = dvp[3 * u + 2];
+    }
+}
+
+struct FrontSolve {
+    int f, b, p0, A, own, steps;
+    long long total;
+    const double* Lb;
+    const int2* pv;
+    const double* dvp;
+    double* xb;
+};
+
+__device__ __forceinline__ FrontSolve front_solve_setup(const Plan& P, int f, int b, const double* Lst,
+                                                        const int2* piv, const double* dinv,
+                                                        const int2* sinfo, double* x, long long sb) {
+    FrontSolve s;
+    s.f = f;
+    s.b = b;
+    s.p0 = P.pos_ptr[f];
+    s.A = P.pos_ptr[f + 1] - s.p0;
+    s.own = P.n_own[f];
+    const int2 inf = sinfo[(long long)b * P.F + f];
+    s.steps = min(max(inf.x, 0), s.own);
+    const long long cap = (long long)s.own * s.A - (long long)s.own * (s.own + 1) / 2;
+    s.total = min(max((long long)inf.y, 0ll), cap);
+    s.Lb = Lst + (long long)b * P.l_size + P.l_off[f];
+    s.pv = piv + (long long)b * P.dim + P.piv_off[f];
+    s.dvp = dinv + ((long long)b * P.dim + P.piv_off[f]) * 3;
+    s.xb = x + (long long)b * sb;
+    return s;
+}
+
 template <int T>
-__global__ __launch_bounds__(ST) void k_kkt_solve(Plan P, int batch, const int* __restrict__ list,
+__global__ __launch_bounds__(ST) void k_front_fwd(Plan P, int f0, int batch, const int* __restrict__ list,
                                                   const double* __restrict__ Lst, const int2* __restrict__ piv,
                                                   const double* __restrict__ dinv, const int2* __restrict__ sinfo,
-                                                  double* __restrict__ x, long long se, long long sb) {
+                                                  double* __restrict__ SC, double* __restrict__ x, long long se,
+                                                  long long sb) {
     constexpr int NP = 32 * T;
-    constexpr int NW = (NP + 63) / 64;
     constexpr int NQ = (NP + 63) / 64;
     __shared__ double ring_buf[2 * CH];
-    __shared__ double cvec[2][NP];            // carried trailing values (forward) / stage vector (backward)
+    __shared__ double cvec[NP];
     __shared__ int2 s_piv[NP];
     __shared__ double s_dinv[3 * NP];
     __shared__ int s_done;
 
-    const int bi = blockIdx.x;
+    const int bi = blockIdx.y;
     if (bi >= batch) return;
     const int b = list ? __builtin_amdgcn_readfirstlane(list[bi]) : bi;
+    const FrontSolve F = front_solve_setup(P, f0 + blockIdx.x, b, Lst, piv, dinv, sinfo, x, sb);
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const bool w0 = tid < 64;
-    const double* Lb = Lst + (long long)b * P.l_size;
-    const int2* pv = piv + (long long)b * P.dim;
-    const double* dvp = dinv + (long long)b * P.dim * 3;
-    const int2* si = sinfo + (long long)b * (P.S + 1);
-    double* xb = x + (long long)b * sb;
     Ring ring{ring_buf};
     double stage_r[CPT];
 
-    const long long total = min((long long)si[P.S].x, P.l_size);
-    int kst_steps = 0;
-    KST_DECL
-    const long long nchunks = (total + CH - 1) / CH;
-
-    // ===================== forward: L y = b, then y <- D^{-1} y per stage =====================
-    double y[NQ];
-    bool lv[NQ];          // position lane + 64 q live (wave 0)
-    int ci[NQ];           // live positions below it (its index in a compact factor column)
-    int nlive = 0;
-    int s = -1, t = 0, steps = 0, A = 0, own = 0, p0 = 0, g0 = 0;
-    int2 rec_nx = make_int2(0, -1);   // pivot record of step t, read one step ahead (off the y chain)
-    long long off = 0;
-    bool finished = false;
-    if (tid == 0) s_done = 0;
-    for (int i = tid; i < 2 * NP; i += ST) (&cvec[0][0])[i] = 0.0;
-    ring_load(Lb, total, 0, stage_r, tid);
+    // ---- right-hand side: own entries of b, zero trailing, plus the children's contributions
+    for (int i = tid; i < NP; i += ST) cvec[i] = i < F.own ? F.xb[(long long)P.pos_index[F.p0 + i] * se] : 0.0;
+    stage_records(F.pv, F.dvp, F.steps, tid, s_piv, s_dinv);
+    ring_load(F.Lb, F.total, 0, stage_r, tid);
     ring_store(ring.buf, 0, stage_r, tid);
-    ring_load(Lb, total, 1, stage_r, tid);
+    ring_load(F.Lb, F.total, 1, stage_r, tid);
     ring_store(ring.buf, 1, stage_r, tid);
     __syncthreads();
+    for (int ci = P.child_ptr[F.f]; ci < P.child_ptr[F.f + 1]; ++ci) {
+        const int c = P.child_list[ci];
+        const int pc = P.pos_ptr[c], oc = P.n_own[c];
+        const int tqc = P.pos_ptr[c + 1] - pc - oc;
+        const double* scc = SC + (long long)b * P.sc_size + P.sc_off[c];
+        for (int q = tid; q < tqc; q += ST) cvec[P.parent_pos[pc + oc + q]] += scc[q];
+        __syncthreads();
+    }
+
+    // ---- forward sweep L y = b (wave 0), factor columns streamed through the ring
+    double y[NQ];
+    bool lv[NQ];          // position lane + 64 q live
+    int ci[NQ];           // live positions below it (its index in a compact factor column)
+    if (w0) {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int i = lane + 64 * q;
+            y[q] = i < NP ? cvec[i] : 0.0;
+            lv[q] = i < F.A;
+            ci[q] = min(i, F.A);
+        }
+    }
+    int nlive = F.A, t = 0;
+    long long off = 0;
+    int2 rec_nx = F.steps > 0 ? s_piv[0] : make_int2(0, -1);   // record of step t, read one step ahead
+    const long long nchunks = (F.total + CH - 1) / CH;
+    if (tid == 0) s_done = 0;
     for (long long c = 0;; ++c) {
-        ring_load(Lb, total, c + 2, stage_r, tid);     // in flight while wave 0 sweeps
-        if (w0 && !finished) {
+        ring_load(F.Lb, F.total, c + 2, stage_r, tid);     // in flight while wave 0 sweeps
+        if (w0) {
             const long long limit = (c + 2) * CH;
-            while (true) {
-                if (s < 0 || t >= steps) {
-                    // ---- close the current stage: D solve, write own, carry trailing
-                    if (s >= 0) {
-                        for (int u = 0; u < steps; ++u) {
-                            const int2 rec = s_piv[u];
-                            const int type = __builtin_amdgcn_readfirstlane(rec.x >> 16);
-                            const int pp = __builtin_amdgcn_readfirstlane(min(rec.x & 0xffff, NP - 1));
-                            const double d0 = s_dinv[3 * u], d1 = s_dinv[3 * u + 1], d2 = s_dinv[3 * u + 2];
-                            if (type == 1) {
-                                const int rr = __builtin_amdgcn_readfirstlane(min(max(rec.y, 0), NP - 1));
-                                const double yp = lane_get<NQ>(y, pp), yr = lane_get<NQ>(y, rr);
-                                lane_set<NQ>(y, pp, d0 * yp + d1 * yr, lane);
-                                lane_set<NQ>(y, rr, d1 * yp + d2 * yr, lane);
-                            } else {
-                                lane_set<NQ>(y, pp, d0 * lane_get<NQ>(y, pp), lane);
-                            }
-                        }
-                        const int nb = (s + 1) & 1;
-#pragma unroll
-                        for (int q = 0; q < NQ; ++q) {
-                            const int i = lane + 64 * q;
-                            if (i < own) xb[(long long)P.pos_index[p0 + i] * se] = y[q];
-                        }
-                        for (int i = lane; i < NP; i += 64) cvec[nb][i] = 0.0;
-                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                        __builtin_amdgcn_wave_barrier();
-                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-                        for (int q = 0; q < NQ; ++q) {
-                            const int i = lane + 64 * q;
-                            if (i >= own && i < A && s + 1 < P.S) cvec[nb][P.carry_dst[p0 + i]] = y[q];
-                        }
-                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                        __builtin_amdgcn_wave_barrier();
-                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                    }
-                    ++s;
-                    if (s >= P.S) {
-                        finished = true;
-                        break;
-                    }
-                    // ---- open stage s
-                    p0 = P.stage_ptr[s];
-                    A = P.stage_ptr[s + 1] - p0;
-                    own = P.n_own[s];
-                    g0 = P.piv_off[s];
-                    const int2 inf = si[s];
-                    steps = min(max(inf.x, 0), own);
-                    off = inf.y;
-                    t = 0;
-                    stage_records(pv, dvp, g0, steps, lane, s_piv, s_dinv);
-                    rec_nx = s_piv[0];
-                    const int cb = s & 1;
-#pragma unroll
-                    for (int q = 0; q < NQ; ++q) {
-                        const int i = lane + 64 * q;
-                        double v = 0.0;
-                        if (i < own) v = xb[(long long)P.pos_index[p0 + i] * se];
-                        if (i < A) v += cvec[cb][i];
-                        y[q] = v;
-                    }
-#pragma unroll
-                    for (int q = 0; q < NQ; ++q) {
-                        const int i = lane + 64 * q;
-                        lv[q] = i < A;
-                        ci[q] = min(i, A);
-                    }
-                    nlive = A;
-                    KST(0);
-                    continue;
-                }
+            while (t < F.steps) {
                 const int2 rec = rec_nx;
                 const int type = __builtin_amdgcn_readfirstlane(rec.x >> 16);
                 const int pp = __builtin_amdgcn_readfirstlane(min(rec.x & 0xffff, NP - 1));
@@ -783,8 +725,9 @@ __global__ __launch_bounds__(ST) void k_kkt_solve(Plan P, int batch, const int* 
                 const int nl_after = nlive - ncol;
                 if (off + (long long)nl_after * ncol > limit) break;     // column not resident yet
                 rec_nx = s_piv[min(t + 1, NP - 1)];
-                // branch-free: every lane reads (dead positions read a harmless ring word); all the
-                // column reads are issued before y is touched, so one LDS round trip per step
+                // branch-free: every lane reads (dead positions read a harmless ring word, and their
+                // update is discarded by the blend); all the column reads are issued before y is
+                // touched, so one LDS round trip per step
                 const bool two = type == 1;
                 double c0[NQ], c1[NQ];
 #pragma unroll
@@ -806,84 +749,95 @@ __global__ __launch_bounds__(ST) void k_kkt_solve(Plan P, int batch, const int* 
                 off += (long long)nl_after * ncol;
                 nlive = nl_after;
                 ++t;
-                ++kst_steps;
-                KST(1);
             }
-            if (finished && lane == 0) s_done = 1;
+            if (lane == 0) s_done = t >= F.steps ? 1 : 0;
         }
         __syncthreads();
-        const bool done = s_done != 0;
-        if (done) break;
+        if (s_done != 0) break;
         ring_store(ring.buf, c + 2, stage_r, tid);
         __syncthreads();
-        KST(2);
         if (c + 2 > nchunks + 2) break;               // safety: never loop past the stream
     }
+    if (!w0) return;
+    // ---- D solve of the own positions, own values out, trailing values to the parent
+    for (int u = 0; u < F.steps; ++u) {
+        const int2 rec = s_piv[u];
+        const int type = __builtin_amdgcn_readfirstlane(rec.x >> 16);
+        const int pp = __builtin_amdgcn_readfirstlane(min(rec.x & 0xffff, NP - 1));
+        const double d0 = s_dinv[3 * u], d1 = s_dinv[3 * u + 1], d2 = s_dinv[3 * u + 2];
+        if (type == 1) {
+            const int rr = __builtin_amdgcn_readfirstlane(min(max(rec.y, 0), NP - 1));
+            const double yp = lane_get<NQ>(y, pp), yr = lane_get<NQ>(y, rr);
+            lane_set<NQ>(y, pp, d0 * yp + d1 * yr, lane);
+            lane_set<NQ>(y, rr, d1 * yp + d2 * yr, lane);
+        } else {
+            lane_set<NQ>(y, pp, d0 * lane_get<NQ>(y, pp), lane);
+        }
+    }
+    double* scf = SC + (long long)b * P.sc_size + P.sc_off[F.f];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        const int i = lane + 64 * q;
+        if (i < F.own) F.xb[(long long)P.pos_index[F.p0 + i] * se] = y[q];
+        else if (i < F.A) scf[i - F.own] = y[q];
+    }
+}
+
+template <int T>
+__global__ __launch_bounds__(ST) void k_front_bwd(Plan P, int f0, int batch, const int* __restrict__ list,
+                                                  const double* __restrict__ Lst, const int2* __restrict__ piv,
+                                                  const double* __restrict__ dinv, const int2* __restrict__ sinfo,
+                                                  double* __restrict__ x, long long se, long long sb) {
+    constexpr int NP = 32 * T;
+    constexpr int NQ = (NP + 63) / 64;
+    __shared__ double ring_buf[2 * CH];
+    __shared__ double cvec[NP];
+    __shared__ int2 s_piv[NP];
+    __shared__ double s_dinv[3 * NP];
+    __shared__ int s_done;
+
+    const int bi = blockIdx.y;
+    if (bi >= batch) return;
+    const int b = list ? __builtin_amdgcn_readfirstlane(list[bi]) : bi;
+    const FrontSolve F = front_solve_setup(P, f0 + blockIdx.x, b, Lst, piv, dinv, sinfo, x, sb);
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const bool w0 = tid < 64;
+    Ring ring{ring_buf};
+    double stage_r[CPT];
+    const long long nchunks = (F.total + CH - 1) / CH;
+    const long long clast = nchunks - 1;
+
+    // own: the forward (D-scaled) values; trailing: final values of the ancestors' positions
+    for (int i = tid; i < NP; i += ST) cvec[i] = i < F.A ? F.xb[(long long)P.pos_index[F.p0 + i] * se] : 0.0;
+    stage_records(F.pv, F.dvp, F.steps, tid, s_piv, s_dinv);
+    ring_load(F.Lb, F.total, clast, stage_r, tid);
+    ring_store(ring.buf, clast, stage_r, tid);
+    ring_load(F.Lb, F.total, clast - 1, stage_r, tid);
+    ring_store(ring.buf, clast - 1, stage_r, tid);
+    if (tid == 0) s_done = 0;
     __syncthreads();
 
-    // ===================== backward: L^T x = z, stages and steps in reverse =====================
-    if (tid == 0) s_done = 0;
-    const long long clast = nchunks - 1;
-    ring_load(Lb, total, clast, stage_r, tid);
-    ring_store(ring.buf, clast, stage_r, tid);
-    ring_load(Lb, total, clast - 1, stage_r, tid);
-    ring_store(ring.buf, clast - 1, stage_r, tid);
-    __syncthreads();
-    s = P.S;
-    t = -1;
-    finished = false;
+    double y[NQ];
+    bool lv[NQ];
+    int ci[NQ];
+    if (w0) {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int i = lane + 64 * q;
+            y[q] = i < NP ? cvec[i] : 0.0;
+            lv[q] = i >= F.own && i < F.A;
+            ci[q] = min(max(i - F.own, 0), F.A - F.own);
+        }
+    }
+    int nlive = F.A - F.own, t = F.steps - 1;
+    long long off = F.total;                                  // stream end of this front
+    int2 rec_nx = s_piv[max(t, 0)];
     for (long long c = clast;; --c) {
-        ring_load(Lb, total, c - 2, stage_r, tid);
-        if (w0 && !finished) {
+        ring_load(F.Lb, F.total, c - 2, stage_r, tid);
+        if (w0) {
             const long long lower = (c - 1) * CH;          // chunks c-1 and c are resident
-            while (true) {
-                if (s >= P.S || t < 0) {
-                    if (s < P.S) {
-                        // ---- close stage s: write own positions, keep the stage vector for s-1
-#pragma unroll
-                        for (int q = 0; q < NQ; ++q) {
-                            const int i = lane + 64 * q;
-                            if (i < own) xb[(long long)P.pos_index[p0 + i] * se] = y[q];
-                            if (i < A) cvec[s & 1][i] = y[q];
-                        }
-                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                        __builtin_amdgcn_wave_barrier();
-                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                    }
-                    --s;
-                    if (s < 0) {
-                        finished = true;
-                        break;
-                    }
-                    p0 = P.stage_ptr[s];
-                    A = P.stage_ptr[s + 1] - p0;
-                    own = P.n_own[s];
-                    g0 = P.piv_off[s];
-                    const int2 inf = si[s];
-                    steps = min(max(inf.x, 0), own);
-                    off = s + 1 < P.S ? (long long)si[s + 1].y : total;   // stream end of this stage
-                    t = steps - 1;
-                    stage_records(pv, dvp, g0, steps, lane, s_piv, s_dinv);
-                    rec_nx = s_piv[max(t, 0)];
-                    const int nb = (s + 1) & 1;
-#pragma unroll
-                    for (int q = 0; q < NQ; ++q) {
-                        const int i = lane + 64 * q;
-                        double v = 0.0;
-                        if (i < own) v = xb[(long long)P.pos_index[p0 + i] * se];
-                        else if (i < A) v = cvec[nb][P.carry_dst[p0 + i]];
-                        y[q] = v;
-                    }
-#pragma unroll
-                    for (int q = 0; q < NQ; ++q) {
-                        const int i = lane + 64 * q;
-                        lv[q] = i >= own && i < A;
-                        ci[q] = min(max(i - own, 0), A - own);
-                    }
-                    nlive = A - own;
-                    KST(0);
-                    continue;
-                }
+            while (t >= 0) {
                 const int2 rec = rec_nx;
                 const int type = __builtin_amdgcn_readfirstlane(rec.x >> 16);
                 const int pp = __builtin_amdgcn_readfirstlane(min(rec.x & 0xffff, NP - 1));
@@ -924,43 +878,91 @@ __global__ __launch_bounds__(ST) void k_kkt_solve(Plan P, int batch, const int* 
                 nlive += ncol;
                 off = o;
                 --t;
-                ++kst_steps;
-                KST(1);
             }
-            if (finished && lane == 0) s_done = 1;
+            if (lane == 0) s_done = t < 0 ? 1 : 0;
         }
         __syncthreads();
         if (s_done != 0) break;
         ring_store(ring.buf, c - 2, stage_r, tid);
         __syncthreads();
-        KST(2);
         if (c < -2) break;                                // safety
     }
-    KST(3);
-    KST_DUMP2(kst_steps);
-    (void)kst_steps;
+    if (!w0) return;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        const int i = lane + 64 * q;
+        if (i < F.own) F.xb[(long long)P.pos_index[F.p0 + i] * se] = y[q];
+    }
 }
 
 template <int T>
-int launch_factor(const ato_kkt* h, const Plan& P, const Vals& V, int batch, const int* list, int* inertia,
-                  hipStream_t st) {
+size_t factor_lds() {
     constexpr int NP = 32 * T;
-    const size_t lds = sizeof(double) * (32 * (NP + 1) + 4 * NP + (size_t)h->max_tq * h->max_tq) +
-                       sizeof(int) * h->max_tq;
-    if (lds > 160 * 1024) return fail(ATO_ERR_UNSUPPORTED, "KKT factor: LDS need exceeds 160 KB");
-    hipLaunchKernelGGL(k_kkt_factor<T>, dim3(batch), dim3(FT), lds, st, P, V, batch, list, h->d_L, h->d_piv,
-                       h->d_dinv, h->d_sinfo, inertia);
+    return sizeof(double) * (32 * (NP + 1) + 4 * NP) + sizeof(int) * NP;
+}
+
+template <int T>
+int launch_factor_level(const ato_kkt* h, const Plan& P, const Vals& V, int f0, int nf, int batch, const int* list,
+                        int* inertia, hipStream_t st) {
+    hipLaunchKernelGGL(k_front_factor<T>, dim3(nf, batch), dim3(FT), factor_lds<T>(), st, P, V, f0, batch, list,
+                       h->d_L, h->d_piv, h->d_dinv, h->d_sinfo, h->d_cb, inertia);
     KKT_HIP(hipGetLastError());
     return ATO_OK;
 }
 
 template <int T>
-int launch_solve(const ato_kkt* h, const Plan& P, int batch, const int* list, double* x, long long se,
-                 long long sb, hipStream_t st) {
-    hipLaunchKernelGGL(k_kkt_solve<T>, dim3(batch), dim3(ST), 0, st, P, batch, list, h->d_L, h->d_piv, h->d_dinv,
-                       h->d_sinfo, x, se, sb);
+int launch_fwd_level(const ato_kkt* h, const Plan& P, int f0, int nf, int batch, const int* list, double* x,
+                     long long se, long long sb, hipStream_t st) {
+    hipLaunchKernelGGL(k_front_fwd<T>, dim3(nf, batch), dim3(ST), 0, st, P, f0, batch, list, h->d_L, h->d_piv,
+                       h->d_dinv, h->d_sinfo, h->d_sc, x, se, sb);
     KKT_HIP(hipGetLastError());
     return ATO_OK;
+}
+
+template <int T>
+int launch_bwd_level(const ato_kkt* h, const Plan& P, int f0, int nf, int batch, const int* list, double* x,
+                     long long se, long long sb, hipStream_t st) {
+    hipLaunchKernelGGL(k_front_bwd<T>, dim3(nf, batch), dim3(ST), 0, st, P, f0, batch, list, h->d_L, h->d_piv,
+                       h->d_dinv, h->d_sinfo, x, se, sb);
+    KKT_HIP(hipGetLastError());
+    return ATO_OK;
+}
+
+int factor_level(const ato_kkt* h, const Plan& P, const Vals& V, int l, int batch, const int* list, int* inertia,
+                 hipStream_t st) {
+    const int f0 = h->level_ptr[l], nf = h->level_ptr[l + 1] - f0;
+#define ATO_CALL(T_) launch_factor_level<T_>(h, P, V, f0, nf, batch, list, inertia, st)
+    switch (h->level_tiles[l]) {
+        case 1: return ATO_CALL(1);
+        case 2: return ATO_CALL(2);
+        case 3: return ATO_CALL(3);
+        case 4: return ATO_CALL(4);
+        case 5: return ATO_CALL(5);
+        case 6: return ATO_CALL(6);
+        case 7: return ATO_CALL(7);
+        case 8: return ATO_CALL(8);
+        default: return fail(ATO_ERR_UNSUPPORTED, "KKT tiles");
+    }
+#undef ATO_CALL
+}
+
+int solve_level(const ato_kkt* h, const Plan& P, int l, bool fwd, int batch, const int* list, double* x,
+                long long se, long long sb, hipStream_t st) {
+    const int f0 = h->level_ptr[l], nf = h->level_ptr[l + 1] - f0;
+#define ATO_CALL(T_) (fwd ? launch_fwd_level<T_>(h, P, f0, nf, batch, list, x, se, sb, st) \
+                          : launch_bwd_level<T_>(h, P, f0, nf, batch, list, x, se, sb, st))
+    switch (h->level_tiles[l]) {
+        case 1: return ATO_CALL(1);
+        case 2: return ATO_CALL(2);
+        case 3: return ATO_CALL(3);
+        case 4: return ATO_CALL(4);
+        case 5: return ATO_CALL(5);
+        case 6: return ATO_CALL(6);
+        case 7: return ATO_CALL(7);
+        case 8: return ATO_CALL(8);
+        default: return fail(ATO_ERR_UNSUPPORTED, "KKT tiles");
+    }
+#undef ATO_CALL
 }
 
 Plan make_plan(const ato_kkt* h) {
@@ -968,17 +970,23 @@ Plan make_plan(const ato_kkt* h) {
     P.n = h->n;
     P.m = h->m;
     P.dim = h->dim;
-    P.S = h->S;
-    P.max_tq = h->max_tq;
-    P.stage_ptr = h->d_stage_ptr;
+    P.F = h->F;
+    P.pos_ptr = h->d_pos_ptr;
     P.n_own = h->d_n_own;
     P.pos_index = h->d_pos_index;
-    P.carry_dst = h->d_carry_dst;
+    P.parent_pos = h->d_parent_pos;
+    P.child_ptr = h->d_child_ptr;
+    P.child_list = h->d_child_list;
     P.ent_ptr = h->d_ent_ptr;
     P.ent_pos = h->d_ent_pos;
     P.ent_src = reinterpret_cast<const int2*>(h->d_ent_src);
+    P.l_off = reinterpret_cast<const long long*>(h->d_l_off);
     P.piv_off = h->d_piv_off;
+    P.cb_off = reinterpret_cast<const long long*>(h->d_cb_off);
+    P.sc_off = h->d_sc_off;
     P.l_size = h->l_size;
+    P.cb_size = h->cb_size;
+    P.sc_size = h->sc_size;
     return P;
 }
 
@@ -992,11 +1000,12 @@ int upload(const V* host, size_t n, V** dev) {
 }
 
 void free_storage(ato_kkt* h) {
-    (void)hipFree(h->d_L);
-    (void)hipFree(h->d_piv);
-    (void)hipFree(h->d_dinv);
-    (void)hipFree(h->d_sinfo);
+    for (void* p : {(void*)h->d_L, (void*)h->d_cb, (void*)h->d_sc, (void*)h->d_piv, (void*)h->d_dinv,
+                    (void*)h->d_sinfo})
+        (void)hipFree(p);
     h->d_L = nullptr;
+    h->d_cb = nullptr;
+    h->d_sc = nullptr;
     h->d_piv = nullptr;
     h->d_dinv = nullptr;
     h->d_sinfo = nullptr;
@@ -1007,47 +1016,70 @@ void free_storage(ato_kkt* h) {
 
 extern "C" {
 
-#ifdef ATO_KKT_STAMPS
-int ato_kkt_diag_stamps(unsigned long long* out) {
-    KKT_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_kkt_stamps), sizeof(unsigned long long) * 16));
-    return ATO_OK;
-}
-#endif
-
 int ato_kkt_create(const ato_kkt_plan_desc* d, ato_kkt** out) {
     if (!d || !out) return fail(ATO_ERR_ARG, "null argument");
     *out = nullptr;
-    if (d->tiles < 1 || d->tiles > 8) return fail(ATO_ERR_UNSUPPORTED, "KKT blocks wider than 256 positions");
-    if (d->n_stages < 1 || d->n < 0 || d->m < 0) return fail(ATO_ERR_ARG, "bad KKT plan sizes");
+    if (d->n_fronts < 1 || d->n_levels < 1 || d->n < 0 || d->m < 0) return fail(ATO_ERR_ARG, "bad KKT plan sizes");
+    const int F = d->n_fronts, L = d->n_levels;
+    if (d->level_ptr[0] != 0 || d->level_ptr[L] != F) return fail(ATO_ERR_ARG, "KKT plan: levels do not cover the fronts");
     ato_kkt* h = new ato_kkt();
     h->n = d->n;
     h->m = d->m;
     h->dim = d->n + d->m;
-    h->S = d->n_stages;
-    h->T = d->tiles;
+    h->F = F;
+    h->L = L;
     h->l_size = d->l_size;
-    const int S = d->n_stages;
-    const int P = d->stage_ptr[S];
-    const int E = d->ent_ptr[S * d->tiles];
-    for (int s = 0; s < S; ++s) {
-        const int A = d->stage_ptr[s + 1] - d->stage_ptr[s];
-        if (A > 32 * d->tiles || d->n_own[s] > A) {
+    h->cb_size = d->cb_size;
+    h->sc_size = d->sc_size;
+    h->level_ptr.assign(d->level_ptr, d->level_ptr + L + 1);
+    h->level_tiles.assign(d->level_tiles, d->level_tiles + L);
+    const int P = d->pos_ptr[F];
+    const int E = d->ent_ptr[F * MAXT];
+    const int C = d->child_ptr[F];
+    int own_total = 0;
+    for (int l = 0; l < L; ++l) {
+        const int T = d->level_tiles[l];
+        if (T < 1 || T > 8) {
             delete h;
-            return fail(ATO_ERR_ARG, "KKT plan: stage larger than its tiles");
+            return fail(ATO_ERR_UNSUPPORTED, "KKT fronts wider than 256 positions");
         }
-        h->max_tq = std::max(h->max_tq, A - d->n_own[s]);
-        const int es = d->ent_ptr[(s + 1) * d->tiles] - d->ent_ptr[s * d->tiles];
-        h->max_ent = std::max(h->max_ent, es);
+        for (int f = d->level_ptr[l]; f < d->level_ptr[l + 1]; ++f) {
+            const int A = d->pos_ptr[f + 1] - d->pos_ptr[f];
+            const int es = d->ent_ptr[(f + 1) * MAXT] - d->ent_ptr[f * MAXT];
+            h->max_ent = std::max(h->max_ent, es);
+            own_total += d->n_own[f];
+            bool children_below = true;
+            for (int c = d->child_ptr[f]; c < d->child_ptr[f + 1]; ++c)
+                children_below = children_below && d->child_list[c] < d->level_ptr[l];
+            if (A > 32 * T || d->n_own[f] > A || !children_below) {
+                delete h;
+                return fail(ATO_ERR_ARG, "KKT plan: front larger than its level's tiles, or a child not below it");
+            }
+            for (int q = d->n_own[f]; q < A; ++q) {
+                const int pp = d->parent_pos[d->pos_ptr[f] + q];
+                if (pp < 0 || pp >= 256) {
+                    delete h;
+                    return fail(ATO_ERR_ARG, "KKT plan: trailing position without a parent position");
+                }
+            }
+        }
+    }
+    if (own_total != h->dim) {
+        delete h;
+        return fail(ATO_ERR_ARG, "KKT plan: own positions do not cover the KKT dimension");
     }
     if (h->max_ent > EPT * FT) {
         delete h;
-        return fail(ATO_ERR_UNSUPPORTED, "KKT plan: more than 4096 entries in one stage");
+        return fail(ATO_ERR_UNSUPPORTED, "KKT plan: more than 4096 entries in one front");
     }
     int rc = ATO_OK;
-    if ((rc = upload(d->stage_ptr, S + 1, &h->d_stage_ptr)) || (rc = upload(d->n_own, S, &h->d_n_own)) ||
-        (rc = upload(d->pos_index, P, &h->d_pos_index)) || (rc = upload(d->carry_dst, P, &h->d_carry_dst)) ||
-        (rc = upload(d->ent_ptr, S * d->tiles + 1, &h->d_ent_ptr)) || (rc = upload(d->ent_pos, E, &h->d_ent_pos)) ||
-        (rc = upload(d->ent_src, 2 * (size_t)E, &h->d_ent_src)) || (rc = upload(d->piv_off, S, &h->d_piv_off))) {
+    if ((rc = upload(d->pos_ptr, F + 1, &h->d_pos_ptr)) || (rc = upload(d->n_own, F, &h->d_n_own)) ||
+        (rc = upload(d->pos_index, P, &h->d_pos_index)) || (rc = upload(d->parent_pos, P, &h->d_parent_pos)) ||
+        (rc = upload(d->child_ptr, F + 1, &h->d_child_ptr)) || (rc = upload(d->child_list, C, &h->d_child_list)) ||
+        (rc = upload(d->ent_ptr, F * MAXT + 1, &h->d_ent_ptr)) || (rc = upload(d->ent_pos, E, &h->d_ent_pos)) ||
+        (rc = upload(d->ent_src, 2 * (size_t)E, &h->d_ent_src)) || (rc = upload(d->piv_off, F, &h->d_piv_off)) ||
+        (rc = upload(d->l_off, F, &h->d_l_off)) || (rc = upload(d->cb_off, F, &h->d_cb_off)) ||
+        (rc = upload(d->sc_off, F, &h->d_sc_off))) {
         ato_kkt_destroy(h);
         return rc;
     }
@@ -1058,8 +1090,10 @@ int ato_kkt_create(const ato_kkt_plan_desc* d, ato_kkt** out) {
 int ato_kkt_destroy(ato_kkt* h) {
     if (!h) return ATO_OK;
     free_storage(h);
-    for (int32_t* p : {h->d_stage_ptr, h->d_n_own, h->d_pos_index, h->d_carry_dst, h->d_ent_ptr, h->d_ent_pos,
-                       h->d_ent_src, h->d_piv_off})
+    for (void* p : {(void*)h->d_pos_ptr, (void*)h->d_n_own, (void*)h->d_pos_index, (void*)h->d_parent_pos,
+                    (void*)h->d_child_ptr, (void*)h->d_child_list, (void*)h->d_ent_ptr, (void*)h->d_ent_pos,
+                    (void*)h->d_ent_src, (void*)h->d_piv_off, (void*)h->d_l_off, (void*)h->d_cb_off,
+                    (void*)h->d_sc_off})
         (void)hipFree(p);
     delete h;
     return ATO_OK;
@@ -1069,10 +1103,13 @@ int ato_kkt_reserve(ato_kkt* h, int32_t max_batch) {
     if (!h || max_batch < 0) return fail(ATO_ERR_ARG, "bad argument");
     if (max_batch <= h->cap) return ATO_OK;
     free_storage(h);
-    KKT_HIP(hipMalloc((void**)&h->d_L, sizeof(double) * (size_t)h->l_size * max_batch));
-    KKT_HIP(hipMalloc((void**)&h->d_piv, sizeof(int2) * (size_t)h->dim * max_batch));
-    KKT_HIP(hipMalloc((void**)&h->d_dinv, sizeof(double) * 3 * (size_t)h->dim * max_batch));
-    KKT_HIP(hipMalloc((void**)&h->d_sinfo, sizeof(int2) * (size_t)(h->S + 1) * max_batch));
+    const size_t B = (size_t)max_batch;
+    KKT_HIP(hipMalloc((void**)&h->d_L, sizeof(double) * std::max<size_t>(1, (size_t)h->l_size * B)));
+    KKT_HIP(hipMalloc((void**)&h->d_cb, sizeof(double) * std::max<size_t>(1, (size_t)h->cb_size * B)));
+    KKT_HIP(hipMalloc((void**)&h->d_sc, sizeof(double) * std::max<size_t>(1, (size_t)h->sc_size * B)));
+    KKT_HIP(hipMalloc((void**)&h->d_piv, sizeof(int2) * (size_t)h->dim * B));
+    KKT_HIP(hipMalloc((void**)&h->d_dinv, sizeof(double) * 3 * (size_t)h->dim * B));
+    KKT_HIP(hipMalloc((void**)&h->d_sinfo, sizeof(int2) * (size_t)h->F * B));
     h->cap = max_batch;
     return ATO_OK;
 }
@@ -1083,20 +1120,17 @@ int ato_kkt_factor(ato_kkt* h, int32_t batch, const int32_t* list, int64_t se, i
     if (batch == 0) return ATO_OK;
     if (!list && batch > h->cap) return fail(ATO_ERR_STATE, "ato_kkt_reserve() too small for this batch");
     if (!h->d_L) return fail(ATO_ERR_STATE, "call ato_kkt_reserve() first");
+    if (batch > 65535) return fail(ATO_ERR_UNSUPPORTED, "KKT batch above 65535 instances per call");
     const Plan P = make_plan(h);
     const Vals V{H, J, dx, dr, se, sb};
     hipStream_t st = static_cast<hipStream_t>(stream);
-    switch (h->T) {
-        case 1: return launch_factor<1>(h, P, V, batch, list, inertia, st);
-        case 2: return launch_factor<2>(h, P, V, batch, list, inertia, st);
-        case 3: return launch_factor<3>(h, P, V, batch, list, inertia, st);
-        case 4: return launch_factor<4>(h, P, V, batch, list, inertia, st);
-        case 5: return launch_factor<5>(h, P, V, batch, list, inertia, st);
-        case 6: return launch_factor<6>(h, P, V, batch, list, inertia, st);
-        case 7: return launch_factor<7>(h, P, V, batch, list, inertia, st);
-        case 8: return launch_factor<8>(h, P, V, batch, list, inertia, st);
-        default: return fail(ATO_ERR_UNSUPPORTED, "KKT tiles");
+    hipLaunchKernelGGL(k_inertia_zero, dim3((batch + 255) / 256), dim3(256), 0, st, batch, list, inertia);
+    KKT_HIP(hipGetLastError());
+    for (int l = 0; l < h->L; ++l) {
+        const int rc = factor_level(h, P, V, l, batch, list, inertia, st);
+        if (rc != ATO_OK) return rc;
     }
+    return ATO_OK;
 }
 
 int ato_kkt_solve(ato_kkt* h, int32_t batch, const int32_t* list, int64_t se, int64_t sb, double* x,
@@ -1105,19 +1139,18 @@ int ato_kkt_solve(ato_kkt* h, int32_t batch, const int32_t* list, int64_t se, in
     if (batch == 0) return ATO_OK;
     if (!h->d_L) return fail(ATO_ERR_STATE, "call ato_kkt_reserve() first");
     if (!list && batch > h->cap) return fail(ATO_ERR_STATE, "ato_kkt_reserve() too small for this batch");
+    if (batch > 65535) return fail(ATO_ERR_UNSUPPORTED, "KKT batch above 65535 instances per call");
     const Plan P = make_plan(h);
     hipStream_t st = static_cast<hipStream_t>(stream);
-    switch (h->T) {
-        case 1: return launch_solve<1>(h, P, batch, list, x, se, sb, st);
-        case 2: return launch_solve<2>(h, P, batch, list, x, se, sb, st);
-        case 3: return launch_solve<3>(h, P, batch, list, x, se, sb, st);
-        case 4: return launch_solve<4>(h, P, batch, list, x, se, sb, st);
-        case 5: return launch_solve<5>(h, P, batch, list, x, se, sb, st);
-        case 6: return launch_solve<6>(h, P, batch, list, x, se, sb, st);
-        case 7: return launch_solve<7>(h, P, batch, list, x, se, sb, st);
-        case 8: return launch_solve<8>(h, P, batch, list, x, se, sb, st);
-        default: return fail(ATO_ERR_UNSUPPORTED, "KKT tiles");
+    for (int l = 0; l < h->L; ++l) {
+        const int rc = solve_level(h, P, l, true, batch, list, x, se, sb, st);
+        if (rc != ATO_OK) return rc;
     }
+    for (int l = h->L - 1; l >= 0; --l) {
+        const int rc = solve_level(h, P, l, false, batch, list, x, se, sb, st);
+        if (rc != ATO_OK) return rc;
+    }
+    return ATO_OK;
 }
 
 }  // extern "C"

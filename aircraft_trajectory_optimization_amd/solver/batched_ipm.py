@@ -466,7 +466,7 @@ class BatchedInteriorPoint:
             dual_x = gf + self._JTy(Js, y) - zl + zu
             E0, du, pr, co = self._errors(dual_x, g, x, s, y, zl, zu, vl, vu, 0.0)
             pr_uns = (self._resid(g, s) / sg).abs().amax(0)
-            history.append(torch.stack([f / sf, pr, du, mu, E0]))
+            history.append(torch.stack([f / sf, pr, du, mu, E0, n_resto.double()]))
             if stop_check is not None:
                 stp = act & (own > 0) & stop_check(x)
                 status = torch.where(stp, torch.full_like(status, STOPPED), status)
@@ -649,7 +649,8 @@ class BatchedInteriorPoint:
             x = torch.minimum(torch.maximum(x, self.lbx0), self.ubx0)
         fu, _, _, _ = self.ev.eval(x)
         st = status.cpu().numpy()
-        self.history = torch.stack(history).cpu().numpy() if history else np.zeros((0, 5, B))
+        # [lockstep iteration][f, inf_pr, inf_du, mu, E0, restorations so far][instance]
+        self.history = torch.stack(history).cpu().numpy() if history else np.zeros((0, 6, B))
         self.stats['restorations'] = self.stats.get('restorations', 0) + int(n_resto.sum())
         return BatchedIPMResult(x=x, f=fu, lam_g=y * sg / sf, lam_x=(zu - zl) / sf,
                                 status=[STATUS_NAMES[int(v)] for v in st], iters=iters.cpu().numpy(),

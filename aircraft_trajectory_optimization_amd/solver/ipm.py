@@ -270,7 +270,8 @@ class InteriorPointSolver:
             E0, du, pr, co = errors(gf, J, g, x, s, y, zl, zu, vl, vu, 0.0)
             # unscaled checks (IPOPT): dual on f-units, primal on g-units
             pr_uns = np.abs(theta_of(g, s)[1] / self.sg).max(initial=0)
-            history.append({'iter': it, 'f': f / self.sf, 'inf_pr': pr, 'inf_du': du, 'mu': mu, 'E0': E0})
+            history.append({'iter': it, 'f': f / self.sf, 'inf_pr': pr, 'inf_du': du, 'mu': mu, 'E0': E0,
+                            'resto': n_resto})
             if o.verbose:
                 print(f'{"r" if in_resto else " "}{it:4d} f={f / self.sf: .10e} pr={pr:.2e} du={du:.2e} mu={mu:.1e}')
             if stop_check is not None and it > 0 and stop_check(x):

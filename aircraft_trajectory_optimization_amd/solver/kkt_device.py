@@ -24,23 +24,31 @@ class AtoKKTPlanDesc(ctypes.Structure):
     _fields_ = [
         ('n', ctypes.c_int32),
         ('m', ctypes.c_int32),
-        ('n_stages', ctypes.c_int32),
-        ('tiles', ctypes.c_int32),
-        ('stage_ptr', _i32p),
+        ('n_fronts', ctypes.c_int32),
+        ('n_levels', ctypes.c_int32),
+        ('level_ptr', _i32p),
+        ('level_tiles', _i32p),
+        ('pos_ptr', _i32p),
         ('n_own', _i32p),
         ('pos_index', _i32p),
-        ('carry_dst', _i32p),
+        ('parent_pos', _i32p),
+        ('child_ptr', _i32p),
+        ('child_list', _i32p),
         ('ent_ptr', _i32p),
         ('ent_pos', _i32p),
         ('ent_src', _i32p),
         ('l_off', _i64p),
         ('l_size', ctypes.c_int64),
         ('piv_off', _i32p),
+        ('cb_off', _i64p),
+        ('cb_size', ctypes.c_int64),
+        ('sc_off', _i32p),
+        ('sc_size', ctypes.c_int32),
     ]
 
 
 class DeviceKKT:
-    ''' staged Bunch-Kaufman LDL^T of the KKT matrix for a batch of instances on one device '''
+    ''' multifrontal Bunch-Kaufman LDL^T of the KKT matrix for a batch of instances on one device '''
 
     def __init__(self, plan: KKTPlan, max_batch: int, device: Optional[torch.device] = None):
         self.lib = native.load()
@@ -54,17 +62,25 @@ class DeviceKKT:
             return a.ctypes.data_as(pt)
 
         d = AtoKKTPlanDesc()
-        d.n, d.m, d.n_stages, d.tiles = plan.n, plan.m, plan.n_stages, plan.tiles
-        d.stage_ptr = arr(plan.stage_ptr, np.int32, _i32p)
+        d.n, d.m, d.n_fronts, d.n_levels = plan.n, plan.m, plan.n_fronts, plan.n_levels
+        d.level_ptr = arr(plan.level_ptr, np.int32, _i32p)
+        d.level_tiles = arr(plan.level_tiles, np.int32, _i32p)
+        d.pos_ptr = arr(plan.pos_ptr, np.int32, _i32p)
         d.n_own = arr(plan.n_own, np.int32, _i32p)
         d.pos_index = arr(plan.pos_index, np.int32, _i32p)
-        d.carry_dst = arr(plan.carry_dst, np.int32, _i32p)
+        d.parent_pos = arr(plan.parent_pos, np.int32, _i32p)
+        d.child_ptr = arr(plan.child_ptr, np.int32, _i32p)
+        d.child_list = arr(plan.child_list if len(plan.child_list) else np.zeros(1), np.int32, _i32p)
         d.ent_ptr = arr(plan.ent_ptr, np.int32, _i32p)
         d.ent_pos = arr(plan.ent_pos, np.int32, _i32p)
         d.ent_src = arr(plan.ent_src.reshape(-1), np.int32, _i32p)
         d.l_off = arr(plan.l_off, np.int64, _i64p)
         d.l_size = plan.l_size
         d.piv_off = arr(plan.piv_off, np.int32, _i32p)
+        d.cb_off = arr(plan.cb_off, np.int64, _i64p)
+        d.cb_size = plan.cb_size
+        d.sc_off = arr(plan.sc_off, np.int32, _i32p)
+        d.sc_size = plan.sc_size
         self.desc = d
         h = ctypes.c_void_p()
         with torch.cuda.device(self.device):

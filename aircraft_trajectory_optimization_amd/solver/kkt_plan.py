@@ -7,36 +7,48 @@ factorises it with MUMPS / MA97 inside ca.nlpsol, base_raceline.py:752-799)
     K = [ W + diag_x   J^T    ]     n variables, m constraint rows, dim = n + m
         [ J            diag_r ]
 
-is ordered by interval (stage) exactly as solver/kkt_blocks.py does on the host: every variable
-belongs to the interval it lives in, a row touching one stage or two neighbouring stages joins
-the later one, and rows reaching further (loop closure, equal step sizes) form the border.
+is factorised by a MULTIFRONTAL symmetric-indefinite LDL^T over an elimination tree of
+FRONTS. A front owns a set of KKT indices (its eliminated, "own" positions, listed first) and
+has a trailing set (positions that its own rows touch and that are eliminated later, by its
+ancestors). The device assembles the front's dense block from the original entries assigned
+to it plus the contribution blocks of its children (extend-add), eliminates the own positions
+with Bunch-Kaufman pivoting restricted to them, and leaves the Schur complement of the
+trailing block as the front's contribution to its parent. Fronts of one LEVEL are independent
+(their children are all in lower levels), so a level is one launch over (front, instance)
+pairs. The inertia of K is the sum of the inertias of all pivots (Haynsworth) -- exactly what
+IPOPT's inertia correction needs.
 
-For every stage s the device works on an AUGMENTED block of positions
+Orderings of the interval chain (every variable belongs to one interval, the Hessian is block
+diagonal by interval, almost every row touches one interval or two neighbouring ones):
 
-    own(s)            the stage's variables, then its rows          (eligible pivots)
-    coupling(s+1)     rows of stage s+1 with entries on stage-s variables
-    border            all border rows
+  'nd'     nested dissection (default). The separator of boundary j (between intervals j-1
+           and j) holds the LINK rows touching both intervals (continuity) and the ANCHOR
+           variables of interval j they touch (the new interval's first node). The leaves are
+           the interval interiors (all other variables of the interval and the rows touching
+           only it): independent fronts, all eliminated in parallel; the anchors pin nothing
+           inside a leaf, so the collocation defects there determine the later nodes and the
+           leaf blocks stay non-singular. Separators are joined by recursive bisection, the
+           border rows (loop closure, equal step sizes: rows spanning non-neighbouring
+           intervals) form the root. The critical path of one factorisation is one leaf plus
+           log2(N) separators instead of the whole chain.
+  'chain'  the staged elimination of solver/kkt_blocks.py: front s owns interval s's variables
+           and rows (a row touching two intervals joins the later one), its child is front s-1,
+           the border is the root. One front per level.
 
-The own positions are eliminated with Bunch-Kaufman pivoting restricted to own(s); what is left
-in the trailing (coupling + border) block is the Schur complement, which is CARRIED into stage
-s+1 (coupling positions are own positions there, border positions stay border). After the last
-stage a pseudo-stage holds the border alone and is factorised completely. The inertia of K is the
-sum of the inertias of all pivots (Haynsworth), which is what IPOPT's inertia correction needs.
-
-This module builds, once per problem structure, the integer tables the kernels read:
-position -> KKT index, the lower-triangle entry list of every augmented block grouped by
-32-row strip with the source of each value (Hessian entry, Jacobian entry, variable or row
-diagonal), the carry map, and the per-stage storage offsets of the factor.
+This module builds the integer tables the kernels read: KKT index of every front position,
+the lower-triangle entry list of every front grouped by 32-row strip with the source of
+each value (Hessian entry, Jacobian entry, variable or row diagonal), the extend-add map of
+every trailing position into the parent front, and the per-front storage offsets.
 '''
 from dataclasses import dataclass
-from typing import List
+from typing import Dict, List
 
 import numpy as np
 
 SRC_H, SRC_J, SRC_DX, SRC_DR = 0, 1, 2, 3
 SRC_SHIFT = 29
 TILE = 32
-MAX_TILES = 8              # augmented blocks up to 256 positions (kernel register tiles)
+MAX_TILES = 8              # fronts up to 256 positions (kernel register tiles)
 
 
 def src_code(kind: int, idx: int) -> int:
@@ -48,145 +60,269 @@ class KKTPlan:
     n: int                      # variables
     m: int                      # rows
     dim: int                    # n + m
-    n_stages: int               # intervals + 1 border pseudo-stage
-    tiles: int                  # 32-wide tiles of the largest augmented block
-    stage_ptr: np.ndarray       # [S+1] into pos_index
-    n_own: np.ndarray           # [S]
-    pos_index: np.ndarray       # [P] KKT index of every augmented position
-    carry_dst: np.ndarray       # [P] trailing position -> position in the next stage (-1: own)
-    ent_ptr: np.ndarray         # [S * tiles + 1] entries of (stage, strip)
+    ordering: str
+    n_fronts: int
+    n_levels: int
+    level_ptr: np.ndarray       # [L+1] fronts of level l: level_ptr[l] .. level_ptr[l+1]-1
+    level_tiles: np.ndarray     # [L] 32-wide tiles of the largest front of the level
+    pos_ptr: np.ndarray         # [F+1] into pos_index / parent_pos
+    n_own: np.ndarray           # [F]
+    pos_index: np.ndarray       # [P] KKT index of every front position (own first)
+    parent_pos: np.ndarray      # [P] trailing position -> position in the parent front (-1: own)
+    parent: np.ndarray          # [F] parent front (-1: root)
+    child_ptr: np.ndarray       # [F+1] into child_list
+    child_list: np.ndarray      # [C] children of every front, ascending
+    ent_ptr: np.ndarray         # [F * MAX_TILES + 1] entries of (front, strip)
     ent_pos: np.ndarray         # [E] (pa << 16) | pb with pa >= pb
     ent_src: np.ndarray         # [E, 2] source codes (-1: none)
-    l_off: np.ndarray           # [S] offset of the stage's factor columns (doubles, per instance)
+    l_off: np.ndarray           # [F] offset of the front's factor columns (doubles, per instance)
     l_size: int                 # doubles of factor columns per instance
-    piv_off: np.ndarray         # [S] offset of the stage's pivot records (per instance)
-    block_sizes: np.ndarray     # [S] augmented size
+    piv_off: np.ndarray         # [F] offset of the front's pivot records (per instance)
+    cb_off: np.ndarray          # [F] offset of the front's contribution block (tq x tq doubles)
+    cb_size: int
+    sc_off: np.ndarray          # [F] offset of the front's solve contribution (tq doubles)
+    sc_size: int
+    block_sizes: np.ndarray     # [F] own + trailing
 
     @property
     def max_block(self) -> int:
         return int(self.block_sizes.max())
 
+    @property
+    def tiles(self) -> int:
+        return int(self.level_tiles.max())
 
-def row_stages(n, m, var_stage, j_row_ptr, j_col) -> np.ndarray:
-    ''' stage of every row: the later stage of a row touching one or two neighbouring stages,
-    -1 for border rows (same rule as solver/kkt_blocks.BlockKKT) '''
+    def front_positions(self, f: int) -> np.ndarray:
+        return self.pos_index[self.pos_ptr[f]:self.pos_ptr[f + 1]]
+
+    def children(self, f: int) -> np.ndarray:
+        return self.child_list[self.child_ptr[f]:self.child_ptr[f + 1]]
+
+
+def row_span(n, m, var_stage, j_row_ptr, j_col):
+    ''' (lowest, highest) interval touched by every row; empty rows -> (0, 0) '''
     var_stage = np.asarray(var_stage)
-    cnt = np.diff(np.asarray(j_row_ptr))
-    jr = np.repeat(np.arange(m), cnt)
+    jr = np.repeat(np.arange(m), np.diff(np.asarray(j_row_ptr)))
     st = var_stage[np.asarray(j_col)]
     lo = np.full(m, np.iinfo(np.int64).max)
     hi = np.full(m, -1)
     np.minimum.at(lo, jr, st)
     np.maximum.at(hi, jr, st)
+    empty = hi < 0
+    lo[empty], hi[empty] = 0, 0
+    return lo, hi
+
+
+def row_stages(n, m, var_stage, j_row_ptr, j_col) -> np.ndarray:
+    ''' stage of every row in the 'chain' ordering: the later stage of a row touching one or two
+    neighbouring stages, -1 for border rows (same rule as solver/kkt_blocks.BlockKKT) '''
+    lo, hi = row_span(n, m, var_stage, j_row_ptr, j_col)
+    return np.where(hi - lo <= 1, hi, -1)
+
+
+def _fronts_chain(n, var_stage, lo, hi):
+    S = int(var_stage.max()) + 1
     rs = np.where(hi - lo <= 1, hi, -1)
-    rs[hi < 0] = 0
-    return rs
+    own = [np.concatenate([np.nonzero(var_stage == s)[0], n + np.nonzero(rs == s)[0]]) for s in range(S)]
+    children: List[List[int]] = [[s - 1] if s > 0 else [] for s in range(S)]
+    border = n + np.nonzero(rs < 0)[0]
+    own.append(border)
+    children.append([S - 1])
+    return own, children
 
 
-def build_plan(n: int, m: int, var_stage, j_row_ptr, j_col, h_row_ptr, h_col) -> KKTPlan:
+def _fronts_nd(n, var_stage, lo, hi, j_row_ptr, j_col):
+    S = int(var_stage.max()) + 1
+    m = len(lo)
+    link = hi - lo == 1
+    interior = hi == lo
+    # anchors of boundary j: the variables of interval j touched by its link rows
+    anchor = np.zeros(n, bool)
+    jr = np.repeat(np.arange(m), np.diff(np.asarray(j_row_ptr)))
+    jc = np.asarray(j_col)
+    sel = link[jr] & (var_stage[jc] == hi[jr])
+    anchor[jc[sel]] = True
+    own: List[np.ndarray] = []
+    children: List[List[int]] = []
+    for s in range(S):                          # leaves 0 .. S-1
+        own.append(np.concatenate([np.nonzero((var_stage == s) & ~anchor)[0],
+                                   n + np.nonzero(interior & (lo == s))[0]]))
+        children.append([])
+
+    def sep(j):
+        return np.concatenate([np.nonzero((var_stage == j) & anchor)[0], n + np.nonzero(link & (hi == j))[0]])
+
+    def build(a, b):                            # subtree over intervals a..b (boundaries a+1..b)
+        if a == b:
+            return a
+        j = (a + b + 1) // 2
+        left, right = build(a, j - 1), build(j, b)
+        own.append(sep(j))
+        children.append([left, right])
+        return len(own) - 1
+
+    top = build(0, S - 1)
+    border = n + np.nonzero(hi - lo > 1)[0]
+    if len(border):
+        own.append(border)
+        children.append([top])
+    return own, children
+
+
+def build_plan(n: int, m: int, var_stage, j_row_ptr, j_col, h_row_ptr, h_col, ordering: str = 'nd') -> KKTPlan:
     var_stage = np.asarray(var_stage, np.int64)
     j_row_ptr = np.asarray(j_row_ptr, np.int64)
     j_col = np.asarray(j_col, np.int64)
     h_row_ptr = np.asarray(h_row_ptr, np.int64)
     h_col = np.asarray(h_col, np.int64)
-    S = int(var_stage.max()) + 1
-    rs = row_stages(n, m, var_stage, j_row_ptr, j_col)
     jr = np.repeat(np.arange(m), np.diff(j_row_ptr))
     hr = np.repeat(np.arange(n), np.diff(h_row_ptr))
     if len(hr) and np.any(var_stage[hr] != var_stage[h_col]):
         raise ValueError('Hessian couples different stages; the staged KKT does not apply')
+    lo, hi = row_span(n, m, var_stage, j_row_ptr, j_col)
+    if ordering == 'nd':
+        own, children = _fronts_nd(n, var_stage, lo, hi, j_row_ptr, j_col)
+    elif ordering == 'chain':
+        own, children = _fronts_chain(n, var_stage, lo, hi)
+    else:
+        raise ValueError(f'unknown KKT ordering {ordering!r}')
+    F0 = len(own)
+    cover = np.concatenate(own)
+    if not np.array_equal(np.sort(cover), np.arange(n + m)):
+        raise AssertionError('KKT fronts do not partition the KKT indices')
 
-    border = n + np.nonzero(rs < 0)[0]
-    own: List[np.ndarray] = []
-    for s in range(S):
-        own.append(np.concatenate([np.nonzero(var_stage == s)[0], n + np.nonzero(rs == s)[0]]))
-    # coupling(s+1): rows of stage s+1 with entries on stage-s variables
-    cpl_rows = (rs[jr] >= 1) & (var_stage[j_col] == rs[jr] - 1)
-    coupling = [np.zeros(0, np.int64) for _ in range(S + 1)]
-    for s in range(1, S):
-        coupling[s] = n + np.unique(jr[cpl_rows & (rs[jr] == s)])
+    # ---- levels (children first), fronts renumbered level by level
+    level = np.zeros(F0, np.int64)
+    for f in range(F0):                         # children always precede parents in creation order
+        if children[f]:
+            level[f] = 1 + max(level[c] for c in children[f])
+    order = np.lexsort((np.arange(F0), level))
+    new_id = np.empty(F0, np.int64)
+    new_id[order] = np.arange(F0)
+    own = [own[f] for f in order]
+    children = [sorted(int(new_id[c]) for c in children[f]) for f in order]
+    level = level[order]
+    F = F0
+    parent = np.full(F, -1, np.int64)
+    for f in range(F):
+        for c in children[f]:
+            parent[c] = f
 
-    blocks = []                 # augmented position lists (KKT indices)
-    n_own = []
-    for s in range(S):
-        blocks.append(np.concatenate([own[s], coupling[s + 1] if s + 1 < S else np.zeros(0, np.int64), border]))
-        n_own.append(len(own[s]))
-    blocks.append(border.copy())
-    n_own.append(len(border))
-    NS = S + 1
-    sizes = np.array([len(b) for b in blocks])
-    tiles = int(max(1, -(-sizes.max() // TILE)))
-    if tiles > MAX_TILES:
-        raise ValueError(f'augmented KKT block of {sizes.max()} positions exceeds the device limit '
-                         f'{MAX_TILES * TILE}')
-    pos_of = []                 # KKT index -> position, per stage
-    for b in blocks:
-        d = np.full(n + m, -1, np.int64)
-        d[b] = np.arange(len(b))
-        pos_of.append(d)
+    # ---- adjacency of the KKT graph (structural nonzeros, both triangles)
+    dim = n + m
+    adj_r = np.concatenate([hr, h_col, jr + n, j_col])
+    adj_c = np.concatenate([h_col, hr, j_col, jr + n])
+    keep = adj_r != adj_c
+    adj_r, adj_c = adj_r[keep], adj_c[keep]
+    srt = np.argsort(adj_r, kind='stable')
+    adj_r, adj_c = adj_r[srt], adj_c[srt]
+    adj_ptr = np.searchsorted(adj_r, np.arange(dim + 1))
 
-    # ---- entries: (stage, pa, pb, src1, src2)
-    ent = {s: {} for s in range(NS)}
+    # ---- trailing sets by symbolic elimination in front order
+    owner = np.empty(dim, np.int64)
+    for f in range(F):
+        owner[own[f]] = f
+    trailing: List[np.ndarray] = []
+    eliminated = np.zeros(dim, bool)
+    for f in range(F):
+        o = own[f]
+        isown = np.zeros(dim, bool)
+        isown[o] = True
+        # neighbours eliminated earlier were assembled into a descendant and reach this front
+        # through the contribution blocks; the children's trailing positions must all be live
+        nb = np.concatenate([adj_c[adj_ptr[i]:adj_ptr[i + 1]] for i in o] + [np.zeros(0, np.int64)])
+        nb = nb[~eliminated[nb]]
+        ct = np.concatenate([trailing[c] for c in children[f]] + [np.zeros(0, np.int64)])
+        if eliminated[ct].any():
+            raise AssertionError(f'front {f}: a child hands over positions eliminated outside its ancestry')
+        cand = np.unique(np.concatenate([nb, ct]))
+        cand = cand[~isown[cand]]
+        trailing.append(cand)
+        eliminated[o] = True
+    if any(len(trailing[f]) for f in range(len(own)) if parent[f] < 0):
+        raise AssertionError('a root front has trailing positions')
+    # every trailing position must be eliminated by an ancestor, and sit in the parent's front
+    pos_of: List[Dict[int, int]] = []
+    for f in range(F):
+        pos_of.append({int(i): q for q, i in enumerate(np.concatenate([own[f], trailing[f]]))})
+    for f in range(F):
+        if len(trailing[f]):
+            p = int(parent[f])
+            if p < 0 or any(int(i) not in pos_of[p] for i in trailing[f]):
+                raise AssertionError(f'front {f}: trailing positions outside the parent front')
 
-    def add(s, i, j, code):
-        pa, pb = pos_of[s][i], pos_of[s][j]
-        assert pa >= 0 and pb >= 0, (s, i, j)
+    sizes = np.array([len(own[f]) + len(trailing[f]) for f in range(F)])
+    if sizes.max(initial=0) > MAX_TILES * TILE:
+        raise ValueError(f'KKT front of {sizes.max()} positions exceeds the device limit {MAX_TILES * TILE}')
+    n_levels = int(level.max()) + 1
+    level_ptr = np.searchsorted(level, np.arange(n_levels + 1))
+    level_tiles = np.array([max(1, -(-int(sizes[level_ptr[l]:level_ptr[l + 1]].max()) // TILE))
+                            for l in range(n_levels)])
+
+    # ---- entries: each original entry (i, j) belongs to the front eliminating the earlier of i, j
+    rank = np.empty(dim, np.int64)               # elimination rank (front order, then own order)
+    r0 = 0
+    for f in range(F):
+        rank[own[f]] = r0 + np.arange(len(own[f]))
+        r0 += len(own[f])
+    ent: List[Dict] = [dict() for _ in range(F)]
+
+    def add(i, j, code):
+        f = int(owner[i] if rank[i] <= rank[j] else owner[j])
+        pa, pb = pos_of[f][int(i)], pos_of[f][int(j)]
         if pa < pb:
             pa, pb = pb, pa
-        key = (int(pa), int(pb))
-        lst = ent[s].setdefault(key, [])
-        lst.append(code)
+        ent[f].setdefault((pa, pb), []).append(code)
 
-    for e in range(len(h_col)):             # Hessian (lower, same stage)
-        r, c = int(hr[e]), int(h_col[e])
-        add(int(var_stage[r]), r, c, src_code(SRC_H, e))
-    for j in range(n):                       # variable diagonal
-        add(int(var_stage[j]), j, j, src_code(SRC_DX, j))
-    for e in range(len(j_col)):              # Jacobian (row i, variable j): stage of the variable
-        i, j = int(jr[e]), int(j_col[e])
-        add(int(var_stage[j]), n + i, j, src_code(SRC_J, e))
-    for i in range(m):                       # row diagonal
-        s = int(rs[i]) if rs[i] >= 0 else S
-        add(s, n + i, n + i, src_code(SRC_DR, i))
+    for e in range(len(h_col)):                 # Hessian (lower)
+        add(int(hr[e]), int(h_col[e]), src_code(SRC_H, e))
+    for j in range(n):                          # variable diagonal
+        add(j, j, src_code(SRC_DX, j))
+    for e in range(len(j_col)):                 # Jacobian (row i, variable j)
+        add(n + int(jr[e]), int(j_col[e]), src_code(SRC_J, e))
+    for i in range(m):                          # row diagonal
+        add(n + i, n + i, src_code(SRC_DR, i))
 
     ent_ptr = [0]
     ent_pos, ent_src = [], []
-    for s in range(NS):
-        keys = sorted(ent[s].keys(), key=lambda k: (k[0] // TILE, k[0], k[1]))
-        strips = [[] for _ in range(tiles)]
-        for k in keys:
-            srcs = ent[s][k]
+    for f in range(F):
+        strips = [[] for _ in range(MAX_TILES)]
+        for k in sorted(ent[f].keys(), key=lambda k: (k[0] // TILE, k[0], k[1])):
+            srcs = ent[f][k]
             if len(srcs) > 2:
-                raise ValueError(f'KKT entry {k} of stage {s} has {len(srcs)} sources')
+                raise ValueError(f'KKT entry {k} of front {f} has {len(srcs)} sources')
             strips[k[0] // TILE].append((k, srcs))
-        for I in range(tiles):
+        for I in range(MAX_TILES):
             for (pa, pb), srcs in strips[I]:
                 ent_pos.append((pa << 16) | pb)
                 ent_src.append([srcs[0], srcs[1] if len(srcs) > 1 else -1])
             ent_ptr.append(len(ent_pos))
 
-    # ---- carry map: trailing position of stage s -> position in stage s+1
-    stage_ptr = np.concatenate([[0], np.cumsum(sizes)])
-    carry_dst = np.full(int(stage_ptr[-1]), -1, np.int64)
-    for s in range(NS - 1):
-        b = blocks[s]
-        for q in range(n_own[s], len(b)):
-            dst = pos_of[s + 1][b[q]]
-            assert dst >= 0
-            carry_dst[stage_ptr[s] + q] = dst
+    # ---- positions, extend-add map, children
+    pos_index = np.concatenate([np.concatenate([own[f], trailing[f]]) for f in range(F)])
+    pos_ptr = np.concatenate([[0], np.cumsum(sizes)])
+    parent_pos = np.full(len(pos_index), -1, np.int64)
+    for f in range(F):
+        p = int(parent[f])
+        for q, i in enumerate(trailing[f]):
+            parent_pos[pos_ptr[f] + len(own[f]) + q] = pos_of[p][int(i)]
+    child_ptr = np.concatenate([[0], np.cumsum([len(c) for c in children])])
+    child_list = np.asarray([c for cs in children for c in cs], np.int64)
 
-    # ---- factor storage: compact columns of live positions after each step
-    l_off, piv_off = [], []
-    lo = po = 0
-    for s in range(NS):
-        A, o = int(sizes[s]), int(n_own[s])
-        l_off.append(lo)
-        piv_off.append(po)
-        lo += o * A - o * (o + 1) // 2
-        po += o
-    return KKTPlan(n=n, m=m, dim=n + m, n_stages=NS, tiles=tiles,
-                   stage_ptr=stage_ptr.astype(np.int32), n_own=np.asarray(n_own, np.int32),
-                   pos_index=np.concatenate(blocks).astype(np.int32), carry_dst=carry_dst.astype(np.int32),
-                   ent_ptr=np.asarray(ent_ptr, np.int32), ent_pos=np.asarray(ent_pos, np.int32),
-                   ent_src=np.asarray(ent_src, np.int32).reshape(-1, 2), l_off=np.asarray(l_off, np.int64),
-                   l_size=int(lo), piv_off=np.asarray(piv_off, np.int32), block_sizes=sizes.astype(np.int32))
+    # ---- per-instance storage: compact factor columns, pivot records, contribution blocks
+    n_own = np.array([len(o) for o in own])
+    tq = sizes - n_own
+    l_sz = n_own * sizes - n_own * (n_own + 1) // 2
+    l_off = np.concatenate([[0], np.cumsum(l_sz)])
+    piv_off = np.concatenate([[0], np.cumsum(n_own)])
+    cb_off = np.concatenate([[0], np.cumsum(tq * tq)])
+    sc_off = np.concatenate([[0], np.cumsum(tq)])
+    i32 = lambda a: np.asarray(a, np.int32)  # noqa: E731
+    return KKTPlan(n=n, m=m, dim=dim, ordering=ordering, n_fronts=F, n_levels=n_levels,
+                   level_ptr=i32(level_ptr), level_tiles=i32(level_tiles), pos_ptr=i32(pos_ptr), n_own=i32(n_own),
+                   pos_index=i32(pos_index), parent_pos=i32(parent_pos), parent=i32(parent),
+                   child_ptr=i32(child_ptr), child_list=i32(child_list),
+                   ent_ptr=i32(ent_ptr), ent_pos=i32(ent_pos), ent_src=i32(ent_src).reshape(-1, 2),
+                   l_off=np.asarray(l_off[:-1], np.int64), l_size=int(l_off[-1]),
+                   piv_off=i32(piv_off[:-1]), cb_off=np.asarray(cb_off[:-1], np.int64), cb_size=int(cb_off[-1]),
+                   sc_off=i32(sc_off[:-1]), sc_size=int(sc_off[-1]), block_sizes=i32(sizes))

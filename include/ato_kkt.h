@@ -11,16 +11,18 @@
  *     K = [ W + diag_x   J^T    ]      W: Lagrangian Hessian (lower CSR, ato_hess_sparsity)
  *         [ J            diag_r ]      J: constraint Jacobian  (CSR, ato_sparsity)
  *
- * is factorised for a BATCH of instances at once, one workgroup per instance, with a staged
- * symmetric-indefinite LDL^T: the KKT indices are ordered by interval (stage), each stage's
- * augmented block (its own variables and rows, the next stage's coupling rows and the border
- * rows) is held in registers, its own positions are eliminated with Bunch-Kaufman pivoting,
- * and the trailing Schur complement is carried to the next stage. The inertia (n+, n-, n0)
- * of K is returned per instance -- what IPOPT's inertia correction needs.
+ * is factorised for a BATCH of instances at once by a multifrontal symmetric-indefinite
+ * LDL^T over an elimination tree of fronts (solver/kkt_plan.py: nested dissection of the
+ * interval chain). A front's dense block -- its own positions and the trailing positions
+ * its ancestors eliminate -- is assembled from the original entries assigned to it and the
+ * contribution blocks of its children, held in registers, and its own positions are
+ * eliminated with Bunch-Kaufman pivoting restricted to them; the trailing Schur complement
+ * is its contribution to the parent. The fronts of one level are independent: one launch
+ * per level over (front, instance) workgroups. The inertia (n+, n-, n0) of K is returned
+ * per instance -- what IPOPT's inertia correction needs.
  *
- * The structure tables come from solver/kkt_plan.py (host analysis of the two sparsity
- * patterns). All value pointers are DEVICE pointers; element e of instance b of every value
- * array (H, J, diag_x, diag_r, x) is at [e * stride_elem + b * stride_inst], so both the
+ * All value pointers are DEVICE pointers; element e of instance b of every value array
+ * (H, J, diag_x, diag_r, x) is at [e * stride_elem + b * stride_inst], so both the
  * interleaved ([e][B]: stride_elem = B, stride_inst = 1) and the instance-major layout work.
  */
 #ifndef ATO_KKT_H
@@ -33,20 +35,28 @@ extern "C" {
 #endif
 
 typedef struct ato_kkt_plan_desc {
-    int32_t n, m;               /* variables, constraint rows (KKT dim = n + m)              */
-    int32_t n_stages;           /* intervals + 1 border pseudo-stage                         */
-    int32_t tiles;              /* 32-wide register tiles of the largest block (<= 8)         */
-    const int32_t* stage_ptr;   /* [n_stages + 1] offsets into pos_index / carry_dst          */
-    const int32_t* n_own;       /* [n_stages] eligible (own) positions of every stage         */
-    const int32_t* pos_index;   /* [P] KKT index of every augmented position                  */
-    const int32_t* carry_dst;   /* [P] trailing position -> position in the next stage, or -1 */
-    const int32_t* ent_ptr;     /* [n_stages * tiles + 1] entries of (stage, 32-row strip)    */
-    const int32_t* ent_pos;     /* [E] (pa << 16) | pb, pa >= pb                               */
-    const int32_t* ent_src;     /* [E][2] (kind << 29) | index; kind 0 H, 1 J, 2 diag_x,       *
-                                 * 3 diag_r; -1 = none. The value is the sum of both sources. */
-    const int64_t* l_off;       /* [n_stages] factor-column offset of every stage (doubles)   */
-    int64_t l_size;             /* factor-column doubles per instance                        */
-    const int32_t* piv_off;     /* [n_stages] pivot-record offset of every stage              */
+    int32_t n, m;               /* variables, constraint rows (KKT dim = n + m)                 */
+    int32_t n_fronts;           /* F                                                            */
+    int32_t n_levels;           /* L                                                            */
+    const int32_t* level_ptr;   /* [L + 1] fronts of level l: level_ptr[l] .. level_ptr[l+1]-1   */
+    const int32_t* level_tiles; /* [L] 32-wide register tiles of the level's largest front (<=8) */
+    const int32_t* pos_ptr;     /* [F + 1] offsets into pos_index / parent_pos                   */
+    const int32_t* n_own;       /* [F] eliminated (own) positions of every front, listed first  */
+    const int32_t* pos_index;   /* [P] KKT index of every front position                        */
+    const int32_t* parent_pos;  /* [P] trailing position -> position in the parent, -1 for own   */
+    const int32_t* child_ptr;   /* [F + 1] offsets into child_list                               */
+    const int32_t* child_list;  /* [C] children of every front (all in lower levels)             */
+    const int32_t* ent_ptr;     /* [F * 8 + 1] entries of (front, 32-row strip)                   */
+    const int32_t* ent_pos;     /* [E] (pa << 16) | pb, pa >= pb                                  */
+    const int32_t* ent_src;     /* [E][2] (kind << 29) | index; kind 0 H, 1 J, 2 diag_x,          *
+                                 * 3 diag_r; -1 = none. The value is the sum of both sources.    */
+    const int64_t* l_off;       /* [F] factor-column offset of every front (doubles)             */
+    int64_t l_size;             /* factor-column doubles per instance                           */
+    const int32_t* piv_off;     /* [F] pivot-record offset of every front                        */
+    const int64_t* cb_off;      /* [F] contribution-block offset (tq * tq doubles per front)     */
+    int64_t cb_size;            /* contribution-block doubles per instance                      */
+    const int32_t* sc_off;      /* [F] solve-contribution offset (tq doubles per front)          */
+    int32_t sc_size;            /* solve-contribution doubles per instance                      */
 } ato_kkt_plan_desc;
 
 typedef struct ato_kkt ato_kkt;
@@ -54,7 +64,8 @@ typedef struct ato_kkt ato_kkt;
 int ato_kkt_create(const ato_kkt_plan_desc* desc, ato_kkt** out);
 int ato_kkt_destroy(ato_kkt* kkt);
 
-/* Device storage of the factors of instances 0 .. max_batch-1 (about l_size doubles each). */
+/* Device storage of the factors of instances 0 .. max_batch-1 (about l_size + cb_size doubles
+ * each). */
 int ato_kkt_reserve(ato_kkt* kkt, int32_t max_batch);
 
 /* Factorise K for `batch` instances: instance list[i] (device int32 array; NULL = 0..batch-1)

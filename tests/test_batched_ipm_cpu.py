@@ -39,3 +39,27 @@ def test_batched_matches_single_instance(cfg):
         assert res.iters[b] == ref.iters
         assert np.abs(x[:, b] - ref.x).max() <= 1e-6 * max(1.0, np.abs(ref.x).max())
         assert abs(x[:spec.N, b].sum() - ref.x[:spec.N].sum()) <= 1e-8
+
+
+@pytest.mark.parametrize('cfg', [dict(track='race', model='point', use_quat=False, N=8, K=3),
+                                 dict(track='fig8', model='point', use_quat=False, frame='global', N=7, K=2)],
+                         ids=['point-param', 'point-global'])
+def test_nested_dissection_order_follows_single_instance(cfg):
+    ''' the device's nested-dissection elimination order (tests/kkt_emulation.py on the 'nd' plan)
+    on real iterates: same statuses and iteration counts (+-5) as the host block LDL^T of the
+    single-instance solver, solutions to rounding-level agreement '''
+    from tests.batched_backends import EmulatedPlanKKT
+    spec = product_spec(**cfg)
+    B = 2
+    W = _instances(spec, B)
+    ev = HostBatchEvaluator(spec, B)
+    opts = IPMOptions(max_iter=300)
+    res = BatchedInteriorPoint(ev, EmulatedPlanKKT(ev, 'nd'), spec.lbw, spec.ubw, opts).solve(W)
+    x = res.x.numpy()
+    for b in range(B):
+        hev = HostEvaluator(spec)
+        ref = InteriorPointSolver(hev, spec.lbw, spec.ubw, hev.lbg, hev.ubg, opts).solve(W[b])
+        assert res.status[b] == ref.status
+        assert abs(int(res.iters[b]) - ref.iters) <= 5
+        assert np.abs(x[:, b] - ref.x).max() <= 1e-6 * max(1.0, np.abs(ref.x).max())
+

@@ -26,14 +26,15 @@ def _dev(arrs):
     return torch.as_tensor(np.stack(arrs, axis=1), dtype=torch.float64, device='cuda').contiguous()
 
 
+@pytest.mark.parametrize('ordering', ['nd', 'chain'])
 @pytest.mark.parametrize('cfg', CASES, ids=IDS)
-def test_device_kkt_matches_dense(cfg):
+def test_device_kkt_matches_dense(cfg, ordering):
     from aircraft_trajectory_optimization_amd.solver.kkt_device import DeviceKKT
     spec = product_spec(**cfg)
     B = 3
     vals = [random_kkt_values(spec, seed) for seed in range(B)]
     ev = vals[0][0]
-    plan = build_plan(ev.nw, ev.ng, var_stages(spec), ev.j_row_ptr, ev.j_col, ev.h_row_ptr, ev.h_col)
+    plan = build_plan(ev.nw, ev.ng, var_stages(spec), ev.j_row_ptr, ev.j_col, ev.h_row_ptr, ev.h_col, ordering)
     kkt = DeviceKKT(plan, B)
     H = _dev([v[1] for v in vals])
     J = _dev([v[2] for v in vals])
@@ -50,7 +51,9 @@ def test_device_kkt_matches_dense(cfg):
         assert tuple(inertia[b]) == (int((eig > 0).sum()), int((eig < 0).sum()), 0)
         res = np.abs(K @ x[:, b] - rhs[:, b]).max()
         assert res <= 1e-8 * max(1.0, np.abs(K).max()), res
-        xe = Factor(plan, Hb, Jb, dxb, drb).solve(rhs[:, b])
+        fe = Factor(plan, Hb, Jb, dxb, drb)
+        assert fe.inertia == tuple(inertia[b])
+        xe = fe.solve(rhs[:, b])
         assert np.abs(x[:, b] - xe).max() <= 1e-8 * max(1.0, np.abs(xe).max())
 
 

@@ -28,16 +28,20 @@ def random_kkt_values(spec, seed):
     return ev, H, jv, dx, dr
 
 
+@pytest.mark.parametrize('ordering', ['nd', 'chain'])
 @pytest.mark.parametrize('cfg', CASES, ids=IDS)
-def test_plan_emulation_matches_dense(cfg):
+def test_plan_emulation_matches_dense(cfg, ordering):
     spec = product_spec(**cfg)
     ev, H, jv, dx, dr = random_kkt_values(spec, 0)
-    plan = build_plan(ev.nw, ev.ng, var_stages(spec), ev.j_row_ptr, ev.j_col, ev.h_row_ptr, ev.h_col)
+    plan = build_plan(ev.nw, ev.ng, var_stages(spec), ev.j_row_ptr, ev.j_col, ev.h_row_ptr, ev.h_col, ordering)
     assert plan.tiles <= MAX_TILES and plan.max_block <= plan.tiles * TILE
-    # every KKT index is own in exactly one stage
-    own = np.concatenate([plan.pos_index[plan.stage_ptr[s]:plan.stage_ptr[s] + plan.n_own[s]]
-                          for s in range(plan.n_stages)])
+    # every KKT index is own in exactly one front; children sit in lower levels than their parent
+    own = np.concatenate([plan.front_positions(f)[:plan.n_own[f]] for f in range(plan.n_fronts)])
     assert np.array_equal(np.sort(own), np.arange(plan.dim))
+    lvl = np.searchsorted(plan.level_ptr, np.arange(plan.n_fronts), side='right') - 1
+    for f in range(plan.n_fronts):
+        assert all(lvl[c] < lvl[f] for c in plan.children(f))
+        assert plan.block_sizes[f] <= 32 * plan.level_tiles[lvl[f]]
     K = dense_kkt(plan, H, jv, dx, dr, ev.h_row_ptr, ev.h_col, ev.j_row_ptr, ev.j_col)
     f = Factor(plan, H, jv, dx, dr)
     rhs = np.random.default_rng(1).standard_normal(plan.dim)
@@ -51,6 +55,10 @@ def test_plan_racetrack_full_size_fits_device_tiles():
     spec = product_spec(track='race', N=50, K=4)
     ev = HostEvaluator(spec)
     plan = build_plan(ev.nw, ev.ng, var_stages(spec), ev.j_row_ptr, ev.j_col, ev.h_row_ptr, ev.h_col)
-    assert plan.n_stages == 51 and plan.tiles == 8
+    # nested dissection: 50 interval leaves, 49 separators, the border; depth 1 + ceil(log2 50) + 1
+    assert plan.n_fronts == 100 and plan.n_levels == 8
+    assert plan.level_ptr[1] == 50 and plan.level_tiles[0] == 7 and plan.level_tiles[1:].max() <= 4
     assert plan.max_block <= 256
-    assert (np.diff(plan.ent_ptr.reshape(-1)[::plan.tiles]) <= 4096).all()
+    assert (np.diff(plan.ent_ptr[::8]) <= 4096).all()
+    chain = build_plan(ev.nw, ev.ng, var_stages(spec), ev.j_row_ptr, ev.j_col, ev.h_row_ptr, ev.h_col, 'chain')
+    assert chain.n_fronts == 51 and chain.tiles == 8

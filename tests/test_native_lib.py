@@ -46,9 +46,18 @@ def test_missing_library_fails_loudly(tmp_path):
         native.load(str(tmp_path / 'nope.so'))
 
 
-def test_kkt_plan_desc_layout():
+def test_kkt_plan_desc_layout(tmp_path):
+    ''' the ctypes mirror of ato_kkt_plan_desc against the C compiler's layout of the header '''
+    import subprocess
     from aircraft_trajectory_optimization_amd.solver.kkt_device import AtoKKTPlanDesc
-    # 4 int32, 8 pointers, int64 l_size between them (header field order)
-    assert AtoKKTPlanDesc.stage_ptr.offset == 16
-    assert AtoKKTPlanDesc.l_size.offset == 16 + 8 * 8
-    assert ctypes.sizeof(AtoKKTPlanDesc) == 16 + 8 * 8 + 8 + 8
+    names = [f[0] for f in AtoKKTPlanDesc._fields_]
+    inc = os.path.dirname(HEADERS[0])
+    src = tmp_path / 'layout.c'
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "ato_kkt.h"\nint main(void) {\n' +
+                   ''.join(f'    printf("%zu\\n", offsetof(ato_kkt_plan_desc, {n}));\n' for n in names) +
+                   '    printf("%zu\\n", sizeof(ato_kkt_plan_desc));\n    return 0;\n}\n')
+    exe = tmp_path / 'layout'
+    subprocess.run(['gcc', '-I', inc, str(src), '-o', str(exe)], check=True)
+    out = [int(v) for v in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    assert out[:-1] == [getattr(AtoKKTPlanDesc, n).offset for n in names]
+    assert out[-1] == ctypes.sizeof(AtoKKTPlanDesc)

@@ -28,6 +28,7 @@ def main():
     ap.add_argument('--track', default='race')
     ap.add_argument('--frame', default='parametric')
     ap.add_argument('--rk4', action='store_true')
+    ap.add_argument('--ordering', default='nd', choices=['nd', 'chain'])
     a = ap.parse_args()
     from aircraft_trajectory_optimization_amd.raceline.batched import BatchedNLP
     from aircraft_trajectory_optimization_amd.raceline.evaluator import variable_stages
@@ -43,7 +44,7 @@ def main():
     bn.evaluate()
     hrp, hcol, _ = bn.problem.hess_sparsity()
     t0 = time.perf_counter()
-    plan = build_plan(bn.sizes[0], bn.sizes[1], variable_stages(spec), bn.row_ptr, bn.col, hrp, hcol)
+    plan = build_plan(bn.sizes[0], bn.sizes[1], variable_stages(spec), bn.row_ptr, bn.col, hrp, hcol, a.ordering)
     t_plan = time.perf_counter() - t0
     g = torch.Generator(device='cuda').manual_seed(0)
     lam = torch.randn((bn.sizes[1], B), dtype=torch.float64, device='cuda', generator=g)
@@ -70,7 +71,7 @@ def main():
         tf.append(ev[0].elapsed_time(ev[1]))
         ts.append(ev[1].elapsed_time(ev[2]))
     inertia = kkt.inertia.cpu().numpy()
-    out = {'batch': B, 'N': a.N, 'K': a.K, 'dim': plan.dim, 'stages': plan.n_stages, 'max_block': plan.max_block,
+    out = {'ordering': a.ordering, 'batch': B, 'N': a.N, 'K': a.K, 'dim': plan.dim, 'fronts': plan.n_fronts, 'levels': plan.n_levels, 'max_block': plan.max_block,
            'tiles': plan.tiles, 'plan_s': t_plan, 'factor_ms': float(np.median(tf)), 'solve_ms': float(np.median(ts)),
            'factor_us_per_instance': float(np.median(tf)) * 1e3 / B,
            'inertia_ok': int(((inertia[:, 0] == plan.n) & (inertia[:, 1] == plan.m)).sum()),

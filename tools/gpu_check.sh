@@ -31,7 +31,7 @@ run() {  # run <name> <seconds> <cmd...>
 
 for s in $STEPS; do
     case $s in
-        tests) run pytest_gpu 600 python -m pytest tests -m gpu -q -x -p no:cacheprovider ;;
+        tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider ;;
         smoke) run smoke 300 python -c 'import __graft_entry__ as g; g.smoke()' ;;
         bench) run bench 900 python bench.py --steps 50 --warmup 10 ;;
         bench32) run bench_f32 300 python bench.py --steps 50 --warmup 10 --dtype f32 --no-cpu-baseline --no-solve ;;
@@ -50,7 +50,10 @@ for s in $STEPS; do
                    python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-solve ;;
         kkt)   run kkt_b512 200 python tools/bench_kkt.py --batch 512 --out "$OUT/kkt_b512.json"
                run kkt_b64 200 python tools/bench_kkt.py --batch 64 --out "$OUT/kkt_b64.json"
-               run kkt_b1 200 python tools/bench_kkt.py --batch 1 --out "$OUT/kkt_b1.json" ;;
+               run kkt_b1 200 python tools/bench_kkt.py --batch 1 --out "$OUT/kkt_b1.json"
+               run kkt_chain_b512 200 python tools/bench_kkt.py --batch 512 --ordering chain --out "$OUT/kkt_chain_b512.json"
+               run kkt_chain_b1 200 python tools/bench_kkt.py --batch 1 --ordering chain --out "$OUT/kkt_chain_b1.json" ;;
+        kkttests) run pytest_kkt 300 python -u -m pytest tests/test_gpu_kkt.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider ;;
         solve) run solve_b512 600 python tools/solve_batched.py --batch 512 --max-iter 200 --no-host --out "$OUT/solve_b512.json" ;;
         solveprof) run solveprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/solveprof" -o run -- \
                    python tools/solve_batched.py --batch 512 --max-iter 60 --no-host --out "$OUT/solveprof.json" ;;
