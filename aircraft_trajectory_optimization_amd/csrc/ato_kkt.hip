@@ -42,6 +42,7 @@ struct ato_kkt {
     int32_t *d_pos_ptr = nullptr, *d_n_own = nullptr, *d_pos_index = nullptr, *d_parent_pos = nullptr;
     int32_t *d_child_ptr = nullptr, *d_child_list = nullptr, *d_ent_ptr = nullptr, *d_ent_pos = nullptr;
     int32_t *d_ent_src = nullptr, *d_piv_off = nullptr, *d_sc_off = nullptr;
+    int32_t *d_kres_ptr = nullptr, *d_kres_col = nullptr, *d_kres_src = nullptr;
     int64_t *d_l_off = nullptr, *d_cb_off = nullptr;
     int32_t cap = 0;                 // instances with factor storage
     double* d_L = nullptr;           // [cap][l_size]
@@ -895,6 +896,28 @@ __global__ __launch_bounds__(ST) void k_front_bwd(Plan P, int f0, int batch, con
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// residual out = rhs - K x (iterative refinement): 4 KKT rows per 256-thread workgroup, one wave
+// per row, lanes = 64 instances (coalesced in the interleaved layout), the row's entries in
+// their fixed CSR order
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_kkt_residual(int dim, int batch, const int* __restrict__ rp,
+                                                      const int* __restrict__ col, const int* __restrict__ src,
+                                                      Vals V, const double* __restrict__ x,
+                                                      const double* __restrict__ rhs, double* __restrict__ out) {
+    const int r = __builtin_amdgcn_readfirstlane(blockIdx.y * 4 + (threadIdx.x >> 6));
+    const int b = blockIdx.x * 64 + (threadIdx.x & 63);
+    if (r >= dim || b >= batch) return;
+    const int e0 = rp[r], e1 = rp[r + 1];
+    double acc = 0.0;
+    for (int e = e0; e < e1; ++e) {
+        const int c = col[e];
+        acc = fma(src_value(V, src[e], b), x[(long long)c * V.se + (long long)b * V.sb], acc);
+    }
+    const long long o = (long long)r * V.se + (long long)b * V.sb;
+    out[o] = rhs[o] - acc;
+}
+
 template <int T>
 size_t factor_lds() {
     constexpr int NP = 32 * T;
@@ -1079,7 +1102,9 @@ int ato_kkt_create(const ato_kkt_plan_desc* d, ato_kkt** out) {
         (rc = upload(d->ent_ptr, F * MAXT + 1, &h->d_ent_ptr)) || (rc = upload(d->ent_pos, E, &h->d_ent_pos)) ||
         (rc = upload(d->ent_src, 2 * (size_t)E, &h->d_ent_src)) || (rc = upload(d->piv_off, F, &h->d_piv_off)) ||
         (rc = upload(d->l_off, F, &h->d_l_off)) || (rc = upload(d->cb_off, F, &h->d_cb_off)) ||
-        (rc = upload(d->sc_off, F, &h->d_sc_off))) {
+        (rc = upload(d->sc_off, F, &h->d_sc_off)) || (rc = upload(d->kres_ptr, h->dim + 1, &h->d_kres_ptr)) ||
+        (rc = upload(d->kres_col, (size_t)d->kres_ptr[h->dim], &h->d_kres_col)) ||
+        (rc = upload(d->kres_src, (size_t)d->kres_ptr[h->dim], &h->d_kres_src))) {
         ato_kkt_destroy(h);
         return rc;
     }
@@ -1093,7 +1118,7 @@ int ato_kkt_destroy(ato_kkt* h) {
     for (void* p : {(void*)h->d_pos_ptr, (void*)h->d_n_own, (void*)h->d_pos_index, (void*)h->d_parent_pos,
                     (void*)h->d_child_ptr, (void*)h->d_child_list, (void*)h->d_ent_ptr, (void*)h->d_ent_pos,
                     (void*)h->d_ent_src, (void*)h->d_piv_off, (void*)h->d_l_off, (void*)h->d_cb_off,
-                    (void*)h->d_sc_off})
+                    (void*)h->d_sc_off, (void*)h->d_kres_ptr, (void*)h->d_kres_col, (void*)h->d_kres_src})
         (void)hipFree(p);
     delete h;
     return ATO_OK;
@@ -1150,6 +1175,20 @@ int ato_kkt_solve(ato_kkt* h, int32_t batch, const int32_t* list, int64_t se, in
         const int rc = solve_level(h, P, l, false, batch, list, x, se, sb, st);
         if (rc != ATO_OK) return rc;
     }
+    return ATO_OK;
+}
+
+int ato_kkt_residual(ato_kkt* h, int32_t batch, int64_t se, int64_t sb, const double* H, const double* J,
+                     const double* dx, const double* dr, const double* x, const double* rhs, double* out,
+                     void* stream) {
+    if (!h || !x || !rhs || !out || !J || !dx || !dr || batch < 0) return fail(ATO_ERR_ARG, "bad argument");
+    if (batch == 0) return ATO_OK;
+    if (h->dim > 4 * 65535) return fail(ATO_ERR_UNSUPPORTED, "KKT residual: dimension above 262140");
+    const Vals V{H, J, dx, dr, se, sb};
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    hipLaunchKernelGGL(k_kkt_residual, dim3((batch + 63) / 64, (h->dim + 3) / 4), dim3(256), 0, st, h->dim, batch,
+                       h->d_kres_ptr, h->d_kres_col, h->d_kres_src, V, x, rhs, out);
+    KKT_HIP(hipGetLastError());
     return ATO_OK;
 }
 

@@ -91,7 +91,8 @@ EXPORTED_SYMBOLS = ('ato_create', 'ato_destroy', 'ato_sizes', 'ato_sparsity', 'a
                     'ato_reserve', 'ato_eval', 'ato_eval_f32', 'ato_hess_sparsity', 'ato_hess_eval',
                     'ato_mesh_create', 'ato_mesh_destroy', 'ato_mesh_signed_distance',
                     'ato_timing', 'ato_timing_read', 'ato_last_error', 'ato_version',
-                    'ato_kkt_create', 'ato_kkt_destroy', 'ato_kkt_reserve', 'ato_kkt_factor', 'ato_kkt_solve')
+                    'ato_kkt_create', 'ato_kkt_destroy', 'ato_kkt_reserve', 'ato_kkt_factor', 'ato_kkt_solve',
+                    'ato_kkt_residual')
 
 
 def library_path() -> str:
@@ -126,7 +127,10 @@ def declare(lib: ctypes.CDLL, prefix: str = 'ato') -> ctypes.CDLL:
         lib.ato_kkt_reserve.argtypes = [vp, ctypes.c_int32]
         lib.ato_kkt_factor.argtypes = [vp, ctypes.c_int32, vp, ctypes.c_int64, ctypes.c_int64, vp, vp, vp, vp, vp, vp]
         lib.ato_kkt_solve.argtypes = [vp, ctypes.c_int32, vp, ctypes.c_int64, ctypes.c_int64, vp, vp]
-        for fn in ('ato_kkt_create', 'ato_kkt_destroy', 'ato_kkt_reserve', 'ato_kkt_factor', 'ato_kkt_solve'):
+        lib.ato_kkt_residual.argtypes = [vp, ctypes.c_int32, ctypes.c_int64, ctypes.c_int64, vp, vp, vp, vp, vp, vp,
+                                         vp, vp]
+        for fn in ('ato_kkt_create', 'ato_kkt_destroy', 'ato_kkt_reserve', 'ato_kkt_factor', 'ato_kkt_solve',
+                   'ato_kkt_residual'):
             getattr(lib, fn).restype = ctypes.c_int
         for fn in ('ato_create', 'ato_destroy', 'ato_sizes', 'ato_sparsity', 'ato_bounds', 'ato_reserve',
                    'ato_eval', 'ato_eval_f32', 'ato_hess_sparsity', 'ato_hess_eval', 'ato_timing',

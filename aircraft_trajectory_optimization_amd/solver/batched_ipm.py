@@ -29,6 +29,8 @@ Interfaces (duck-typed so tests can substitute CPU stand-ins):
   kkt:       factor(H, J, dx, dr, instances) -> inertia [B,3] (int),
              solve(x [n+m, B], instances) in place
 '''
+import os
+import time
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
 
@@ -86,6 +88,47 @@ class BatchedDeviceEvaluator:
         self.counts['hess'] += 1
         return self.bn.hessian(lam.contiguous(), sigma.contiguous()).clone()
 
+    def subset(self, count: int) -> '_SubsetDeviceEvaluator':
+        ''' an evaluator over `count` <= batch instances (its own [element][count] buffers, the same
+        library handle): the restoration phase iterates only the instances it restores '''
+        return _SubsetDeviceEvaluator(self, count)
+
+
+class _SubsetDeviceEvaluator:
+    def __init__(self, base: BatchedDeviceEvaluator, count: int):
+        if not 0 < count <= base.batch:
+            raise ValueError('subset size out of range')
+        self.problem = base.bn.problem
+        self.device, self.batch = base.device, int(count)
+        self.n, self.m, self.nnz = base.n, base.m, base.nnz
+        self.j_row_ptr, self.j_col = base.j_row_ptr, base.j_col
+        self.h_row_ptr, self.h_col = base.h_row_ptr, base.h_col
+        self.lbg, self.ubg = base.lbg, base.ubg
+        self.var_stage = base.var_stage
+        opts = {'device': self.device, 'dtype': torch.float64}
+        B = self.batch
+        self.w = torch.zeros((self.n, B), **opts)
+        self.g = torch.zeros((self.m, B), **opts)
+        self.jac = torch.zeros((self.nnz, B), **opts)
+        self.gf = torch.zeros((self.n, B), **opts)
+        self.f = torch.zeros(B, **opts)
+        self.h = torch.zeros((len(self.h_col), B), **opts)
+
+    def eval(self, X: torch.Tensor):
+        self.w.copy_(X)
+        st = torch.cuda.current_stream(self.device)
+        self.problem.eval_ptrs(self.batch, self.w.data_ptr(), g=self.g.data_ptr(), jac=self.jac.data_ptr(),
+                               f=self.f.data_ptr(), grad_f=self.gf.data_ptr(), stream=st.cuda_stream)
+        return self.f.clone(), self.g.clone(), self.gf.clone(), self.jac.clone()
+
+    def hess(self, X: torch.Tensor, lam: torch.Tensor, sigma: torch.Tensor) -> torch.Tensor:
+        self.w.copy_(X)
+        lam, sigma = lam.contiguous(), sigma.contiguous()
+        st = torch.cuda.current_stream(self.device)
+        self.problem.hess_eval_ptrs(self.batch, self.w.data_ptr(), lam.data_ptr(), sigma.data_ptr(),
+                                    self.h.data_ptr(), stream=st.cuda_stream)
+        return self.h.clone()
+
 
 def device_solver(spec, batch: int, lbx, ubx, options: Optional[IPMOptions] = None, device=None):
     ''' BatchedInteriorPoint over the HIP evaluation library and the device KKT factorisation '''
@@ -95,6 +138,27 @@ def device_solver(spec, batch: int, lbx, ubx, options: Optional[IPMOptions] = No
     plan = build_plan(ev.n, ev.m, ev.var_stage, ev.j_row_ptr, ev.j_col, ev.h_row_ptr, ev.h_col)
     kkt = DeviceKKT(plan, batch, ev.device)
     return BatchedInteriorPoint(ev, kkt, lbx, ubx, options)
+
+
+class _Laps:
+    ''' diagnostic wall-time split of the solve (ATO_IPM_PROFILE=1): lap(name) synchronises the
+    device and books the time since the previous lap under `name`; off, it costs nothing '''
+
+    def __init__(self, device):
+        self.on = os.environ.get('ATO_IPM_PROFILE', '0') == '1'
+        self.cuda = torch.device(device).type == 'cuda'
+        self.t: Dict[str, float] = {}
+        self.last = None
+
+    def lap(self, name=None):
+        if not self.on:
+            return
+        if self.cuda:
+            torch.cuda.synchronize()
+        now = time.perf_counter()
+        if name is not None and self.last is not None:
+            self.t[name] = self.t.get(name, 0.0) + now - self.last
+        self.last = now
 
 
 def _idx(mask: torch.Tensor) -> np.ndarray:
@@ -152,6 +216,7 @@ class BatchedInteriorPoint:
         self.w_src, self.w_col = t(w_src[pw], torch.long), t(w_col[pw], torch.long)
         self.w_len = t(np.bincount(w_row, minlength=n), torch.long)
         self.stats = {'factorizations': 0, 'solves': 0, 'evals': 0, 'hess': 0}
+        self.laps = _Laps(dev)
 
     # ------------------------------------------------------------------ sparse products
     @staticmethod
@@ -174,6 +239,12 @@ class BatchedInteriorPoint:
             ox = ox + self._Wx(H, vx)
         oy = self._Jx(Js, vx) + dr * vy
         return torch.cat([ox, oy])
+
+    def _residual(self, H, Js, dx, dr, x, rhs):
+        ''' rhs - K x: the KKT backend's fused kernel (ato_kkt_residual) when it has one '''
+        if hasattr(self.kkt, 'residual'):
+            return self.kkt.residual(H, Js, dx, dr, x, rhs)
+        return rhs - self._Kmul(H, Js, dx, dr, x)
 
     # ------------------------------------------------------------------ pieces
     def _eval(self, x):
@@ -286,22 +357,27 @@ class BatchedInteriorPoint:
         if len(idx) == 0:
             self.last_solve_ok = torch.zeros_like(mask)
             return x
+        self.laps.lap('kkt_other')
         self.kkt.solve(x, idx)
+        self.laps.lap('kkt_solve')
         self.stats['solves'] += 1
         scale = rhs.abs().amax(0) + 1e-300
         for _ in range(10):
-            res = rhs - self._Kmul(H, Js, dx, dr, x)
+            res = self._residual(H, Js, dx, dr, x, rhs)
             rmax = res.abs().amax(0)
             need = mask & torch.isfinite(rmax) & (rmax > 1e-10 * scale)
             if not bool(need.any()):
                 break
             corr = res.clone()
+            self.laps.lap('kkt_refine')
             self.kkt.solve(corr, _idx(need))
+            self.laps.lap('kkt_solve')
             self.stats['solves'] += 1
             x = torch.where(need[None, :], x + corr, x)
         # IPOPT (residual_ratio_singular): unrefinable solves count as singular matrices
-        res = (rhs - self._Kmul(H, Js, dx, dr, x)).abs().amax(0)
+        res = self._residual(H, Js, dx, dr, x, rhs).abs().amax(0)
         self.last_solve_ok = torch.isfinite(res) & (res <= 1e-5 * scale)
+        self.laps.lap('kkt_refine')
         return x
 
     def _ls_multipliers(self, Js, gf, zl, zu, vl, vu, act):
@@ -343,7 +419,9 @@ class BatchedInteriorPoint:
             dr = (-delta_c).expand(m, B).clone()
             dr[self.iin] -= 1.0 / Ds_tot
             dx = Sx + delta_w
+            self.laps.lap('kkt_other')
             inertia = self.kkt.factor(W, Js, dx, dr, _idx(pend))
+            self.laps.lap('kkt_factor')
             self.stats['factorizations'] += 1
             ok = (inertia[:, 0] == n) & (inertia[:, 1] == m) & (inertia[:, 2] == 0)
             sing = inertia[:, 2] > 0
@@ -460,6 +538,8 @@ class BatchedInteriorPoint:
             F[rows, pos] = torch.where(mask[:, None], entry, cur)
             nf = torch.where(mask, torch.clamp(nf + 1, max=FILTER_MAX), nf)
 
+        laps = self.laps
+        laps.lap()
         for it in range(3 * o.max_iter + 3):
             iters = torch.where(act, own, iters)
             Js = jv * sg[self.jr]
@@ -484,6 +564,7 @@ class BatchedInteriorPoint:
             act = act & ~mx
             if not bool(act.any()) and not bool(waiting.any()):
                 break
+            laps.lap('check')
             stepping = act.clone()
             resto = torch.zeros(B, dtype=torch.bool, device=dev)
             if progress and it % progress == 0:
@@ -501,9 +582,11 @@ class BatchedInteriorPoint:
                     mu = torch.where(upd, mu_new, mu)
                     tau = torch.where(upd, torch.clamp(1.0 - mu, min=o.tau_min), tau)
                     nf = torch.where(upd, torch.zeros_like(nf), nf)
+                laps.lap('barrier')
                 # ---- Newton step
                 W = self.ev.hess(x, y * sg, sf)
                 self.stats['hess'] += 1
+                laps.lap('hess')
                 a, b, c, d = self._slacks(x, s)
                 Sx = torch.where(self.hxl, zl / a, 0.0) + torch.where(self.hxu, zu / b, 0.0)
                 Ss = torch.where(self.hsl, vl / c, 0.0) + torch.where(self.hsu, vu / d, 0.0)
@@ -512,7 +595,9 @@ class BatchedInteriorPoint:
                 rhs_x = -(gx + self._JTy(Js, y))
                 rhs_s = -(gs - y[self.iin])
                 rhs_y = -r
+                laps.lap('rhs')
                 dx, ds, dy, delta_w, ok, ctx = self._kkt_step(W, Js, Sx, Ss, rhs_x, rhs_s, rhs_y, mu, dwl, act)
+                laps.lap('kkt_other')
                 kfail = act & ~ok
                 status = torch.where(kfail, torch.full_like(status, KKT_FAILED), status)
                 act = act & ok
@@ -560,6 +645,7 @@ class BatchedInteriorPoint:
                     dyn = torch.where(m2, dyt, dyn)
                     armn = torch.where(mask, arm, armn)
 
+                laps.lap('direction')
                 for _ls in range(200):
                     failed = pend & ~(alpha >= alpha_min)
                     if bool(failed.any()):
@@ -573,7 +659,9 @@ class BatchedInteriorPoint:
                         break
                     xt = x + alpha * dx
                     st = s + alpha * ds
+                    laps.lap('ls_logic')
                     ft, gt, gft, jvt = self._eval(xt)
+                    laps.lap('ls_eval')
                     rt = self._resid(gt, st)
                     tht = rt.abs().sum(0)
                     pht = self._phi(ft, xt, st, mu)
@@ -583,11 +671,14 @@ class BatchedInteriorPoint:
                     pend = pend & ~okt
                     soc = pend & first & (tht >= theta)
                     if bool(soc.any()):
+                        laps.lap('ls_logic')
                         got = self._soc(soc, ctx, rhs_x, rhs_s, x, s, alpha, r, rt, theta, phi, gphi_d, F, nf, tau,
                                         (a, b, c, d), mu, take)
                         pend = pend & ~got
+                        laps.lap('soc')
                     first = first & False
                     alpha = torch.where(pend, alpha * 0.5, alpha)
+                laps.lap('ls_logic')
                 # ---- accept
                 upd = act & ~resto
                 add_filter(upd & ~armn, theta, phi)
@@ -609,6 +700,7 @@ class BatchedInteriorPoint:
                 vl = torch.where(self.hsl, torch.minimum(torch.maximum(vl, mu / (ks * c)), ks * mu / c), 0.0)
                 vu = torch.where(self.hsu, torch.minimum(torch.maximum(vu, mu / (ks * d)), ks * mu / d), 0.0)
             own = own + stepping.long()
+            laps.lap('accept')
             # ---- feasibility restoration: instances whose line search failed wait (frozen) and are
             # restored together, so one nested batched solve serves many of them
             waiting = waiting | resto
@@ -626,6 +718,7 @@ class BatchedInteriorPoint:
                     phi_w = self._phi(f, x, s, mu)
                     add_filter(can, theta_w, phi_w)
                     xr, okr = self._restore(can, x, g, mu, theta_w, F, nf)
+                    laps.lap('resto')
                     bad = can & ~okr
                     status = torch.where(bad, torch.full_like(status, LS_FAILED), status)
                     if bool(okr.any()):
@@ -644,6 +737,7 @@ class BatchedInteriorPoint:
                         vu = torch.where(r2, torch.where(self.hsu, mu / d, 0.0), vu)
                         y = torch.where(r2, self._ls_multipliers(jv * sg[self.jr], gf, zl, zu, vl, vu, okr), y)
                         act = act | okr
+                laps.lap('resto_post')
 
         if o.honor_original_bounds:
             x = torch.minimum(torch.maximum(x, self.lbx0), self.ubx0)
@@ -652,6 +746,8 @@ class BatchedInteriorPoint:
         # [lockstep iteration][f, inf_pr, inf_du, mu, E0, restorations so far][instance]
         self.history = torch.stack(history).cpu().numpy() if history else np.zeros((0, 6, B))
         self.stats['restorations'] = self.stats.get('restorations', 0) + int(n_resto.sum())
+        if laps.on:
+            self.stats['laps'] = dict(laps.t)
         return BatchedIPMResult(x=x, f=fu, lam_g=y * sg / sf, lam_x=(zu - zl) / sf,
                                 status=[STATUS_NAMES[int(v)] for v in st], iters=iters.cpu().numpy(),
                                 stats=dict(self.stats))
@@ -703,16 +799,31 @@ class BatchedInteriorPoint:
         a_ = (mu_r - rho * viol) / (2 * rho)
         nn = a_ + torch.sqrt(a_ * a_ + mu_r * viol / (2 * rho))
         pp = viol + nn
-        rev = _RestorationEvaluator(self.ev, self.sg, x, torch.sqrt(mu), rho, self.lbg_s, self.ubg_s)
-        Xr0 = torch.cat([x, pp, nn])
-        lbx = torch.cat([self.lbx0, torch.zeros((2 * m, B), dtype=torch.float64, device=dev)])
-        ubx = torch.cat([self.ubx0, torch.full((2 * m, B), np.inf, dtype=torch.float64, device=dev)])
+        # the nested solve runs on the restored instances only (compacted columns) when the
+        # evaluator and the KKT backend offer subsets; the others would only be carried along
+        compact = hasattr(self.ev, 'subset') and hasattr(self.kkt, 'view')
+        sel = torch.nonzero(R).reshape(-1) if compact else None
+        cols = (lambda t: t.index_select(t.dim() - 1, sel).contiguous()) if compact else (lambda t: t)  # noqa: E731
+        ev_r = self.ev.subset(len(sel)) if compact else self.ev
+        kkt_r = self.kkt.view(len(sel)) if compact else self.kkt
+        rev = _RestorationEvaluator(ev_r, cols(self.sg), cols(x), cols(torch.sqrt(mu)), rho, cols(self.lbg_s),
+                                    cols(self.ubg_s))
+        Br = rev.batch
+        Xr0 = torch.cat([cols(x), cols(pp), cols(nn)])
+        lbx = torch.cat([cols(self.lbx0), torch.zeros((2 * m, Br), dtype=torch.float64, device=dev)])
+        ubx = torch.cat([cols(self.ubx0), torch.full((2 * m, Br), np.inf, dtype=torch.float64, device=dev)])
         ro = IPMOptions(**{**o.__dict__, 'nlp_scaling': False, 'max_iter': 3000})
-        sub = BatchedInteriorPoint(rev, _RestorationKKT(self.kkt, rev), lbx.cpu().numpy(), ubx.cpu().numpy(), ro)
+        sub = BatchedInteriorPoint(rev, _RestorationKKT(kkt_r, rev), lbx.cpu().numpy(), ubx.cpu().numpy(), ro)
         theta_start = theta
 
         def accept(xr):
-            xo = xr[:n]
+            # restoration's return test on the original NLP (full width: the stored state, filter
+            # and bounds of the outer solve are [.., B])
+            xo = x.clone()
+            if compact:
+                xo[:, sel] = xr[:n]
+            else:
+                xo = xr[:n]
             f2, g2, _, _ = self._eval(xo)
             s2 = self._push(g2[self.iin], self.dL, self.dU)
             th = self._resid(g2, s2).abs().sum(0)
@@ -720,15 +831,25 @@ class BatchedInteriorPoint:
             k = torch.arange(F.shape[1], device=dev)
             valid = k[None, :] < nf[:, None]
             in_f = (valid & (th[:, None] >= F[:, :, 0]) & (ph[:, None] >= F[:, :, 1])).any(1)
-            return (th <= o.resto_kappa * theta_start) & ~in_f
+            ok = (th <= o.resto_kappa * theta_start) & ~in_f
+            return ok[sel] if compact else ok
 
-        res = sub.solve(Xr0, mu0=mu_r, active=R, stop_check=accept, allow_restoration=False,
-                        progress=self._progress)
+        res = sub.solve(Xr0, mu0=cols(mu_r), active=None if compact else R, stop_check=accept,
+                        allow_restoration=False, progress=self._progress)
         for k2, v in sub.stats.items():
-            if k2 != 'restorations':
+            if k2 not in ('restorations', 'laps'):
                 self.stats[k2] = self.stats.get(k2, 0) + v
-        ok = R & torch.as_tensor(np.array([st == 'stopped' for st in res.status]), device=dev)
-        return torch.minimum(torch.maximum(res.x[:n], self.xL), self.xU), ok
+        for k2, v in sub.laps.t.items():          # diagnostic split of the nested solve
+            self.laps.t['resto:' + k2] = self.laps.t.get('resto:' + k2, 0.0) + v
+        stopped = torch.as_tensor(np.array([st == 'stopped' for st in res.status]), device=dev)
+        if compact:
+            xr = x.clone()
+            xr[:, sel] = res.x[:n]
+            ok = torch.zeros_like(R)
+            ok[sel] = stopped
+        else:
+            xr, ok = res.x[:n], R & stopped
+        return torch.minimum(torch.maximum(xr, self.xL), self.xU), ok
 
 
 class _RestorationEvaluator:

@@ -44,6 +44,9 @@ class AtoKKTPlanDesc(ctypes.Structure):
         ('cb_size', ctypes.c_int64),
         ('sc_off', _i32p),
         ('sc_size', ctypes.c_int32),
+        ('kres_ptr', _i32p),
+        ('kres_col', _i32p),
+        ('kres_src', _i32p),
     ]
 
 
@@ -81,6 +84,9 @@ class DeviceKKT:
         d.cb_size = plan.cb_size
         d.sc_off = arr(plan.sc_off, np.int32, _i32p)
         d.sc_size = plan.sc_size
+        d.kres_ptr = arr(plan.kres_ptr, np.int32, _i32p)
+        d.kres_col = arr(plan.kres_col, np.int32, _i32p)
+        d.kres_src = arr(plan.kres_src, np.int32, _i32p)
         self.desc = d
         h = ctypes.c_void_p()
         with torch.cuda.device(self.device):
@@ -139,6 +145,17 @@ class DeviceKKT:
         self._last_list = lst
         return x
 
+    def residual(self, H: Optional[torch.Tensor], J: torch.Tensor, dx: torch.Tensor, dr: torch.Tensor,
+                 x: torch.Tensor, rhs: torch.Tensor, stream=None) -> torch.Tensor:
+        ''' rhs - K x for every instance (x, rhs [dim][max_batch]); iterative-refinement residual '''
+        return _residual(self, self.cap, H, J, dx, dr, x, rhs, stream)
+
+    def view(self, count: int) -> '_KKTView':
+        ''' the same factor storage driven with [element][count] value arrays (instances 0 .. count-1
+        of the view's own numbering use storage slots 0 .. count-1): the restoration phase runs
+        its nested solve on a compacted batch between two outer factorisations '''
+        return _KKTView(self, count)
+
     def close(self):
         if getattr(self, 'handle', None):
             self.lib.ato_kkt_destroy(self.handle)
@@ -149,3 +166,60 @@ class DeviceKKT:
             self.close()
         except Exception:  # pylint: disable=broad-except
             pass
+
+
+def _residual(kkt, B, H, J, dx, dr, x, rhs, stream):
+    vals = [t.contiguous() for t in (J, dx, dr, x, rhs)] + ([H.contiguous()] if H is not None else [])
+    for t in vals:
+        if t.dtype != torch.float64 or t.dim() != 2 or t.shape[1] != B or t.device != kkt.device:
+            raise ValueError('KKT residual operands must be fp64 [elements][batch] tensors on the KKT device')
+    J, dx, dr, x, rhs = vals[:5]
+    H = vals[5] if H is not None else None
+    out = torch.empty_like(rhs)
+    st = stream if stream is not None else torch.cuda.current_stream(kkt.device)
+    kkt._check(kkt.lib.ato_kkt_residual(kkt.handle, B, B, 1, H.data_ptr() if H is not None else None, J.data_ptr(),
+                                        dx.data_ptr(), dr.data_ptr(), x.data_ptr(), rhs.data_ptr(), out.data_ptr(),
+                                        st.cuda_stream))
+    return out
+
+
+class _KKTView:
+    def __init__(self, base: DeviceKKT, count: int):
+        if not 0 < count <= base.cap:
+            raise ValueError('KKT view larger than the reserved batch')
+        self.base, self.cap, self.plan, self.device = base, int(count), base.plan, base.device
+
+    def factor(self, H, J, dx, dr, instances=None, stream=None) -> torch.Tensor:
+        b = self.base
+        J, dx, dr = J.contiguous(), dx.contiguous(), dr.contiguous()
+        H = H.contiguous() if H is not None else None
+        for t in (J, dx, dr) + ((H,) if H is not None else ()):
+            if t.dtype != torch.float64 or t.dim() != 2 or t.shape[1] != self.cap or t.device != self.device:
+                raise ValueError('KKT view values must be fp64 [elements][count] tensors on the KKT device')
+        self._keep_vals = (H, J, dx, dr)
+        lst, nb = b._list(instances)
+        if instances is None:
+            nb = self.cap
+        st = stream if stream is not None else torch.cuda.current_stream(self.device)
+        b._check(b.lib.ato_kkt_factor(b.handle, nb, lst.data_ptr() if lst is not None else None, self.cap, 1,
+                                      H.data_ptr() if H is not None else None, J.data_ptr(), dx.data_ptr(),
+                                      dr.data_ptr(), b.inertia.data_ptr(), st.cuda_stream))
+        self._last_list = lst
+        return b.inertia[:self.cap]
+
+    def residual(self, H, J, dx, dr, x, rhs, stream=None):
+        return _residual(self.base, self.cap, H, J, dx, dr, x, rhs, stream)
+
+    def solve(self, x, instances=None, stream=None):
+        b = self.base
+        if x.dtype != torch.float64 or x.shape != (self.plan.dim, self.cap) or not x.is_contiguous() or \
+                x.device != self.device:
+            raise ValueError('x must be a contiguous fp64 [dim][count] tensor on the KKT device')
+        lst, nb = b._list(instances)
+        if instances is None:
+            nb = self.cap
+        st = stream if stream is not None else torch.cuda.current_stream(self.device)
+        b._check(b.lib.ato_kkt_solve(b.handle, nb, lst.data_ptr() if lst is not None else None, self.cap, 1,
+                                     x.data_ptr(), st.cuda_stream))
+        self._last_list = lst
+        return x

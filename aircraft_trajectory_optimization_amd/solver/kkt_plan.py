@@ -83,6 +83,9 @@ class KKTPlan:
     sc_off: np.ndarray          # [F] offset of the front's solve contribution (tq doubles)
     sc_size: int
     block_sizes: np.ndarray     # [F] own + trailing
+    kres_ptr: np.ndarray        # [dim+1] CSR of the whole K (both triangles) for residuals r - K x
+    kres_col: np.ndarray        # [nnz_K] column (KKT index), ascending within a row
+    kres_src: np.ndarray        # [nnz_K] source code of the value (a diagonal with two sources: two entries)
 
     @property
     def max_block(self) -> int:
@@ -309,6 +312,25 @@ def build_plan(n: int, m: int, var_stage, j_row_ptr, j_col, h_row_ptr, h_col, or
     child_ptr = np.concatenate([[0], np.cumsum([len(c) for c in children])])
     child_list = np.asarray([c for cs in children for c in cs], np.int64)
 
+    # ---- CSR of K for the residual kernel (refinement): every structural entry in both triangles
+    rr, cc, ss = [], [], []
+    for e in range(len(h_col)):
+        r_, c_ = int(hr[e]), int(h_col[e])
+        rr.append(r_), cc.append(c_), ss.append(src_code(SRC_H, e))
+        if r_ != c_:
+            rr.append(c_), cc.append(r_), ss.append(src_code(SRC_H, e))
+    for j in range(n):
+        rr.append(j), cc.append(j), ss.append(src_code(SRC_DX, j))
+    for e in range(len(j_col)):
+        i, j = n + int(jr[e]), int(j_col[e])
+        rr.append(i), cc.append(j), ss.append(src_code(SRC_J, e))
+        rr.append(j), cc.append(i), ss.append(src_code(SRC_J, e))
+    for i in range(m):
+        rr.append(n + i), cc.append(n + i), ss.append(src_code(SRC_DR, i))
+    rr, cc, ss = np.asarray(rr), np.asarray(cc), np.asarray(ss)
+    o = np.lexsort((ss, cc, rr))
+    kres_ptr = np.searchsorted(rr[o], np.arange(dim + 1))
+
     # ---- per-instance storage: compact factor columns, pivot records, contribution blocks
     n_own = np.array([len(o) for o in own])
     tq = sizes - n_own
@@ -325,4 +347,5 @@ def build_plan(n: int, m: int, var_stage, j_row_ptr, j_col, h_row_ptr, h_col, or
                    ent_ptr=i32(ent_ptr), ent_pos=i32(ent_pos), ent_src=i32(ent_src).reshape(-1, 2),
                    l_off=np.asarray(l_off[:-1], np.int64), l_size=int(l_off[-1]),
                    piv_off=i32(piv_off[:-1]), cb_off=np.asarray(cb_off[:-1], np.int64), cb_size=int(cb_off[-1]),
-                   sc_off=i32(sc_off[:-1]), sc_size=int(sc_off[-1]), block_sizes=i32(sizes))
+                   sc_off=i32(sc_off[:-1]), sc_size=int(sc_off[-1]), block_sizes=i32(sizes),
+                   kres_ptr=i32(kres_ptr), kres_col=i32(cc[o]), kres_src=i32(ss[o]))

@@ -57,6 +57,9 @@ typedef struct ato_kkt_plan_desc {
     int64_t cb_size;            /* contribution-block doubles per instance                      */
     const int32_t* sc_off;      /* [F] solve-contribution offset (tq doubles per front)          */
     int32_t sc_size;            /* solve-contribution doubles per instance                      */
+    const int32_t* kres_ptr;    /* [n + m + 1] CSR of the whole K (both triangles): residuals    */
+    const int32_t* kres_col;    /* [nnz_K] column (KKT index) of every entry                     */
+    const int32_t* kres_src;    /* [nnz_K] source code of every entry (as ent_src, one source)   */
 } ato_kkt_plan_desc;
 
 typedef struct ato_kkt ato_kkt;
@@ -80,6 +83,13 @@ int ato_kkt_factor(ato_kkt* kkt, int32_t batch, const int32_t* list, int64_t str
  * factors of the listed instances. Asynchronous on stream. */
 int ato_kkt_solve(ato_kkt* kkt, int32_t batch, const int32_t* list, int64_t stride_elem,
                   int64_t stride_inst, double* x, void* stream);
+
+/* out = rhs - K x for all `batch` instances (x, rhs, out: [n + m] KKT order; H may be NULL),
+ * the residual of IPOPT's iterative refinement of a KKT solve. Every instance sums its row
+ * entries in a fixed order (deterministic). Asynchronous on stream. */
+int ato_kkt_residual(ato_kkt* kkt, int32_t batch, int64_t stride_elem, int64_t stride_inst,
+                     const double* H, const double* J, const double* diag_x, const double* diag_r,
+                     const double* x, const double* rhs, double* out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -16,6 +16,7 @@ from tests.helpers import HostEvaluator
 
 class HostBatchEvaluator:
     def __init__(self, spec, batch):
+        self.spec = spec
         self.h = HostEvaluator(spec)
         self.batch, self.device = batch, torch.device('cpu')
         self.n, self.m = self.h.nw, self.h.ng
@@ -32,6 +33,10 @@ class HostBatchEvaluator:
     def hess(self, X, lam, sigma):
         H = self.h.hc.hess(X.T.contiguous().numpy(), lam.T.contiguous().numpy(), sigma.numpy())
         return torch.as_tensor(np.ascontiguousarray(H.T))
+
+    def subset(self, count):
+        ''' the solver's compacted restoration batch (BatchedDeviceEvaluator.subset) '''
+        return HostBatchEvaluator(self.spec, count)
 
 
 class HostBlockKKT:
@@ -58,6 +63,16 @@ class HostBlockKKT:
         for b in instances:
             x[:, b] = torch.as_tensor(self.fac[b].solve(x[:, b].numpy()))
         return x
+
+    def view(self, count):
+        ''' a backend for the compacted restoration batch (DeviceKKT.view) '''
+        class _Shape:
+            pass
+        ev = _Shape()
+        ev.__dict__.update({k: getattr(self.ev, k) for k in ('n', 'm', 'var_stage', 'j_row_ptr', 'j_col',
+                                                              'h_row_ptr', 'h_col')})
+        ev.batch = count
+        return HostBlockKKT(ev)
 
 
 class EmulatedPlanKKT:

@@ -124,3 +124,27 @@ def test_device_kkt_racetrack_full_size():
         assert tuple(inertia[b]) == tuple(host_inertia)
         res = np.abs(K @ x[:, b] - rhs[:, b]).max()
         assert res <= 1e-8 * max(1.0, abs(K).max()), res
+
+
+@pytest.mark.parametrize('with_h', [True, False])
+def test_device_kkt_residual_matches_dense(with_h):
+    ''' ato_kkt_residual (iterative refinement) = rhs - K x of the dense matrix, with and without W '''
+    from aircraft_trajectory_optimization_amd.solver.kkt_device import DeviceKKT
+    spec = product_spec(track='race', N=6, K=4)
+    B = 3
+    vals = [random_kkt_values(spec, seed) for seed in range(B)]
+    ev = vals[0][0]
+    plan = build_plan(ev.nw, ev.ng, var_stages(spec), ev.j_row_ptr, ev.j_col, ev.h_row_ptr, ev.h_col)
+    kkt = DeviceKKT(plan, B)
+    rng = np.random.default_rng(11)
+    x = rng.standard_normal((plan.dim, B))
+    rhs = rng.standard_normal((plan.dim, B))
+    H = _dev([v[1] for v in vals]) if with_h else None
+    out = kkt.residual(H, _dev([v[2] for v in vals]), _dev([v[3] for v in vals]), _dev([v[4] for v in vals]),
+                       torch.as_tensor(x, device='cuda'), torch.as_tensor(rhs, device='cuda')).cpu().numpy()
+    for b in range(B):
+        _, Hb, Jb, dxb, drb = vals[b]
+        K = dense_kkt(plan, Hb if with_h else np.zeros_like(Hb), Jb, dxb, drb, ev.h_row_ptr, ev.h_col,
+                      ev.j_row_ptr, ev.j_col)
+        ref = rhs[:, b] - K @ x[:, b]
+        assert np.abs(out[:, b] - ref).max() <= 1e-12 * max(1.0, np.abs(ref).max())

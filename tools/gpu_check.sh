@@ -53,10 +53,12 @@ for s in $STEPS; do
                run kkt_b1 200 python tools/bench_kkt.py --batch 1 --out "$OUT/kkt_b1.json"
                run kkt_chain_b512 200 python tools/bench_kkt.py --batch 512 --ordering chain --out "$OUT/kkt_chain_b512.json"
                run kkt_chain_b1 200 python tools/bench_kkt.py --batch 1 --ordering chain --out "$OUT/kkt_chain_b1.json" ;;
+        ipmtests) run pytest_ipm 600 python -u -m pytest tests/test_gpu_batched_ipm.py -x -v --timeout 300 --timeout-method thread -p no:cacheprovider ;;
         kkttests) run pytest_kkt 300 python -u -m pytest tests/test_gpu_kkt.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider ;;
         solve) run solve_b512 600 python tools/solve_batched.py --batch 512 --max-iter 200 --no-host --out "$OUT/solve_b512.json" ;;
         solveprof) run solveprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/solveprof" -o run -- \
                    python tools/solve_batched.py --batch 512 --max-iter 60 --no-host --out "$OUT/solveprof.json" ;;
+        solvelaps) ATO_IPM_PROFILE=1 run solvelaps 600 python tools/solve_batched.py --batch 512 --max-iter 60 --no-host --out "$OUT/solvelaps.json" ;;
         listpmc) run listpmc 120 rocprofv3 -L ;;
         mbpmc) run mb_fetch 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/mb_fetch" -o run -- ./tools/mb_store
                run mb_write 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/mb_write" -o run -- ./tools/mb_store ;;
