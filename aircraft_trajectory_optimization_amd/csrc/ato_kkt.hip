@@ -53,6 +53,12 @@ struct ato_kkt {
     int2* d_sinfo = nullptr;         // [cap][F] {steps, used stream length of the front}
 };
 
+#ifdef ATO_KKT_STAMPS
+// DIAGNOSTIC build only (tools/diag/kkt_phase.py): shader-clock phase totals of the workgroup
+// (front 0 = the first interval leaf, instance 0) of the factorisation, thread 0
+__device__ unsigned long long g_kkt_stamps[8];
+#endif
+
 namespace {
 
 int fail(int code, const std::string& m) {
@@ -150,6 +156,23 @@ struct Mask {
         }
     }
 };
+
+#ifdef ATO_KKT_STAMPS
+__device__ __forceinline__ unsigned long long kstamp() {
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#define KST_DECL(on_) unsigned long long kst_acc[6] = {0, 0, 0, 0, 0, 0}, kst_last = kstamp(); const bool kst_on = (on_);
+#define KST(i) do { if (kst_on) { const unsigned long long t_ = kstamp(); kst_acc[i] += t_ - kst_last; kst_last = t_; } } while (0)
+#define KST_DUMP(n_) do { if (kst_on && threadIdx.x == 0) { for (int i_ = 0; i_ < 6; ++i_) g_kkt_stamps[i_] = kst_acc[i_]; g_kkt_stamps[6] = (n_); } } while (0)
+#else
+#define KST_DECL(on_)
+#define KST(i)
+#define KST_DUMP(n_)
+#endif
 
 // LDS-only workgroup barrier: waits for this wave's LDS operations, not for its global stores
 // (the factor columns written every step are read only by later launches)
@@ -302,6 +325,7 @@ __global__ __launch_bounds__(FT) void k_front_factor(Plan P, Vals V, int f0, int
     double* dv = dinv + ((long long)b * P.dim + P.piv_off[f]) * 3;
     int npos = 0, nneg = 0, nzero = 0;
     long long loff = 0;                          // running offset in the front's column stream
+    KST_DECL(f == 0 && blockIdx.y == 0)
 
     // ---- original entries (positions and values) into registers
     const int e0 = P.ent_ptr[f * MAXT], e1 = P.ent_ptr[(f + 1) * MAXT];
@@ -378,6 +402,7 @@ __global__ __launch_bounds__(FT) void k_front_factor(Plan P, Vals V, int f0, int
     bool lvt = tid < A;           // per thread: its factor-column position tid live ...
     int cit = tid;                // ... and its index among the live positions
     int kc = 0, steps = 0, par = 0;
+    KST(0);                      // assembly
     while (true) {
         while (kc < own && !live.get(kc)) ++kc;
         if (kc >= own) break;
@@ -386,6 +411,7 @@ __global__ __launch_bounds__(FT) void k_front_factor(Plan P, Vals V, int f0, int
         double* cr = colb + (par * 2 + 1) * NP;
         extract_column<T>(a, k, ti, tj, ck);
         lds_barrier();
+        KST(1);                  // extract + barrier (waits for the slowest wave's update)
         // lambda = max_{i eligible, i != k} |A_ik| and its index r
         // every lane keeps its column values: A_kk and lambda come back by readlane, not LDS
         unsigned key = 0u;
@@ -435,6 +461,7 @@ __global__ __launch_bounds__(FT) void k_front_factor(Plan P, Vals V, int f0, int
                 type = 1;
             }
         }
+        KST(2);                  // pivot search and decision
         // ---- pivot record, inertia, factor columns, Schur update
         double i00 = 0.0, i01 = 0.0, i11 = 0.0;
         if (type == 2) {
@@ -481,10 +508,11 @@ __global__ __launch_bounds__(FT) void k_front_factor(Plan P, Vals V, int f0, int
         // second (2x2 pivot); A -= l0 c0^T (+ l1 cr^T), c0 = column p (1x1) or k (2x2)
         double l0[T], l1[T];
         {
-            double xk[T], xr[T];
-            column_rows<T, NQ>(cv, xk);
-            column_rows<T, NQ>(cw, xr);
+            double xk[T];
+            column_rows<T, NQ>(use_r ? cw : cv, xk);
             if (type == 1) {
+                double xr[T];
+                column_rows<T, NQ>(cw, xr);
 #pragma unroll
                 for (int I = 0; I < T; ++I) {
                     l0[I] = xk[I] * i00 + xr[I] * i01;
@@ -493,7 +521,7 @@ __global__ __launch_bounds__(FT) void k_front_factor(Plan P, Vals V, int f0, int
             } else {
 #pragma unroll
                 for (int I = 0; I < T; ++I) {
-                    l0[I] = (use_r ? xr[I] : xk[I]) * i00;
+                    l0[I] = xk[I] * i00;
                     l1[I] = 0.0;
                 }
             }
@@ -517,8 +545,10 @@ __global__ __launch_bounds__(FT) void k_front_factor(Plan P, Vals V, int f0, int
             }
         }
         loff += (long long)nlive * ncol;
+        KST(3);                  // pivot inverse, record, row factors, factor-column stores
         // Schur update: one rank-1 pass (1x1 pivot) or two (2x2 pivot); tiles of dead rows are
-        // skipped, dead column tiles are updated too (harmless, no per-tile branches)
+        // skipped, dead column tiles are updated too (skipping them per tile costs the compiler a
+        // select per entry: measured 2x slower)
         const int npass = type == 0 ? 1 : type == 1 ? 2 : 0;
         for (int pass = 0; pass < npass; ++pass) {
             const double* cc = pass == 1 ? cr : (use_r ? cr : ck);
@@ -544,7 +574,9 @@ __global__ __launch_bounds__(FT) void k_front_factor(Plan P, Vals V, int f0, int
         }
         ++steps;
         par ^= 1;
+        KST(4);                  // Schur update
     }
+    KST_DUMP(steps);
     if (tid == 0) {
         sinfo[(long long)b * P.F + f] = make_int2(steps, (int)loff);
         atomicAdd(&inertia[3 * b + 0], npos);
@@ -1038,6 +1070,13 @@ void free_storage(ato_kkt* h) {
 }  // namespace
 
 extern "C" {
+
+#ifdef ATO_KKT_STAMPS
+int ato_kkt_diag_stamps(unsigned long long* out) {
+    KKT_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_kkt_stamps), sizeof(unsigned long long) * 8));
+    return ATO_OK;
+}
+#endif
 
 int ato_kkt_create(const ato_kkt_plan_desc* d, ato_kkt** out) {
     if (!d || !out) return fail(ATO_ERR_ARG, "null argument");

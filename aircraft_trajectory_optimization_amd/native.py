@@ -96,8 +96,9 @@ EXPORTED_SYMBOLS = ('ato_create', 'ato_destroy', 'ato_sizes', 'ato_sparsity', 'a
 
 
 def library_path() -> str:
-    ''' in-tree location of the HIP library '''
-    return os.path.join(os.path.dirname(os.path.abspath(__file__)), '_lib', 'libato.so')
+    ''' in-tree location of the HIP library (ATO_LIB_PATH overrides it: diagnostic kernel variants) '''
+    return os.environ.get('ATO_LIB_PATH') or os.path.join(os.path.dirname(os.path.abspath(__file__)), '_lib',
+                                                          'libato.so')
 
 
 def declare(lib: ctypes.CDLL, prefix: str = 'ato') -> ctypes.CDLL:

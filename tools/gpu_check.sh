@@ -54,6 +54,14 @@ for s in $STEPS; do
                run kkt_chain_b512 200 python tools/bench_kkt.py --batch 512 --ordering chain --out "$OUT/kkt_chain_b512.json"
                run kkt_chain_b1 200 python tools/bench_kkt.py --batch 1 --ordering chain --out "$OUT/kkt_chain_b1.json" ;;
         ipmtests) run pytest_ipm 600 python -u -m pytest tests/test_gpu_batched_ipm.py -x -v --timeout 300 --timeout-method thread -p no:cacheprovider ;;
+        kktvar) for v in $(ls tools/diag/_lib/libato_*.so | grep -v stamps); do
+                   n=$(basename "$v" .so)
+                   for b in 512 1; do
+                       ATO_LIB_PATH=$PWD/$v run "kkt_${n}_b$b" 200 python tools/bench_kkt.py --batch $b --reps 7 --out "$OUT/kkt_${n}_b$b.json"
+                   done
+               done
+               for b in 512 1; do run kkt_cur_b$b 200 python tools/bench_kkt.py --batch $b --reps 7 --out "$OUT/kkt_cur_b$b.json"; done ;;
+        kktphase) ATO_LIB_PATH=$PWD/tools/diag/_lib/libato_stamps.so run kkt_phase 120 python tools/diag/kkt_phase.py ;;
         kkttests) run pytest_kkt 300 python -u -m pytest tests/test_gpu_kkt.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider ;;
         solve) run solve_b512 600 python tools/solve_batched.py --batch 512 --max-iter 200 --no-host --out "$OUT/solve_b512.json" ;;
         solveprof) run solveprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/solveprof" -o run -- \
