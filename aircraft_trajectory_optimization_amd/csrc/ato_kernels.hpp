@@ -177,8 +177,13 @@ __global__ __launch_bounds__(WAVE) void k_eval(ProbD p, int B, int layout, const
 
 // Interleaved layout, even B: every lane stays active (permlane swaps need the whole wave);
 // lanes past the end of the batch compute on the last instance and store nothing.
+#ifdef ATO_EVAL_WPE      // DIAGNOSTIC (tools/diag/kkt_variants.py): force an occupancy target
+#define ATO_EVAL_ATTR __attribute__((amdgpu_waves_per_eu(ATO_EVAL_WPE, ATO_EVAL_WPE)))
+#else
+#define ATO_EVAL_ATTR
+#endif
 template <class M, class T, int KS, bool WJ, bool WG, bool WF, bool FULL, int UMASK>
-__global__ __launch_bounds__(WAVE) void k_eval_paired(ProbD p, int B, int unit0, const T* __restrict__ w,
+__global__ __launch_bounds__(WAVE) ATO_EVAL_ATTR void k_eval_paired(ProbD p, int B, int unit0, const T* __restrict__ w,
                                                       T* __restrict__ g, T* __restrict__ J,
                                                       T* __restrict__ gf, T* __restrict__ fpart) {
     const int l = threadIdx.x;

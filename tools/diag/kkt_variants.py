@@ -1,10 +1,11 @@
 '''
-DIAGNOSTIC builds of the KKT kernels (not shipped): compile csrc/ato_kkt.hip with extra
+DIAGNOSTIC builds of libato.so (not shipped): recompile one translation unit with extra
 defines and link it with the library's other objects into tools/diag/_lib/libato_<name>.so,
-which tools/gpu_check.sh `kktvar` times with tools/bench_kkt.py (ATO_LIB_PATH).
+which tools/gpu_check.sh (`kktvar`, `evalvar`) times through ATO_LIB_PATH.
 
-    python tools/diag/kkt_variants.py NAME [-DFLAG ...]      (CPU: build only)
+    python tools/diag/kkt_variants.py NAME [--unit ato_kkt|ato_inst1|...] [-DFLAG ...]   (CPU)
 '''
+import argparse
 import glob
 import os
 import subprocess
@@ -15,14 +16,18 @@ ROOT = os.path.dirname(os.path.dirname(HERE))
 PKG = os.path.join(ROOT, 'aircraft_trajectory_optimization_amd')
 
 
-def build(name, flags):
+def build(name, unit, flags):
     from aircraft_trajectory_optimization_amd import build_native as bn
     bn.build(verbose=False)
     out = os.path.join(HERE, '_lib')
     os.makedirs(out, exist_ok=True)
-    obj = os.path.join(out, f'ato_kkt_{name}.o')
-    subprocess.run(['hipcc', *bn.FLAGS, *flags, '-c', os.path.join(PKG, 'csrc', 'ato_kkt.hip'), '-o', obj], check=True)
-    objs = [o for o in glob.glob(os.path.join(bn.OBJ, '*.o')) if not o.endswith('ato_kkt.o')] + [obj]
+    obj = os.path.join(out, f'{unit}_{name}.o')
+    if unit.startswith('ato_inst'):
+        src, extra = os.path.join(PKG, 'csrc', 'ato_inst.hip'), [f'-DATO_INST={unit[len("ato_inst"):]}']
+    else:
+        src, extra = os.path.join(PKG, 'csrc', unit + '.hip'), []
+    subprocess.run(['hipcc', *bn.FLAGS, *extra, *flags, '-c', src, '-o', obj], check=True)
+    objs = [o for o in glob.glob(os.path.join(bn.OBJ, '*.o')) if os.path.basename(o) != unit + '.o'] + [obj]
     lib = os.path.join(out, f'libato_{name}.so')
     subprocess.run(['hipcc', '-shared', '-fPIC', f'--offload-arch={bn.ARCH}', '-o', lib, *objs], check=True)
     os.remove(obj)
@@ -31,4 +36,8 @@ def build(name, flags):
 
 if __name__ == '__main__':
     sys.path.insert(0, ROOT)
-    build(sys.argv[1], sys.argv[2:])
+    ap = argparse.ArgumentParser()
+    ap.add_argument('name')
+    ap.add_argument('--unit', default='ato_kkt')
+    a, rest = ap.parse_known_args()
+    build(a.name, a.unit, rest)

@@ -61,6 +61,11 @@ for s in $STEPS; do
                    done
                done
                for b in 512 1; do run kkt_cur_b$b 200 python tools/bench_kkt.py --batch $b --reps 7 --out "$OUT/kkt_cur_b$b.json"; done ;;
+        evalvar) for v in $(ls tools/diag/_lib/libato_*.so | grep -v stamps); do
+                   n=$(basename "$v" .so)
+                   ATO_LIB_PATH=$PWD/$v run "bench_$n" 200 python bench.py --steps 50 --warmup 10 --no-cpu-baseline --no-solve
+               done
+               run bench_cur 200 python bench.py --steps 50 --warmup 10 --no-cpu-baseline --no-solve ;;
         kktphase) ATO_LIB_PATH=$PWD/tools/diag/_lib/libato_stamps.so run kkt_phase 120 python tools/diag/kkt_phase.py ;;
         kkttests) run pytest_kkt 300 python -u -m pytest tests/test_gpu_kkt.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider ;;
         solve) run solve_b512 600 python tools/solve_batched.py --batch 512 --max-iter 200 --no-host --out "$OUT/solve_b512.json" ;;
