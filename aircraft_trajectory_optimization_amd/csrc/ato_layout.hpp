@@ -10,6 +10,8 @@
 //     continuity (n >= 1)                           :460-490 / :1132-1163
 //     fixed-s rows (parametric)                     :1165-1181
 //   base loop closure (closed point mass)           :357-358, :492-514, :1183-1227
+//   open lines: initial and terminal rows           :359-361, :516-543, drone_raceline.py:110-148,
+//                                                   point_raceline.py:15-45
 //   gates                                           :907-918 / :986-1032
 //   obstacle-tube spheres                           :1293-1310
 //   drone loop closure (closed drone)               drone_raceline.py:150-156
@@ -113,6 +115,8 @@ ATO_HD void run_tail_seg(const ProbD& p, int kind, int index, const W& w, S& s, 
                 if (rk4) { seg_closure_base_rk4<M, T, KS>(p, grp, w, s); break; }
             seg_closure_base<M, T, KS>(p, w, s);
             break;
+        case TAIL_INITIAL: seg_boundary<M, T, KS>(p, 0, w, s); break;
+        case TAIL_TERMINAL: seg_boundary<M, T, KS>(p, 1, w, s); break;
         case TAIL_GATE: seg_gate<M, T, KS>(p, index, w, s); break;
         case TAIL_DRONE_CLOSURE:
             if constexpr (RK4)
@@ -279,7 +283,10 @@ struct Layout {
             return "unknown transcription";
         }
         if (d.closed && d.N < 2) return "closed problems need N >= 2";
-        if (!d.closed) return "open (non-periodic) racelines are not supported by this build";
+        if (!d.closed && d.transcription == ATO_TRANS_RK4)
+            return "open (non-periodic) RK4 racelines are not supported by this build";
+        if (!d.closed && d.frame == ATO_FRAME_PARAMETRIC && !d.global_r)
+            return "open parametric racelines need global_r (the relative attitude's R depends on s)";
         std::memset(&p, 0, sizeof(p));
         p.model = d.model;
         p.att = d.attitude;
@@ -494,6 +501,10 @@ struct Layout {
             if (param) ATO_TRY(node_segment<M>(SEG_SROWS, n, 0));
         }
         if (p.closed && !M::IS_DRONE) ATO_TRY(tail_segment<M>(TAIL_CLOSURE_BASE, 0));
+        if (!p.closed) {        // base_raceline.py:359-361
+            ATO_TRY(tail_segment<M>(TAIL_INITIAL, 0));
+            ATO_TRY(tail_segment<M>(TAIL_TERMINAL, 0));
+        }
         for (int g = 0; g < p.n_gates; ++g) ATO_TRY(tail_segment<M>(TAIL_GATE, g));
         if (p.has_spheres) {
             if (!param) return "obstacle spheres need the parametric frame";

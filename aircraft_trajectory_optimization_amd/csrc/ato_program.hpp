@@ -460,6 +460,166 @@ ATO_HD void seg_drone_closure(const ProbD& p, const W& w, S& s) {
     if (!M::PARAM) plain(0, T(0));
 }
 
+// open-line boundary rows (not closed): at the start (end = 0: Z[0,0], U[0,0]) and at the end
+// (end = 1: zF = op(sum_k D_k Z[N-1,k]), uF = sum_k D_k U[N-1,k]; _zF applies the continuity
+// operator), in the reference's order:
+//   |v_g|^2 <= 0                      BaseRaceline._enforce_initial/terminal_constraints
+//                                     (base_raceline.py:516-543), v_g = R v_b (f_vg)
+//   drone: R[:, 2] = (0, 0, 1), w_b = 0   DroneRaceline (drone_raceline.py:110-148)
+//   point mass: T_g[0] = T_g[1] = 0       PointRaceline (point_raceline.py:15-45), T_g = R u
+// R is the global rotation of the attitude (global frame, parametric with global_r); the point
+// mass has R = I there. (Parametric relative attitude, R = R_p(s) R(r), is rejected by the
+// layout: its R depends on s through the centreline spline.)
+template <class M, class T, int KS, class W, class S>
+ATO_HD void seg_boundary(const ProbD& p, int end, const W& w, S& s) {
+    constexpr int NZ = M::NZ, NU = M::NU, IR = M::IR, IV = M::IV;
+    const Cols<M> c{p.N, K1S(p)};
+    const int nb = end ? p.N - 1 : 0;
+    const int kn = end ? K1S(p) : 1;
+    T zb[NZ], u[NU];
+#pragma unroll
+    for (int i = 0; i < NZ; ++i) zb[i] = T(0);
+#pragma unroll
+    for (int i = 0; i < NU; ++i) u[i] = T(0);
+    for (int k = 0; k < kn; ++k) {
+        const T ck = end ? T(p.D[k]) : T(1);
+#pragma unroll
+        for (int i = 0; i < NZ; ++i) zb[i] += w(c.z(nb, k, i)) * ck;
+#pragma unroll
+        for (int i = 0; i < NU; ++i) u[i] += w(c.u(nb, k, i)) * ck;
+    }
+    T z[NZ];
+#pragma unroll
+    for (int i = 0; i < NZ; ++i) z[i] = zb[i];
+    T qh[4] = {T(0), T(0), T(0), T(0)}, iq = T(0);
+    const bool opq = M::IS_DRONE && M::HAS_QUAT && end;
+    if constexpr (M::IS_DRONE && M::HAS_QUAT) {
+        if (opq) {
+            qnormalize(zb + IR, qh, iq);
+#pragma unroll
+            for (int a = 0; a < 4; ++a) z[IR + a] = qh[a];
+        }
+    }
+    // one row: derivatives dz (after the operator, mask zm) and du (mask um), chained through
+    // op and the node coefficients; columns ascend node by node (z block, then u block)
+    auto emit = [&](const T* dz, const bool* zm, const T* du, const bool* um, T val, double lb, double ub) {
+        T dzb[NZ];
+        bool zmb[NZ];
+#pragma unroll
+        for (int m = 0; m < NZ; ++m) {
+            dzb[m] = dz[m];
+            zmb[m] = zm[m];
+        }
+        if constexpr (M::IS_DRONE && M::HAS_QUAT) {
+            if (opq) {
+                const bool anyq = zm[IR] || zm[IR + 1] || zm[IR + 2] || zm[IR + 3];
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    T acc = T(0);
+#pragma unroll
+                    for (int a = 0; a < 4; ++a) acc += dz[IR + a] * ((a == m ? T(1) : T(0)) - qh[a] * qh[m]) * iq;
+                    dzb[IR + m] = acc;
+                    zmb[IR + m] = anyq;
+                }
+            }
+        }
+        for (int k = 0; k < kn; ++k) {
+            const T ck = end ? T(p.D[k]) : T(1);
+#pragma unroll
+            for (int m = 0; m < NZ; ++m)
+                if (zmb[m]) s.jac(c.z(nb, k, m), dzb[m] * ck);
+#pragma unroll
+            for (int j = 0; j < NU; ++j)
+                if (um[j]) s.jac(c.u(nb, k, j), du[j] * ck);
+        }
+        s.row(val, lb, ub);
+    };
+    T dz[NZ], du[NU];
+    bool zm[NZ], um[NU];
+    auto clear = [&]() {
+#pragma unroll
+        for (int m = 0; m < NZ; ++m) {
+            dz[m] = T(0);
+            zm[m] = false;
+        }
+#pragma unroll
+        for (int j = 0; j < NU; ++j) {
+            du[j] = T(0);
+            um[j] = false;
+        }
+    };
+    if constexpr (M::IS_DRONE) {
+        using A = typename M::A;
+        constexpr int NR = M::NR, IW = M::IW;
+        T Ra[9];
+        A::R(z + IR, Ra);
+        const T* v = z + IV;
+        T vg[3];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) vg[a] = Ra[a * 3] * v[0] + Ra[a * 3 + 1] * v[1] + Ra[a * 3 + 2] * v[2];
+        // |v_g|^2 <= 0
+        clear();
+#pragma unroll
+        for (int m = 0; m < NR; ++m) {
+            T dRa[9];
+            A::dR(z + IR, Ra, m, dRa);
+            T acc = T(0);
+#pragma unroll
+            for (int a = 0; a < 3; ++a)
+                acc += vg[a] * (dRa[a * 3] * v[0] + dRa[a * 3 + 1] * v[1] + dRa[a * 3 + 2] * v[2]);
+            dz[IR + m] = T(2) * acc;
+            bool dep = false;
+            for (int a = 0; a < 3; ++a)
+                for (int b = 0; b < 3; ++b) dep = dep || A::R_dep(a, b, m);
+            zm[IR + m] = dep;
+        }
+#pragma unroll
+        for (int b = 0; b < 3; ++b) {
+            dz[IV + b] = T(2) * (vg[0] * Ra[b] + vg[1] * Ra[3 + b] + vg[2] * Ra[6 + b]);
+            zm[IV + b] = true;
+        }
+        emit(dz, zm, du, um, vg[0] * vg[0] + vg[1] * vg[1] + vg[2] * vg[2], -ATO_INF, 0.0);
+        // e3 = R[:, 2] = (0, 0, 1)
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            clear();
+#pragma unroll
+            for (int m = 0; m < NR; ++m) {
+                T dRa[9];
+                A::dR(z + IR, Ra, m, dRa);
+                dz[IR + m] = dRa[a * 3 + 2];
+                zm[IR + m] = A::R_dep(a, 2, m);
+            }
+            const double tgt = a == 2 ? 1.0 : 0.0;
+            emit(dz, zm, du, um, Ra[a * 3 + 2], tgt, tgt);
+        }
+        // w_b = 0
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            clear();
+            dz[IW + j] = T(1);
+            zm[IW + j] = true;
+            emit(dz, zm, du, um, z[IW + j], 0.0, 0.0);
+        }
+    } else {
+        // point mass with R = I: |v|^2 <= 0, T_g[0] = u[0], T_g[1] = u[1]
+        clear();
+#pragma unroll
+        for (int b = 0; b < 3; ++b) {
+            dz[IV + b] = T(2) * z[IV + b];
+            zm[IV + b] = true;
+        }
+        emit(dz, zm, du, um, z[IV] * z[IV] + z[IV + 1] * z[IV + 1] + z[IV + 2] * z[IV + 2], -ATO_INF, 0.0);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            clear();
+            du[j] = T(1);
+            um[j] = true;
+            emit(dz, zm, du, um, u[j], 0.0, 0.0);
+        }
+    }
+}
+
 // base loop closure used by the point-mass racelines (base_raceline.py:492-514, :1183-1227)
 template <class M, class T, int KS, class W, class S>
 ATO_HD void seg_closure_base(const ProbD& p, const W& w, S& s) {

@@ -8,6 +8,8 @@ Host-side precompute of the reference transcription (drone3d/raceline/base_racel
   * per-node geometry       f_param_terms(s_nk) feeding _eval_ode :963-970 (A7)
   * regularity mask         :1121-1129
   * gates                   _add_gate_constraints :907-918 (global), :986-1032 (parametric)
+  * open lines              the final gate at zF (global, :914-918); the initial / terminal rows
+                            (:359-361, :516-543) are laid out by the native library
   * initial guess + bounds  _build_decision_vector :670-750, :920-937, :1229-1251,
                             drone_raceline.py:158-274 (cold-start quaternion (1,0,0,0), F9)
 The row order, CSR pattern and lbg/ubg are produced by the native library from this spec.
@@ -73,6 +75,11 @@ class ProblemSpec:
             config.K = 0
         if self.param and not line.cleanly_closed and self.is_drone and not vehicle.global_r:
             raise NotImplementedError('Global orientation must be used for skewly closed centerlines')
+        if not config.closed and self.rk4:
+            raise NotImplementedError('open (non-periodic) RK4 racelines are not supported by this build')
+        if not config.closed and self.param and not vehicle.global_r:
+            raise NotImplementedError('open parametric racelines need global_r in this build (the relative '
+                                      'attitude rotation R_p(s) R depends on s through the centreline)')
         self.phase_len = 0
         if not self.param:
             x = np.array([config.gate_xi, config.gate_xj, config.gate_xk], dtype=float)
@@ -145,7 +152,11 @@ class ProblemSpec:
                           'coef': np.ones(1), 'xc': np.zeros(3), 'ey': np.zeros(3), 'en': np.zeros(3)})
                 gates.append(g)
             if not self.config.closed:
-                raise NotImplementedError('open global racelines are not implemented by this build')
+                # final gate at the end of the horizon (base_raceline.py:914-918)
+                g = self._gate_common(len(self.config.gate_xi) - 1)
+                g.update({'interval': self.N - 1, 'axial': 1, 'at_end': 1, 'n_coef': self.K1,
+                          'coef': self.D.copy(), 'xc': np.zeros(3), 'ey': np.zeros(3), 'en': np.zeros(3)})
+                gates.append(g)
             return gates
         fixed = self.config.fixed_gates
         if fixed is None:

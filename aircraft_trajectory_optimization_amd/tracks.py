@@ -26,24 +26,25 @@ OBST = np.array([[-5, -2.75, -0.66, 2.95, 8.67, 9.2, 1.57, -2.39, -4.7, -2.39, 4
 TRACKS = {'race': (RACE, 'square'), 'fig8': (FIG8, 'circle'), 'obstacles': (OBST, 'circle')}
 
 
-def make_line(track: str) -> SplineCenterline:
-    ''' closed spline centreline of a named scenario '''
+def make_line(track: str, closed: bool = True) -> SplineCenterline:
+    ''' spline centreline of a named scenario (closed as in the scripts, or open: the waypoints
+    as an open line, the demo of point_raceline.py:170-178) '''
     x, shape = TRACKS[track]
     cfg = SplineCenterlineConfig(x=np.array(x, float))
-    cfg.closed = True
+    cfg.closed = bool(closed)
     cfg.gate_shape = GateShape.SQUARE if shape == 'square' else GateShape.CIRCLE
     return SplineCenterline(cfg)
 
 
 def make_spec(track='race', model='drone', frame='parametric', N=50, K=4, use_quat=True, global_r=True,
               fix_gate_center=False, quat_flip=False, spheres=None, v0=1.0, h0=1, rk4=False,
-              euler_wraps=0.0) -> ProblemSpec:
+              euler_wraps=0.0, closed=True) -> ProblemSpec:
     ''' ProblemSpec of a scenario the way solve_util configures it (utils/solve_util.py:29-75) '''
-    line = make_line(track)
+    line = make_line(track, closed)
     if frame == 'parametric':
         cfg = ParametricRacelineConfig(verbose=False, N=N, K=K, v0=v0, h0=h0, use_rk4=rk4)
         cfg.closed = line.config.closed
-        cfg.fixed_gates = line.config.s[:-1]
+        cfg.fixed_gates = line.config.s[:-1] if line.config.closed else line.config.s
     else:
         cfg = GlobalRacelineConfig(verbose=False, N=N, K=K, v0=v0, h0=h0, use_rk4=rk4)
         cfg.closed = line.config.closed

@@ -12,6 +12,8 @@ hand-written Jacobians.
   interval constraints                 base_raceline.py:436-451, :1114-1130
   continuity                           base_raceline.py:460-490, :1132-1181
   closure                              base_raceline.py:492-514, :1183-1227; drone_raceline.py:47-104
+  open-line initial / terminal rows    base_raceline.py:359-361, :516-543; drone_raceline.py:110-148;
+                                       point_raceline.py:15-45
   gates                                base_raceline.py:545-595, :891-918, :986-1032
   obstacle spheres                     obstacles/mesh_obstacle.py:219-237
   cost                                 base_raceline.py:601-623
@@ -22,6 +24,11 @@ import numpy as np
 
 from oracle.ref_collocation import coefficients, intermediate
 from oracle import ref_models
+
+
+def mv_(R, x):
+    ''' (3,3[,B]) times (3,B) '''
+    return ref_models.mv(R, x)
 
 DRONE_DEFAULTS = dict(m=1.0, g=9.81, b1=0, b2=0, b3=0, collision_radius=0.3, I1=1e-3, I2=1e-3, I3=1.7e-3,
                       l=0.15, k=0.05, T_max=8.1, T_min=0.2, dT_max=20, dT_min=-20, bw1=1e-4, bw2=1e-4,
@@ -300,8 +307,18 @@ class RefNLP:
             return acc
 
         if not self.closed:
-            raise NotImplementedError('oracle covers closed racelines')
-        if self.model == 'point':
+            # _enforce_initial_constraints / _enforce_terminal_constraints, at Z[0,0] and _zF()
+            for z, u in ((Z[0][0], U[0][0]), (zF(), uF())):
+                vg, R = self._vg_R(z)
+                add(vg[0] * vg[0] + vg[1] * vg[1] + vg[2] * vg[2], -inf, 0.)    # vg.T @ vg
+                if self.model == 'drone':
+                    add([R[0, 2], R[1, 2], R[2, 2]], [0., 0., 1.], [0., 0., 1.])  # e3 = R[:, 2]
+                    add(z[-3:], 0., 0.)                                          # w_b
+                else:
+                    Tg = mv_(R, u)                                               # T = R @ Tb
+                    add(Tg[0], 0., 0.)
+                    add(Tg[1], 0., 0.)
+        elif self.model == 'point':
             # base / parametric _enforce_loop_closure
             z0, u0, zf = Z[0][0], U[0][0], zF()
             add(uF() - u0, 0., 0.)
@@ -343,6 +360,9 @@ class RefNLP:
         else:
             for gate_no, n in enumerate(range(0, N, self.gate_n_interval)):
                 self._fix_gate(add, Z[n][0][:3], gate_no, True)
+            if not self.closed:
+                # final gate (base_raceline.py:914-918)
+                self._fix_gate(add, zF()[:3], np.array(self.line.x).shape[1] - 1, True)
 
         if self.spheres is not None:
             for n in range(N):
@@ -351,8 +371,8 @@ class RefNLP:
                     z = Z[n][k]
                     add((z[1] - dy) ** 2 + (z[2] - dn) ** 2, -inf, max(r, 0) ** 2)
 
-        if self.model == 'drone':
-            # DroneRaceline._enforce_modified_loop_closure
+        if self.model == 'drone' and self.closed:
+            # DroneRaceline._enforce_modified_loop_closure (only for closed lines, drone_raceline.py:153)
             z0, u0 = Z[0][0], U[0][0]
             zf, uf = zF(), uF()
             zd = zf - z0
@@ -374,6 +394,17 @@ class RefNLP:
         if with_bounds:
             return out, np.array(lb, float), np.array(ub, float)
         return out
+
+    def _vg_R(self, z):
+        ''' f_vg and f_R of the model (global / global_r attitude; point mass: R = I) '''
+        if self.model == 'drone':
+            if not (self.frame == 'global' or self.global_r):
+                raise NotImplementedError('oracle: open lines with the relative attitude')
+            return ref_models.drone_vg_R(z, self.use_quat, self.frame, self.global_r)
+        if self.frame == 'parametric' and not self.global_r:
+            raise NotImplementedError('oracle: open lines with the relative attitude')
+        R = np.eye(3)
+        return z[3:6], R
 
     def _fix_gate(self, add, x_var, s, axial):
         ''' base_raceline.py:545-595 '''

@@ -148,7 +148,8 @@ def test_race_script_rk4(frame):
 
 HESS_CASES = [dict(track='race', N=4, K=2), dict(track='fig8', N=3, K=3, use_quat=False),
               dict(track='race', frame='global', N=7, K=2), dict(track='race', model='point', use_quat=False, N=4, K=2),
-              dict(track='race', N=7, K=2, rk4=True), dict(track='race', N=50, K=4)]
+              dict(track='race', N=7, K=2, rk4=True), dict(track='race', N=50, K=4),
+              dict(track='race', N=4, K=3, closed=False)]
 
 
 @pytest.mark.parametrize('cfg', HESS_CASES, ids=_id)

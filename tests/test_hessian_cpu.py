@@ -21,6 +21,9 @@ CASES = [
     dict(track='race', N=7, K=2, rk4=True),
     dict(track='race', frame='global', N=7, K=2, rk4=True),
     dict(track='fig8', N=4, K=3, quat_flip=True),
+    dict(track='race', N=4, K=3, closed=False),
+    dict(track='race', frame='global', N=6, K=2, use_quat=False, closed=False),
+    dict(track='race', model='point', use_quat=False, N=4, K=2, closed=False),
 ]
 
 

@@ -28,6 +28,12 @@ for _model, _frame, _quat, _gr in [('drone', 'parametric', True, True), ('drone'
                                    ('point', 'global', False, True)]:
     VARIANTS.append(dict(track='race', model=_model, frame=_frame, use_quat=_quat, global_r=_gr, N=7, K=2, rk4=True))
 VARIANTS.append(dict(track='fig8', N=8, K=2, rk4=True, quat_flip=True))
+# open (non-periodic) lines: initial / terminal rows instead of the closure, the final gate at zF
+for _model, _frame, _quat in [('drone', 'parametric', True), ('drone', 'parametric', False),
+                              ('drone', 'global', True), ('drone', 'global', False),
+                              ('point', 'parametric', False), ('point', 'global', False)]:
+    VARIANTS.append(dict(track='race', model=_model, frame=_frame, use_quat=_quat, closed=False,
+                         N=6 if _frame == 'global' else 4, K=3))
 
 
 def _id(c):

@@ -78,3 +78,23 @@ def test_ipm_drone_with_point_mass_warm_start():
     J = sp.csr_matrix((jv, (jr, ev.j_col)), shape=(ev.ng, ev.nw))
     dual = gf + J.T @ res.lam_g + res.lam_x
     assert np.abs(dual).max() <= 1e-5 * max(1.0, np.abs(gf).max())
+
+
+def test_ipm_open_line_point_mass_starts_and_ends_at_rest():
+    ''' open (non-periodic) line (A14): the point mass starts and ends at rest with vertical thrust
+    (base_raceline.py:516-543, point_raceline.py:15-45) and the solve reaches a KKT point '''
+    spec = product_spec(track='race', model='point', use_quat=False, N=10, K=3, closed=False)
+    ev = HostEvaluator(spec)
+    res = InteriorPointSolver(ev, spec.lbw, spec.ubw, ev.lbg, ev.ubg, IPMOptions(max_iter=300)).solve(spec.w0)
+    assert res.status == 'optimal', res.status
+    f, g, gf, jv = ev.eval(res.x)
+    viol = np.maximum(ev.lbg - g, 0) + np.maximum(g - ev.ubg, 0)
+    assert viol.max() <= 1e-6
+    jr = np.repeat(np.arange(ev.ng), np.diff(ev.j_row_ptr))
+    J = sp.csr_matrix((jv, (jr, ev.j_col)), shape=(ev.ng, ev.nw))
+    dual = gf + J.T @ res.lam_g + res.lam_x
+    assert np.abs(dual).max() <= 1e-5 * max(1.0, np.abs(gf).max())
+    v0 = res.x[spec.col_z(0, 0, 3):spec.col_z(0, 0, 6)]
+    assert np.linalg.norm(v0) <= 1e-3                    # |v_g|^2 <= 0 at the start
+    u0 = res.x[spec.col_z(0, 0, 6):spec.col_z(0, 0, 8)]
+    assert np.abs(u0).max() <= 1e-6                       # horizontal thrust components
