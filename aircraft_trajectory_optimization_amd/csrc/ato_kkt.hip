@@ -75,7 +75,10 @@ int fail(int code, const std::string& m) {
 constexpr int FT = 512;                   // factor threads per (front, instance) (16 x 32 grid)
 constexpr int ST = 256;                   // solve threads per (front, instance)
 constexpr int EPT = 8;                    // entries per thread and front (<= 4096 per front)
-constexpr int CH = 4096;                  // doubles per ring chunk of the solve (2 x 32 KB LDS ring)
+#ifndef ATO_KKT_CH
+#define ATO_KKT_CH 1024     // 16 KB ring: 5 solve workgroups per CU (64 KB: 2); B = 512 solve 11.1 -> 4.2 ms
+#endif
+constexpr int CH = ATO_KKT_CH;            // doubles per ring chunk of the solve (2 x CH x 8 B LDS ring)
 constexpr int CPT = CH / ST;              // chunk doubles per thread
 constexpr int MAXT = 8;                   // strips per front in ent_ptr
 constexpr double BK_ALPHA = 0.64038820320220756872767623199676;   // (1 + sqrt(17)) / 8
