@@ -56,7 +56,7 @@ struct ato_kkt {
 #ifdef ATO_KKT_STAMPS
 // DIAGNOSTIC build only (tools/diag/kkt_phase.py): shader-clock phase totals of the workgroup
 // (front 0 = the first interval leaf, instance 0) of the factorisation, thread 0
-__device__ unsigned long long g_kkt_stamps[8];
+__device__ unsigned long long g_kkt_stamps[16];
 #endif
 
 namespace {
@@ -168,9 +168,9 @@ __device__ __forceinline__ unsigned long long kstamp() {
     __builtin_amdgcn_sched_barrier(0);
     return t;
 }
-#define KST_DECL(on_) unsigned long long kst_acc[6] = {0, 0, 0, 0, 0, 0}, kst_last = kstamp(); const bool kst_on = (on_);
+#define KST_DECL(on_) unsigned long long kst_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, kst_last = kstamp(); const bool kst_on = (on_);
 #define KST(i) do { if (kst_on) { const unsigned long long t_ = kstamp(); kst_acc[i] += t_ - kst_last; kst_last = t_; } } while (0)
-#define KST_DUMP(n_) do { if (kst_on && threadIdx.x == 0) { for (int i_ = 0; i_ < 6; ++i_) g_kkt_stamps[i_] = kst_acc[i_]; g_kkt_stamps[6] = (n_); } } while (0)
+#define KST_DUMP(n_) do { if (kst_on && threadIdx.x == 0) { for (int i_ = 0; i_ < 10; ++i_) g_kkt_stamps[i_] = kst_acc[i_]; g_kkt_stamps[15] = (n_); } } while (0)
 #else
 #define KST_DECL(on_)
 #define KST(i)
@@ -426,6 +426,7 @@ __global__ __launch_bounds__(FT) void k_front_factor(Plan P, Vals V, int f0, int
             if (i < own && i != k && lvq[q]) key = max(key, mag_key(cv[q], i));
         }
         key = wave_max_u32(key);
+        KST(5);                  // column read, magnitude keys, DPP max
         const int r = key ? 511 - (int)(key & 0x1FFu) : -1;
         const double akk = lane_pick<NQ>(cv, k);
         const double lam = r >= 0 ? fabs(lane_pick<NQ>(cv, r)) : 0.0;
@@ -488,6 +489,7 @@ __global__ __launch_bounds__(FT) void k_front_factor(Plan P, Vals V, int f0, int
             else if (A00 + A11 > 0.0) npos += 2;
             else nneg += 2;
         }
+        KST(6);                  // pivot inverse, inertia
         const int nlive = live.count();
         const int ncol = type == 1 ? 2 : 1;
         {
@@ -501,6 +503,7 @@ __global__ __launch_bounds__(FT) void k_front_factor(Plan P, Vals V, int f0, int
                 lvq[q] = lvq[q] && i != e1p && i != e2p;
             }
         }
+        KST(7);                  // live-set bookkeeping
         if (tid == 0) {
             pv[steps] = make_int2((type == 1 ? k : p) | (type << 16), type == 1 ? r : -1);
             dv[3 * steps + 0] = i00;
@@ -529,6 +532,7 @@ __global__ __launch_bounds__(FT) void k_front_factor(Plan P, Vals V, int f0, int
                 }
             }
         }
+        KST(8);                  // record, row factors (permlane broadcast)
         if (lvt) {
             // position tid = row 32 tj + ti of the thread: its factor entries are l0[tj], l1[tj]
             double v0 = l0[0];
@@ -1076,7 +1080,7 @@ extern "C" {
 
 #ifdef ATO_KKT_STAMPS
 int ato_kkt_diag_stamps(unsigned long long* out) {
-    KKT_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_kkt_stamps), sizeof(unsigned long long) * 8));
+    KKT_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_kkt_stamps), sizeof(unsigned long long) * 16));
     return ATO_OK;
 }
 #endif

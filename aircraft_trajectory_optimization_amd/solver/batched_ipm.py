@@ -165,6 +165,47 @@ def _idx(mask: torch.Tensor) -> np.ndarray:
     return torch.nonzero(mask).reshape(-1).cpu().numpy().astype(np.int32)
 
 
+def _structure(ev, dev) -> Dict[str, torch.Tensor]:
+    ''' index tensors of the sparse products (structure only), cached on the evaluator (or on the
+    shared structure holder of the restoration evaluators) '''
+    holder = getattr(ev, 'structure_holder', ev)
+    cache = getattr(holder, '_ipm_structure', None)
+    if cache is not None and cache['_dev'] == str(dev):
+        return {k: v for k, v in cache.items() if k != '_dev'}
+    n, m = ev.n, ev.m
+
+    def t(a, dt=torch.float64):
+        return torch.as_tensor(np.asarray(a), dtype=dt, device=dev)
+
+    d = {}
+    d['jr'] = t(np.repeat(np.arange(m), np.diff(ev.j_row_ptr)), torch.long)
+    d['jc'] = t(np.asarray(ev.j_col), torch.long)
+    hr = np.repeat(np.arange(n), np.diff(ev.h_row_ptr))
+    hc = np.asarray(ev.h_col)
+    d['hr'], d['hc'] = t(hr, torch.long), t(hc, torch.long)
+    off = np.nonzero(hr != hc)[0]
+    d['hoff'], d['hr_off'], d['hc_off'] = t(off, torch.long), t(hr[off], torch.long), t(hc[off], torch.long)
+    # deterministic sparse products: entries grouped by output row, summed in a fixed order
+    # per segment (segment_reduce), not by atomics (index_add_), so that a batched solve is
+    # reproducible run to run
+    jr_np, jc_np = np.repeat(np.arange(m), np.diff(ev.j_row_ptr)), np.asarray(ev.j_col)
+    d['j_len'] = t(np.diff(ev.j_row_ptr), torch.long)
+    pc = np.argsort(jc_np, kind='stable')
+    d['jt_src'], d['jt_row'] = t(pc, torch.long), t(jr_np[pc], torch.long)
+    d['jt_len'] = t(np.bincount(jc_np, minlength=n), torch.long)
+    w_row = np.concatenate([hr, hc[off]])
+    w_col = np.concatenate([hc, hr[off]])
+    w_src = np.concatenate([np.arange(len(hr)), off])
+    pw = np.argsort(w_row, kind='stable')
+    d['w_src'], d['w_col'] = t(w_src[pw], torch.long), t(w_col[pw], torch.long)
+    d['w_len'] = t(np.bincount(w_row, minlength=n), torch.long)
+    try:
+        holder._ipm_structure = {**d, '_dev': str(dev)}
+    except AttributeError:
+        pass
+    return d
+
+
 class BatchedInteriorPoint:
     def __init__(self, ev, kkt, lbx, ubx, options: Optional[IPMOptions] = None):
         self.ev, self.kkt = ev, kkt
@@ -194,27 +235,8 @@ class BatchedInteriorPoint:
         self.mi = int((~eq).sum())
         self.lbg0 = t(np.where(lbg <= -INF, -np.inf, lbg))
         self.ubg0 = t(np.where(ubg >= INF, np.inf, ubg))
-        self.jr = t(np.repeat(np.arange(m), np.diff(ev.j_row_ptr)), torch.long)
-        self.jc = t(np.asarray(ev.j_col), torch.long)
-        hr = np.repeat(np.arange(n), np.diff(ev.h_row_ptr))
-        hc = np.asarray(ev.h_col)
-        self.hr, self.hc = t(hr, torch.long), t(hc, torch.long)
-        off = np.nonzero(hr != hc)[0]
-        self.hoff, self.hr_off, self.hc_off = t(off, torch.long), t(hr[off], torch.long), t(hc[off], torch.long)
-        # deterministic sparse products: entries grouped by output row, summed in a fixed order
-        # per segment (segment_reduce), not by atomics (index_add_), so that a batched solve is
-        # reproducible run to run
-        jr_np, jc_np = np.repeat(np.arange(m), np.diff(ev.j_row_ptr)), np.asarray(ev.j_col)
-        self.j_len = t(np.diff(ev.j_row_ptr), torch.long)
-        pc = np.argsort(jc_np, kind='stable')
-        self.jt_src, self.jt_row = t(pc, torch.long), t(jr_np[pc], torch.long)
-        self.jt_len = t(np.bincount(jc_np, minlength=n), torch.long)
-        w_row = np.concatenate([hr, hc[off]])
-        w_col = np.concatenate([hc, hr[off]])
-        w_src = np.concatenate([np.arange(len(hr)), off])
-        pw = np.argsort(w_row, kind='stable')
-        self.w_src, self.w_col = t(w_src[pw], torch.long), t(w_col[pw], torch.long)
-        self.w_len = t(np.bincount(w_row, minlength=n), torch.long)
+        for k_, v_ in _structure(ev, dev).items():
+            setattr(self, k_, v_)
         self.stats = {'factorizations': 0, 'solves': 0, 'evals': 0, 'hess': 0}
         self.laps = _Laps(dev)
 
@@ -806,8 +828,10 @@ class BatchedInteriorPoint:
         cols = (lambda t: t.index_select(t.dim() - 1, sel).contiguous()) if compact else (lambda t: t)  # noqa: E731
         ev_r = self.ev.subset(len(sel)) if compact else self.ev
         kkt_r = self.kkt.view(len(sel)) if compact else self.kkt
+        if getattr(self, '_resto_structure', None) is None:
+            self._resto_structure = _RestorationStructure(ev_r)
         rev = _RestorationEvaluator(ev_r, cols(self.sg), cols(x), cols(torch.sqrt(mu)), rho, cols(self.lbg_s),
-                                    cols(self.ubg_s))
+                                    cols(self.ubg_s), self._resto_structure)
         Br = rev.batch
         Xr0 = torch.cat([cols(x), cols(pp), cols(nn)])
         lbx = torch.cat([cols(self.lbx0), torch.zeros((2 * m, Br), dtype=torch.float64, device=dev)])
@@ -852,21 +876,12 @@ class BatchedInteriorPoint:
         return torch.minimum(torch.maximum(xr, self.xL), self.xU), ok
 
 
-class _RestorationEvaluator:
-    '''
-    Restoration NLP over (x, p, n) on the scaled rows of the base evaluator, per instance
-    (solver/ipm.py _RestorationEvaluator on [element][instance] tensors):
-        min  rho sum(p + n) + zeta/2 |D_R (x - x_r)|^2   s.t.  sg * g(x) - p + n  in scaled bounds
-    Jacobian rows [sg_i J_i, -1 (p_i), +1 (n_i)]; Hessian = base constraint Hessian (sigma = 0)
-    plus zeta D_R^2 on the x diagonal (pattern: base pattern plus the full x diagonal).
-    '''
+class _RestorationStructure:
+    ''' sparsity of the restoration NLP (structure only; built once per outer solver) '''
 
-    def __init__(self, base, sg, x_ref, zeta, rho, lbg_s, ubg_s):
-        n, m, B = base.n, base.m, base.batch
+    def __init__(self, base):
+        n, m = base.n, base.m
         dev = base.device
-        self.base, self.sg, self.x_ref, self.zeta, self.rho = base, sg, x_ref.clone(), zeta, rho
-        self.n0, self.m, self.n, self.batch, self.device = n, m, n + 2 * m, B, dev
-        self.dr2 = torch.clamp(1.0 / torch.clamp(self.x_ref.abs(), min=1e-300), max=1.0) ** 2
         cnt = np.diff(np.asarray(base.j_row_ptr))
         self.j_row_ptr = np.concatenate([[0], np.cumsum(cnt + 2)]).astype(np.int64)
         rows = np.repeat(np.arange(m), cnt)
@@ -891,6 +906,29 @@ class _RestorationEvaluator:
         self.h_map = torch.as_tensor(np.searchsorted(keys, hr * n + hc), device=dev)
         self.h_diag = torch.as_tensor(np.searchsorted(keys, dkeys), device=dev)
         self.diag_new = torch.as_tensor(~np.isin(dkeys, hr * n + hc), device=dev)
+
+
+class _RestorationEvaluator:
+    '''
+    Restoration NLP over (x, p, n) on the scaled rows of the base evaluator, per instance
+    (solver/ipm.py _RestorationEvaluator on [element][instance] tensors):
+        min  rho sum(p + n) + zeta/2 |D_R (x - x_r)|^2   s.t.  sg * g(x) - p + n  in scaled bounds
+    Jacobian rows [sg_i J_i, -1 (p_i), +1 (n_i)]; Hessian = base constraint Hessian (sigma = 0)
+    plus zeta D_R^2 on the x diagonal (pattern: base pattern plus the full x diagonal).
+    '''
+
+    def __init__(self, base, sg, x_ref, zeta, rho, lbg_s, ubg_s, structure: Optional['_RestorationStructure'] = None):
+        n, m, B = base.n, base.m, base.batch
+        dev = base.device
+        self.base, self.sg, self.x_ref, self.zeta, self.rho = base, sg, x_ref.clone(), zeta, rho
+        self.n0, self.m, self.n, self.batch, self.device = n, m, n + 2 * m, B, dev
+        self.dr2 = torch.clamp(1.0 / torch.clamp(self.x_ref.abs(), min=1e-300), max=1.0) ** 2
+        st = structure if structure is not None else _RestorationStructure(base)
+        self.structure_holder = st            # _structure() caches the solver's index tensors there
+        self.j_row_ptr, self.j_col, self.pos_orig, self.pe, self.jrow_orig = \
+            st.j_row_ptr, st.j_col, st.pos_orig, st.pe, st.jrow_orig
+        self.h_row_ptr, self.h_col, self.nnz_h = st.h_row_ptr, st.h_col, st.nnz_h
+        self.h_map, self.h_diag, self.diag_new = st.h_map, st.h_diag, st.diag_new
         self.lbg, self.ubg = lbg_s, ubg_s
 
     def eval(self, X):

@@ -44,14 +44,16 @@ def main():
     torch.cuda.synchronize()
     lib = native.load()
     lib.ato_kkt_diag_stamps.argtypes = [ctypes.c_void_p]
-    out = (ctypes.c_ulonglong * 8)()
+    out = (ctypes.c_ulonglong * 16)()
     assert lib.ato_kkt_diag_stamps(out) == 0
     v = list(out)
-    steps = max(int(v[6]), 1)
-    names = ['assembly', 'extract+barrier', 'search+decide', 'inverse+record+store', 'update']
-    res = {n: v[i] for i, n in enumerate(names)}
+    steps = max(int(v[15]), 1)
+    names = {0: 'assembly', 1: 'extract+barrier', 5: 'column read+keys+DPP max', 2: 'pivot picks+decision',
+             6: 'inverse+inertia', 7: 'live bookkeeping', 8: 'record+row factors', 3: 'factor-column store',
+             4: 'update'}
+    res = {n: v[i] for i, n in names.items()}
     res['steps'] = steps
-    res['per_step_cycles'] = {n: v[i] / steps for i, n in enumerate(names[1:], start=1)}
+    res['per_step_cycles'] = {n: v[i] / steps for i, n in names.items() if i != 0}
     print(json.dumps(res))
 
 
