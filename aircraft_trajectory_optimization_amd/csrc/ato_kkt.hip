@@ -55,7 +55,10 @@ struct ato_kkt {
 
 #ifdef ATO_KKT_STAMPS
 // DIAGNOSTIC build only (tools/diag/kkt_phase.py): shader-clock phase totals of the workgroup
-// (front 0 = the first interval leaf, instance 0) of the factorisation, thread 0
+// (front ATO_KKT_STAMP_FRONT, instance 0) of the factorisation, thread 0
+#ifndef ATO_KKT_STAMP_FRONT
+#define ATO_KKT_STAMP_FRONT 0
+#endif
 __device__ unsigned long long g_kkt_stamps[16];
 #endif
 
@@ -228,6 +231,15 @@ __device__ __forceinline__ unsigned mag_key(double v, int i) {
 
 constexpr int slot(int I, int J) { return I * (I + 1) / 2 + J; }
 
+// 1 / d by the hardware reciprocal and two Newton steps (a few ulp; four dependent ops instead of
+// the ten of an IEEE division on the pivot chain). d is never 0 here: Bunch-Kaufman takes a 1x1
+// pivot only with |d| >= alpha lambda > 0, and a 2x2 only with det <= (alpha^2 - 1) lambda^2 < 0.
+__device__ __forceinline__ double rcp_nr(double d) {
+    double r = __builtin_amdgcn_rcp(d);
+    r = fma(fma(-d, r, 1.0), r, r);
+    return fma(fma(-d, r, 1.0), r, r);
+}
+
 // rows 32I + ti (I < T) of a column held as v[q] = c[lane + 64q]: lanes 0-31 of v[q] hold tile 2q,
 // lanes 32-63 tile 2q + 1, and a self v_permlane32_swap broadcasts each half to the whole wave
 // (no LDS round trip for the row factors of the Schur update)
@@ -328,7 +340,7 @@ __global__ __launch_bounds__(FT) void k_front_factor(Plan P, Vals V, int f0, int
     double* dv = dinv + ((long long)b * P.dim + P.piv_off[f]) * 3;
     int npos = 0, nneg = 0, nzero = 0;
     long long loff = 0;                          // running offset in the front's column stream
-    KST_DECL(f == 0 && blockIdx.y == 0)
+    KST_DECL(f == ATO_KKT_STAMP_FRONT && blockIdx.y == 0)
 
     // ---- original entries (positions and values) into registers
     const int e0 = P.ent_ptr[f * MAXT], e1 = P.ent_ptr[(f + 1) * MAXT];
@@ -473,13 +485,13 @@ __global__ __launch_bounds__(FT) void k_front_factor(Plan P, Vals V, int f0, int
             ++nzero;
         } else if (type == 0) {
             const double d = use_r ? arr : akk;
-            i00 = 1.0 / d;
+            i00 = rcp_nr(d);
             live.clear(p);
             if (d > 0.0) ++npos; else ++nneg;
         } else {
             const double A00 = akk, A01 = lane_pick<NQ>(cv, r), A11 = arr;
             const double det = A00 * A11 - A01 * A01;
-            const double rdet = 1.0 / det;
+            const double rdet = rcp_nr(det);
             i00 = A11 * rdet;
             i01 = -A01 * rdet;
             i11 = A00 * rdet;

@@ -30,7 +30,9 @@ diagonal by interval, almost every row touches one interval or two neighbouring 
            leaf blocks stay non-singular. Separators are joined by recursive bisection, the
            border rows (loop closure, equal step sizes: rows spanning non-neighbouring
            intervals) form the root. The critical path of one factorisation is one leaf plus
-           log2(N) separators instead of the whole chain.
+           log2(N) separators instead of the whole chain. Variable / row pairs isolated inside an
+           interval (the input rates and their defect rows) form a child front of the leaf
+           (split_pairs), which shrinks the leaf block.
   'chain'  the staged elimination of solver/kkt_blocks.py: front s owns interval s's variables
            and rows (a row touching two intervals joins the later one), its child is front s-1,
            the border is the root. One front per level.
@@ -134,7 +136,7 @@ def _fronts_chain(n, var_stage, lo, hi):
     return own, children
 
 
-def _fronts_nd(n, var_stage, lo, hi, j_row_ptr, j_col):
+def _fronts_nd(n, var_stage, lo, hi, j_row_ptr, j_col, split_pairs=True):
     S = int(var_stage.max()) + 1
     m = len(lo)
     link = hi - lo == 1
@@ -147,17 +149,47 @@ def _fronts_nd(n, var_stage, lo, hi, j_row_ptr, j_col):
     anchor[jc[sel]] = True
     own: List[np.ndarray] = []
     children: List[List[int]] = []
-    for s in range(S):                          # leaves 0 .. S-1
-        own.append(np.concatenate([np.nonzero((var_stage == s) & ~anchor)[0],
-                                   n + np.nonzero(interior & (lo == s))[0]]))
-        children.append([])
+    # isolated pairs: an interior variable whose only Jacobian entry is in an interior row of its
+    # interval (the input rates dU_k and their defect rows dU_k - sum_j C_jk U_j / h: the row is the
+    # variable's only coupling besides its Hessian diagonal and h). The pairs of an interval form a
+    # child front of the leaf: eliminated first, they leave a smaller leaf block (fewer register
+    # tiles, cheaper pivot steps) and a short chain of small-front steps instead
+    pre = [np.zeros(0, np.int64) for _ in range(S)]
+    if split_pairs:
+        cnt = np.bincount(jc, minlength=n)
+        used = np.zeros(m, bool)
+        pairs: List[List[int]] = [[] for _ in range(S)]
+        for e in np.nonzero(cnt[jc] == 1)[0]:
+            v, r = int(jc[e]), int(jr[e])
+            st = int(var_stage[v])
+            if anchor[v] or used[r] or not (interior[r] and lo[r] == st):
+                continue
+            used[r] = True
+            pairs[st].append((v, r))
+        for st in range(S):
+            if pairs[st]:
+                pre[st] = np.concatenate([np.sort([v for v, _ in pairs[st]]), n + np.sort([r for _, r in pairs[st]])])
+    pre_id = [-1] * S
+    for st in range(S):                          # pre-fronts first (children precede parents)
+        if len(pre[st]):
+            pre_id[st] = len(own)
+            own.append(pre[st])
+            children.append([])
+    leaf_id = []
+    for st in range(S):                          # leaves
+        inner = np.concatenate([np.nonzero((var_stage == st) & ~anchor)[0], n + np.nonzero(interior & (lo == st))[0]])
+        if len(pre[st]):
+            inner = inner[~np.isin(inner, pre[st])]
+        leaf_id.append(len(own))
+        own.append(inner)
+        children.append([pre_id[st]] if pre_id[st] >= 0 else [])
 
     def sep(j):
         return np.concatenate([np.nonzero((var_stage == j) & anchor)[0], n + np.nonzero(link & (hi == j))[0]])
 
     def build(a, b):                            # subtree over intervals a..b (boundaries a+1..b)
         if a == b:
-            return a
+            return leaf_id[a]
         j = (a + b + 1) // 2
         left, right = build(a, j - 1), build(j, b)
         own.append(sep(j))
@@ -172,7 +204,8 @@ def _fronts_nd(n, var_stage, lo, hi, j_row_ptr, j_col):
     return own, children
 
 
-def build_plan(n: int, m: int, var_stage, j_row_ptr, j_col, h_row_ptr, h_col, ordering: str = 'nd') -> KKTPlan:
+def build_plan(n: int, m: int, var_stage, j_row_ptr, j_col, h_row_ptr, h_col, ordering: str = 'nd',
+               split_pairs: bool = True) -> KKTPlan:
     var_stage = np.asarray(var_stage, np.int64)
     j_row_ptr = np.asarray(j_row_ptr, np.int64)
     j_col = np.asarray(j_col, np.int64)
@@ -184,7 +217,7 @@ def build_plan(n: int, m: int, var_stage, j_row_ptr, j_col, h_row_ptr, h_col, or
         raise ValueError('Hessian couples different stages; the staged KKT does not apply')
     lo, hi = row_span(n, m, var_stage, j_row_ptr, j_col)
     if ordering == 'nd':
-        own, children = _fronts_nd(n, var_stage, lo, hi, j_row_ptr, j_col)
+        own, children = _fronts_nd(n, var_stage, lo, hi, j_row_ptr, j_col, split_pairs)
     elif ordering == 'chain':
         own, children = _fronts_chain(n, var_stage, lo, hi)
     else:

@@ -55,9 +55,15 @@ def test_plan_racetrack_full_size_fits_device_tiles():
     spec = product_spec(track='race', N=50, K=4)
     ev = HostEvaluator(spec)
     plan = build_plan(ev.nw, ev.ng, var_stages(spec), ev.j_row_ptr, ev.j_col, ev.h_row_ptr, ev.h_col)
-    # nested dissection: 50 interval leaves, 49 separators, the border; depth 1 + ceil(log2 50) + 1
-    assert plan.n_fronts == 100 and plan.n_levels == 8
-    assert plan.level_ptr[1] == 50 and plan.level_tiles[0] == 7 and plan.level_tiles[1:].max() <= 4
+    # nested dissection: 50 input-rate pair fronts (40 positions: dU_k and their defect rows) under
+    # 50 interval leaves, 49 separators, the border; depth 2 + ceil(log2 50) + 1
+    assert plan.n_fronts == 150 and plan.n_levels == 9
+    assert plan.level_ptr[1] == 50 and plan.level_ptr[2] == 100
+    assert (plan.n_own[:50] == 40).all() and plan.level_tiles[0] == 2 and plan.level_tiles[1] == 6
+    assert plan.level_tiles[2:].max() <= 4
+    plain = build_plan(ev.nw, ev.ng, var_stages(spec), ev.j_row_ptr, ev.j_col, ev.h_row_ptr, ev.h_col,
+                       split_pairs=False)
+    assert plain.n_fronts == 100 and plain.n_levels == 8 and plain.level_tiles[0] == 7
     assert plan.max_block <= 256
     assert (np.diff(plan.ent_ptr[::8]) <= 4096).all()
     chain = build_plan(ev.nw, ev.ng, var_stages(spec), ev.j_row_ptr, ev.j_col, ev.h_row_ptr, ev.h_col, 'chain')
