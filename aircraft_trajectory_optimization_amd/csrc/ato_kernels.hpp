@@ -78,6 +78,21 @@ __device__ __forceinline__ void swap_halves<float>(float& a, float& b) {
 template <class T>
 struct Pair2 { T x, y; };
 
+#ifdef ATO_EVAL_NT       // DIAGNOSTIC (tools/diag/kkt_variants.py): streaming (nontemporal) J / g stores
+template <class T>
+__device__ __forceinline__ void st_pair(char* p, T a, T b) {
+    typedef T v2 __attribute__((ext_vector_type(2)));
+    __builtin_nontemporal_store(v2{a, b}, reinterpret_cast<v2*>(p));
+}
+template <class T>
+__device__ __forceinline__ void st_one(char* p, T a) { __builtin_nontemporal_store(a, reinterpret_cast<T*>(p)); }
+#else
+template <class T>
+__device__ __forceinline__ void st_pair(char* p, T a, T b) { *reinterpret_cast<Pair2<T>*>(p) = Pair2<T>{a, b}; }
+template <class T>
+__device__ __forceinline__ void st_one(char* p, T a) { *reinterpret_cast<T*>(p) = a; }
+#endif
+
 template <class T, bool WJ, bool WG, bool FULL>
 struct DevSinkPaired {
     const char* Jc;     // (char*) (J + chunk base): uniform
@@ -91,7 +106,7 @@ struct DevSinkPaired {
     T pend;
     bool odd;
     __device__ __forceinline__ void flush() {
-        if (WJ && odd && (FULL || svalid)) *reinterpret_cast<T*>(Jr - Bb + self_off) = pend;
+        if (WJ && odd && (FULL || svalid)) st_one(Jr - Bb + self_off, pend);
         odd = false;
     }
     __device__ __forceinline__ void begin(int row0, int nnz0) {
@@ -108,14 +123,14 @@ struct DevSinkPaired {
             } else {
                 T a = pend, b2 = v;
                 swap_halves(a, b2);
-                if (FULL || pvalid) *reinterpret_cast<Pair2<T>*>(Jr - Bb + pair_off) = Pair2<T>{a, b2};
+                if (FULL || pvalid) st_pair(Jr - Bb + pair_off, a, b2);
                 odd = false;
             }
         }
         Jr += Bb;
     }
     __device__ __forceinline__ void row(T gv, double, double) {
-        if (WG && (FULL || svalid)) *reinterpret_cast<T*>(gr + self_off) = gv;
+        if (WG && (FULL || svalid)) st_one(gr + self_off, gv);
         gr += Bb;
     }
     // an entry another work unit writes: the pending entry (if any) is stored alone

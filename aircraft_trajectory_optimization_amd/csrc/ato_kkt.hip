@@ -4,7 +4,7 @@
 // independent instances; the plan tables (fronts, levels, extend-add maps) come from
 // solver/kkt_plan.py.
 //
-// Factor (k_front_factor<T>): one 512-thread workgroup per (front, instance) of a level. The
+// Factor (k_front_factor_w<T, W>): one 512-thread workgroup per (front, instance) of a level. The
 // front's block (<= 32*T positions) lives in REGISTERS: thread (ti, tj) = (tid % 32, tid / 32)
 // holds A[32 I + ti][32 J + tj] and A[32 I + ti][32 J + 16 + tj] for every lower tile J <= I
 // (T(T+1) doubles). The original entries are assembled through a 32-row LDS strip per tile
@@ -240,21 +240,6 @@ __device__ __forceinline__ double rcp_nr(double d) {
     return fma(fma(-d, r, 1.0), r, r);
 }
 
-// rows 32I + ti (I < T) of a column held as v[q] = c[lane + 64q]: lanes 0-31 of v[q] hold tile 2q,
-// lanes 32-63 tile 2q + 1, and a self v_permlane32_swap broadcasts each half to the whole wave
-// (no LDS round trip for the row factors of the Schur update)
-template <int T, int NQ>
-__device__ __forceinline__ void column_rows(const double (&v)[NQ], double (&x)[T]) {
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-        const uint2 u = __builtin_bit_cast(uint2, v[q]);
-        const auto lo = __builtin_amdgcn_permlane32_swap(u.x, u.x, false, false);
-        const auto hi = __builtin_amdgcn_permlane32_swap(u.y, u.y, false, false);
-        if (2 * q < T) x[2 * q] = __builtin_bit_cast(double, make_uint2(lo[0], hi[0]));
-        if (2 * q + 1 < T) x[2 * q + 1] = __builtin_bit_cast(double, make_uint2(lo[1], hi[1]));
-    }
-}
-
 // value of position p (= lane p % 64, register p / 64) of a per-lane array, wave-uniform
 template <int NQ>
 __device__ __forceinline__ double lane_pick(const double (&v)[NQ], int p) {
@@ -308,8 +293,9 @@ __global__ void k_inertia_zero(int batch, const int* __restrict__ list, int* __r
     inertia[3 * b + 2] = 0;
 }
 
-template <int T>
-__global__ __launch_bounds__(FT) void k_front_factor(Plan P, Vals V, int f0, int batch, const int* __restrict__ list,
+// W: waves per SIMD the register allocation targets (the _w variant below)
+template <int T, int W>
+__global__ __launch_bounds__(FT) __attribute__((amdgpu_waves_per_eu(W))) void k_front_factor_w(Plan P, Vals V, int f0, int batch, const int* __restrict__ list,
                                                      double* __restrict__ Lst, int2* __restrict__ piv,
                                                      double* __restrict__ dinv, int2* __restrict__ sinfo,
                                                      double* __restrict__ CB, int* __restrict__ inertia) {
@@ -522,71 +508,49 @@ __global__ __launch_bounds__(FT) void k_front_factor(Plan P, Vals V, int f0, int
             dv[3 * steps + 1] = i01;
             dv[3 * steps + 2] = i11;
         }
-        // row factors of the thread's rows 32I + ti: l0 = rows of L's first column, l1 of the
-        // second (2x2 pivot); A -= l0 c0^T (+ l1 cr^T), c0 = column p (1x1) or k (2x2)
-        double l0[T], l1[T];
-        {
-            double xk[T];
-            column_rows<T, NQ>(use_r ? cw : cv, xk);
-            if (type == 1) {
-                double xr[T];
-                column_rows<T, NQ>(cw, xr);
-#pragma unroll
-                for (int I = 0; I < T; ++I) {
-                    l0[I] = xk[I] * i00 + xr[I] * i01;
-                    l1[I] = xk[I] * i01 + xr[I] * i11;
-                }
-            } else {
-#pragma unroll
-                for (int I = 0; I < T; ++I) {
-                    l0[I] = xk[I] * i00;
-                    l1[I] = 0.0;
-                }
-            }
-        }
-        KST(8);                  // record, row factors (permlane broadcast)
+        // L's column(s) of this step from the pivot columns in LDS: row i of the first column is
+        // c0[i] i00 (+ cr[i] i01 for a 2x2 pivot), of the second cr[i] i11 + c0[i] i01. Re-read
+        // from LDS rather than held in registers across the decision (frees the registers for a
+        // second workgroup per CU).
+        const double* c0p = use_r ? cr : ck;     // column p (1x1) or k (2x2)
         if (lvt) {
-            // position tid = row 32 tj + ti of the thread: its factor entries are l0[tj], l1[tj]
-            double v0 = l0[0];
-#pragma unroll
-            for (int I = 1; I < T; ++I) v0 = blend(v0, l0[I], tj == I ? ~0ull : 0ull);
             const int ci = cit;
+            const double x0 = c0p[tid];
             if (type == 0) {
-                Lb[loff + ci] = v0;
+                Lb[loff + ci] = x0 * i00;
             } else if (type == 1) {
-                double v1 = l1[0];
-#pragma unroll
-                for (int I = 1; I < T; ++I) v1 = blend(v1, l1[I], tj == I ? ~0ull : 0ull);
-                Lb[loff + 2 * ci] = v0;
-                Lb[loff + 2 * ci + 1] = v1;
+                const double x1 = cr[tid];
+                Lb[loff + 2 * ci] = x0 * i00 + x1 * i01;
+                Lb[loff + 2 * ci + 1] = x0 * i01 + x1 * i11;
             } else {
                 Lb[loff + ci] = 0.0;
             }
         }
         loff += (long long)nlive * ncol;
-        KST(3);                  // pivot inverse, record, row factors, factor-column stores
-        // Schur update: one rank-1 pass (1x1 pivot) or two (2x2 pivot); tiles of dead rows are
-        // skipped, dead column tiles are updated too (skipping them per tile costs the compiler a
-        // select per entry: measured 2x slower)
+        KST(3);                  // pivot inverse, record, factor-column stores
+        // Schur update: one rank-1 pass (1x1 pivot) or two (2x2 pivot), A -= l c^T with c the
+        // pivot column (pass 0: c0, pass 1: cr); tiles of dead rows are skipped, dead column
+        // tiles are updated too (skipping them per tile costs the compiler a select per entry:
+        // measured 2x slower)
         const int npass = type == 0 ? 1 : type == 1 ? 2 : 0;
         for (int pass = 0; pass < npass; ++pass) {
-            const double* cc = pass == 1 ? cr : (use_r ? cr : ck);
+            const double* cc = pass == 1 ? cr : c0p;
+            const double f0 = pass == 1 ? i01 : i00, f1 = pass == 1 ? i11 : i01;
             double cj[T][2];
 #pragma unroll
             for (int J = 0; J < T; ++J) {
                 cj[J][0] = cc[32 * J + tj];
                 cj[J][1] = cc[32 * J + 16 + tj];
             }
-            double li[T];
-#pragma unroll
-            for (int I = 0; I < T; ++I) li[I] = pass == 1 ? l1[I] : l0[I];
 #pragma unroll
             for (int I = 0; I < T; ++I) {
                 if (live.any_in_tile(I)) {
+                    const double x0 = c0p[32 * I + ti];
+                    const double li = type == 1 ? x0 * f0 + cr[32 * I + ti] * f1 : x0 * i00;
 #pragma unroll
                     for (int J = 0; J <= I; ++J) {
-                        a[slot(I, J)][0] = fma(-li[I], cj[J][0], a[slot(I, J)][0]);
-                        a[slot(I, J)][1] = fma(-li[I], cj[J][1], a[slot(I, J)][1]);
+                        a[slot(I, J)][0] = fma(-li, cj[J][0], a[slot(I, J)][0]);
+                        a[slot(I, J)][1] = fma(-li, cj[J][1], a[slot(I, J)][1]);
                     }
                 }
             }
@@ -975,10 +939,19 @@ size_t factor_lds() {
     return sizeof(double) * (32 * (NP + 1) + 4 * NP) + sizeof(int) * NP;
 }
 
+// Six-tile fronts hold 138 VGPRs: one 512-thread workgroup per CU. Allocated for four waves per
+// SIMD (a few spilled registers, reloaded from scratch a few times per pivot step), two workgroups
+// share a CU and overlap their pivot chains: B = 512 factorisation 37.3 -> 28.1 ms, B = 1 0.77 ->
+// 0.80 ms. So the four-wave variant runs when the level has more workgroups than the chip has CUs.
+constexpr int CUS = 256;
+
 template <int T>
 int launch_factor_level(const ato_kkt* h, const Plan& P, const Vals& V, int f0, int nf, int batch, const int* list,
                         int* inertia, hipStream_t st) {
-    hipLaunchKernelGGL(k_front_factor<T>, dim3(nf, batch), dim3(FT), factor_lds<T>(), st, P, V, f0, batch, list,
+    auto k = k_front_factor_w<T, 1>;
+    if constexpr (T == 6)
+        if ((long long)nf * batch > CUS) k = k_front_factor_w<T, 4>;
+    hipLaunchKernelGGL(k, dim3(nf, batch), dim3(FT), factor_lds<T>(), st, P, V, f0, batch, list,
                        h->d_L, h->d_piv, h->d_dinv, h->d_sinfo, h->d_cb, inertia);
     KKT_HIP(hipGetLastError());
     return ATO_OK;

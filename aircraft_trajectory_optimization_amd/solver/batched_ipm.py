@@ -562,7 +562,16 @@ class BatchedInteriorPoint:
 
         laps = self.laps
         laps.lap()
+        trace = []                                   # profiling: (active, waiting, seconds) per lockstep iteration
+        t_it = time.perf_counter()
         for it in range(3 * o.max_iter + 3):
+            if laps.on and it:
+                if laps.cuda:
+                    torch.cuda.synchronize()
+                t_now = time.perf_counter()
+                trace.append([int(stepping.sum()), int(R.sum()) if resto_ran else 0, t_now - t_it])
+                t_it = t_now
+            resto_ran = False
             iters = torch.where(act, own, iters)
             Js = jv * sg[self.jr]
             dual_x = gf + self._JTy(Js, y) - zl + zu
@@ -740,6 +749,7 @@ class BatchedInteriorPoint:
                     phi_w = self._phi(f, x, s, mu)
                     add_filter(can, theta_w, phi_w)
                     xr, okr = self._restore(can, x, g, mu, theta_w, F, nf)
+                    resto_ran = True
                     laps.lap('resto')
                     bad = can & ~okr
                     status = torch.where(bad, torch.full_like(status, LS_FAILED), status)
@@ -770,6 +780,8 @@ class BatchedInteriorPoint:
         self.stats['restorations'] = self.stats.get('restorations', 0) + int(n_resto.sum())
         if laps.on:
             self.stats['laps'] = dict(laps.t)
+            if stop_check is None:
+                self.stats['iter_trace'] = trace
         return BatchedIPMResult(x=x, f=fu, lam_g=y * sg / sf, lam_x=(zu - zl) / sf,
                                 status=[STATUS_NAMES[int(v)] for v in st], iters=iters.cpu().numpy(),
                                 stats=dict(self.stats))
@@ -860,8 +872,10 @@ class BatchedInteriorPoint:
 
         res = sub.solve(Xr0, mu0=cols(mu_r), active=None if compact else R, stop_check=accept,
                         allow_restoration=False, progress=self._progress)
+        # (restored instances, nested lockstep iterations) of every restoration phase
+        self.stats.setdefault('resto_phases', []).append([int(R.sum()), int(len(sub.history))])
         for k2, v in sub.stats.items():
-            if k2 not in ('restorations', 'laps'):
+            if k2 not in ('restorations', 'laps', 'resto_phases'):
                 self.stats[k2] = self.stats.get(k2, 0) + v
         for k2, v in sub.laps.t.items():          # diagnostic split of the nested solve
             self.laps.t['resto:' + k2] = self.laps.t.get('resto:' + k2, 0.0) + v

@@ -73,6 +73,7 @@ for s in $STEPS; do
                    python tools/solve_batched.py --batch 512 --max-iter 60 --no-host --out "$OUT/solveprof.json" ;;
         solvelaps) ATO_IPM_PROFILE=1 run solvelaps 600 python tools/solve_batched.py --batch 512 --max-iter 60 --no-host --out "$OUT/solvelaps.json" ;;
         listpmc) run listpmc 120 rocprofv3 -L ;;
+        mb)    run mb_store 120 ./tools/mb_store ;;
         mbpmc) run mb_fetch 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/mb_fetch" -o run -- ./tools/mb_store
                run mb_write 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/mb_write" -o run -- ./tools/mb_store ;;
         units) for k in 0 1 2 3 4 12 34; do

@@ -4,6 +4,7 @@
 //   B: same grid, 44 stores of 1 KB (16 B / lane: two rows per instruction)
 //   C: 256-thread workgroups, grid-stride 16 B / lane streaming stores (reference)
 //   D: A plus 55 coalesced 512-B loads per wave from a 21 MB buffer (k_eval's read volume)
+//   F, G: A and D with nontemporal stores
 // Build: hipcc -O3 --offload-arch=gfx950 -o mb_store tools/mb_store.hip
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -42,6 +43,23 @@ __global__ __launch_bounds__(64) void kD(double* J, const double* w, double v) {
     for (int i = 0; i < ROWS; ++i) J[base + (long)i * B] = acc + i;
 }
 
+// F: A with nontemporal (streaming) stores; G: D with nontemporal stores
+__global__ __launch_bounds__(64) void kF(double* J, double v) {
+    const long base = (long)blockIdx.y * ROWS * B + blockIdx.x * 64 + threadIdx.x;
+#pragma unroll 8
+    for (int i = 0; i < ROWS; ++i) __builtin_nontemporal_store(v + i, J + base + (long)i * B);
+}
+
+__global__ __launch_bounds__(64) void kG(double* J, const double* w, double v) {
+    const long base = (long)blockIdx.y * ROWS * B + blockIdx.x * 64 + threadIdx.x;
+    const long rb = (long)(blockIdx.y % 50) * 106 * B + blockIdx.x * 64 + threadIdx.x;
+    double acc = v;
+#pragma unroll 11
+    for (int i = 0; i < 55; ++i) acc += w[rb + (long)i * B];
+#pragma unroll 8
+    for (int i = 0; i < ROWS; ++i) __builtin_nontemporal_store(acc + i, J + base + (long)i * B);
+}
+
 // E: read 64 MiB once, 8 B / lane coalesced (FETCH_SIZE calibration for k_eval's load width)
 __global__ __launch_bounds__(256) void kE(const double* x, long n, double* out) {
     double acc = 0;
@@ -78,6 +96,8 @@ int main() {
     run("B one-wave WG, 16B/lane paired stores", [&] { kB<<<g, 64>>>(J, 1.0); });
     run("C 256-thr grid-stride 16B/lane (2048 WG)", [&] { kC<<<2048, 256>>>((double2*)J, (long)(bytes / 16), 1.0); });
     run("D = A + 55 coalesced loads per wave", [&] { kD<<<g, 64>>>(J, w, 1.0); });
+    run("F = A, nontemporal stores", [&] { kF<<<g, 64>>>(J, 1.0); });
+    run("G = D, nontemporal stores", [&] { kG<<<g, 64>>>(J, w, 1.0); });
     double* big;
     const long nbig = 8L << 20;   // 64 MiB of doubles
     CHECK(hipMalloc(&big, nbig * sizeof(double)));
