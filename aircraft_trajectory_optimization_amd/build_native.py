@@ -57,7 +57,9 @@ def build(verbose=True, jobs=None) -> str:
     work = [(os.path.join(CSRC, 'ato_capi.hip'), os.path.join(OBJ, 'ato_capi.o'), []),
             (os.path.join(CSRC, 'ato_hstruct.cpp'), os.path.join(OBJ, 'ato_hstruct.o'), []),
             (os.path.join(CSRC, 'ato_mesh.hip'), os.path.join(OBJ, 'ato_mesh.o'), []),
-            (os.path.join(CSRC, 'ato_kkt.hip'), os.path.join(OBJ, 'ato_kkt.o'), [])]
+            (os.path.join(CSRC, 'ato_kkt.hip'), os.path.join(OBJ, 'ato_kkt.o'), []),
+            # no contraction: the interior-point column kernels reproduce the host formulas bit for bit
+            (os.path.join(CSRC, 'ato_ipm.hip'), os.path.join(OBJ, 'ato_ipm.o'), ['-ffp-contract=off'])]
     for i in range(N_INST):
         work.append((os.path.join(CSRC, 'ato_inst.hip'), os.path.join(OBJ, f'ato_inst{i}.o'), [f'-DATO_INST={i}']))
     jobs = jobs or min(len(work), max(1, min(8, os.cpu_count() or 4)))

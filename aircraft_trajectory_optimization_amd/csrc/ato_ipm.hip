@@ -1,0 +1,517 @@
+// ato_ipm.hip -- fused column kernels of the batched interior-point iteration (include/ato_ipm.h).
+//
+// The batched solver (solver/batched_ipm.py) restates IPOPT's iteration (ref:
+// drone3d/raceline/base_raceline.py:752-799, the solver behind ca.nlpsol) on [element][W]
+// device tensors. Each of its vector steps -- optimality errors, barrier right-hand side,
+// fraction to the boundary, filter measures, multiplier safeguard -- was tens of elementwise
+// tensor operations (one launch each, most of an iteration's launches once the batch has
+// shrunk). Here each step is one launch (plus one for per-column reductions).
+//
+// Layout: element e of column b at e * W + b; thread b of a 64-wide column block reads
+// consecutive columns (coalesced 512-byte rows). Reductions: stage 1 = one workgroup per
+// (column block, chunk of CH elements of one part), partial results to the workspace
+// [quantity][chunk][W]; stage 2 = one thread per column folds the chunks in order. Maxima and
+// minima propagate NaN like torch.maximum / amax. Compiled with -ffp-contract=off: no fused
+// multiply-adds, so elementwise results equal the host formulas bit for bit.
+#include <hip/hip_runtime.h>
+#include <cmath>
+#include <string>
+#include "../../include/ato_ipm.h"
+#include "../../include/ato.h"
+
+void ato_internal_set_error(const std::string& msg);   // ato_capi.hip: ato_last_error()
+
+namespace {
+
+constexpr int CH = 32;          // elements per reduction chunk
+constexpr int CB = 64;          // columns per workgroup
+constexpr int QMAX = 9;         // partial quantities per chunk (errors)
+
+__device__ __forceinline__ double nmax(double a, double b) {
+    return (a != a || b != b) ? __builtin_nan("") : (a > b ? a : b);
+}
+__device__ __forceinline__ double nmin(double a, double b) {
+    return (a != a || b != b) ? __builtin_nan("") : (a < b ? a : b);
+}
+__device__ __forceinline__ bool fin(double v) { return fabs(v) < INFINITY; }
+
+// chunking of up to four parts of different lengths
+struct Parts {
+    int len[4];
+    int c0[5];                  // first chunk of every part; c0[4] = total
+};
+
+Parts make_parts(int a, int b, int c, int d) {
+    Parts p;
+    const int l[4] = {a, b, c, d};
+    p.c0[0] = 0;
+    for (int i = 0; i < 4; ++i) {
+        p.len[i] = l[i];
+        p.c0[i + 1] = p.c0[i] + (l[i] + CH - 1) / CH;
+    }
+    return p;
+}
+
+__device__ __forceinline__ void chunk_of(const Parts& p, int c, int& part, int& e0, int& e1) {
+    part = c < p.c0[1] ? 0 : c < p.c0[2] ? 1 : c < p.c0[3] ? 2 : 3;
+    e0 = (c - p.c0[part]) * CH;
+    e1 = min(e0 + CH, p.len[part]);
+}
+
+struct Dev {
+    int n, m, mi, meq, W;
+    const int* iin;
+    const int* ieq;
+    const double *xL, *xU, *dL, *dU;
+};
+
+__device__ __forceinline__ long long at(const Dev& d, int e, int b) { return (long long)e * d.W + b; }
+
+// slacks of the bounds (batched_ipm.py _slacks): 1 where the bound is absent
+__device__ __forceinline__ void xslacks(const Dev& d, const double* x, int e, int b, double& a, double& bb,
+                                        bool& hl, bool& hu) {
+    const long long i = at(d, e, b);
+    const double lo = d.xL[i], hi = d.xU[i], v = x[i];
+    hl = fin(lo);
+    hu = fin(hi);
+    a = hl ? v - lo : 1.0;
+    bb = hu ? hi - v : 1.0;
+}
+
+__device__ __forceinline__ void sslacks(const Dev& d, const double* s, int i0, int b, double& c, double& dd,
+                                        bool& hl, bool& hu) {
+    const long long i = at(d, i0, b);
+    const double lo = d.dL[i], hi = d.dU[i], v = s[i];
+    hl = fin(lo);
+    hu = fin(hi);
+    c = hl ? v - lo : 1.0;
+    dd = hu ? hi - v : 1.0;
+}
+
+// ------------------------------------------------------------------------------------------
+// errors: q = 0 du, 1 pr, 2 co, 3 pr_uns (max); 4 |zl|, 5 |zu|, 6 |vl|, 7 |vu|, 8 |y| (sums)
+// parts: variables, slack rows, equality rows, all rows (for |y|)
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(CB) void k_errors(Dev d, Parts P, const double* __restrict__ x,
+                                               const double* __restrict__ s, const double* __restrict__ g,
+                                               const double* __restrict__ c_rhs, const double* __restrict__ sg,
+                                               const double* __restrict__ y, const double* __restrict__ zl,
+                                               const double* __restrict__ zu, const double* __restrict__ vl,
+                                               const double* __restrict__ vu, const double* __restrict__ dual_x,
+                                               const double* __restrict__ mu, double* __restrict__ work) {
+    const int b = blockIdx.x * CB + threadIdx.x;
+    const int c = blockIdx.y;
+    if (b >= d.W) return;
+    int part, e0, e1;
+    chunk_of(P, c, part, e0, e1);
+    const double m_ = mu[b];
+    double q[QMAX] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    if (part == 0) {
+        for (int e = e0; e < e1; ++e) {
+            double a, bb;
+            bool hl, hu;
+            xslacks(d, x, e, b, a, bb, hl, hu);
+            const long long i = at(d, e, b);
+            q[0] = nmax(q[0], fabs(dual_x[i]));
+            if (hl) q[2] = nmax(q[2], fabs(a * zl[i] - m_));
+            if (hu) q[2] = nmax(q[2], fabs(bb * zu[i] - m_));
+            q[4] += fabs(zl[i]);
+            q[5] += fabs(zu[i]);
+        }
+    } else if (part == 1) {
+        for (int k = e0; k < e1; ++k) {
+            double cc, dd;
+            bool hl, hu;
+            sslacks(d, s, k, b, cc, dd, hl, hu);
+            const long long i = at(d, k, b);
+            const int row = d.iin[k];
+            const long long ir = at(d, row, b);
+            const double ds = (-y[ir] - vl[i]) + vu[i];
+            q[0] = nmax(q[0], fabs(ds));
+            if (hl) q[2] = nmax(q[2], fabs(cc * vl[i] - m_));
+            if (hu) q[2] = nmax(q[2], fabs(dd * vu[i] - m_));
+            q[6] += fabs(vl[i]);
+            q[7] += fabs(vu[i]);
+            const double r = g[ir] - s[i];
+            q[1] = nmax(q[1], fabs(r));
+            q[3] = nmax(q[3], fabs(r / sg[ir]));
+        }
+    } else if (part == 2) {
+        for (int k = e0; k < e1; ++k) {
+            const long long ir = at(d, d.ieq[k], b);
+            const double r = g[ir] - c_rhs[at(d, k, b)];
+            q[1] = nmax(q[1], fabs(r));
+            q[3] = nmax(q[3], fabs(r / sg[ir]));
+        }
+    } else {
+        for (int k = e0; k < e1; ++k) q[8] += fabs(y[at(d, k, b)]);
+    }
+    const int NC = P.c0[4];
+#pragma unroll
+    for (int k = 0; k < QMAX; ++k) work[((long long)k * NC + c) * d.W + b] = q[k];
+}
+
+__global__ __launch_bounds__(CB) void k_errors_fold(int W, int NC, int m, double s_max,
+                                                    const double* __restrict__ n_bounds,
+                                                    const double* __restrict__ work, double* __restrict__ out) {
+    const int b = blockIdx.x * CB + threadIdx.x;
+    if (b >= W) return;
+    double q[QMAX] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (int c = 0; c < NC; ++c) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) q[k] = nmax(q[k], work[((long long)k * NC + c) * W + b]);
+#pragma unroll
+        for (int k = 4; k < QMAX; ++k) q[k] += work[((long long)k * NC + c) * W + b];
+    }
+    const double nz = n_bounds[b];
+    const double zsum = ((q[4] + q[5]) + q[6]) + q[7];
+    const double s_d = nmax((q[8] + zsum) / fmax((double)m + nz, 1.0), s_max) / s_max;
+    const double s_c = nmax(zsum / fmax(nz, 1.0), s_max) / s_max;
+    const double du = q[0], pr = q[1], co = q[2];
+    out[0 * W + b] = nmax(nmax(du / s_d, pr), co / s_c);
+    out[1 * W + b] = du;
+    out[2 * W + b] = pr;
+    out[3 * W + b] = co;
+    out[4 * W + b] = q[3];
+}
+
+// ------------------------------------------------------------------------------------------
+// right-hand side: one thread per (element, column) of variables | slacks | rows
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_rhs(Dev d, const double* __restrict__ x, const double* __restrict__ s,
+                                             const double* __restrict__ g, const double* __restrict__ c_rhs,
+                                             const double* __restrict__ gf, const double* __restrict__ jty,
+                                             const double* __restrict__ y, const double* __restrict__ zl,
+                                             const double* __restrict__ zu, const double* __restrict__ vl,
+                                             const double* __restrict__ vu, const double* __restrict__ mu,
+                                             double kd, double* __restrict__ Sx, double* __restrict__ Ss,
+                                             double* __restrict__ gx, double* __restrict__ gs,
+                                             double* __restrict__ rhs_x, double* __restrict__ rhs_s,
+                                             double* __restrict__ rhs_y) {
+    const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
+    const long long nx = (long long)d.n * d.W, ns = (long long)d.mi * d.W;
+    if (t < nx) {
+        const int e = (int)(t / d.W), b = (int)(t - (long long)e * d.W);
+        double a, bb;
+        bool hl, hu;
+        xslacks(d, x, e, b, a, bb, hl, hu);
+        const double m_ = mu[b];
+        Sx[t] = (hl ? zl[t] / a : 0.0) + (hu ? zu[t] / bb : 0.0);
+        double v = (gf[t] - m_ * (hl ? 1.0 / a : 0.0)) + m_ * (hu ? 1.0 / bb : 0.0);
+        v = v + (kd * m_) * ((hl && !hu ? 1.0 : 0.0) - (hu && !hl ? 1.0 : 0.0));
+        gx[t] = v;
+        rhs_x[t] = -(v + jty[t]);
+    } else if (t < nx + ns) {
+        const long long u = t - nx;
+        const int k = (int)(u / d.W), b = (int)(u - (long long)k * d.W);
+        double cc, dd;
+        bool hl, hu;
+        sslacks(d, s, k, b, cc, dd, hl, hu);
+        const double m_ = mu[b];
+        Ss[u] = (hl ? vl[u] / cc : 0.0) + (hu ? vu[u] / dd : 0.0);
+        double v = (-m_) * (hl ? 1.0 / cc : 0.0) + m_ * (hu ? 1.0 / dd : 0.0);
+        v = v + (kd * m_) * ((hl && !hu ? 1.0 : 0.0) - (hu && !hl ? 1.0 : 0.0));
+        gs[u] = v;
+        rhs_s[u] = -(v - y[at(d, d.iin[k], b)]);
+    }
+}
+
+// rhs_y = -r: slack rows -(g - s), equality rows -(g - c_rhs)
+__global__ __launch_bounds__(256) void k_resid_rows(Dev d, const double* __restrict__ g, const double* __restrict__ s,
+                                                    const double* __restrict__ c_rhs, double* __restrict__ out) {
+    const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
+    const long long ns = (long long)d.mi * d.W, ne = (long long)d.meq * d.W;
+    if (t < ns) {
+        const int k = (int)(t / d.W), b = (int)(t - (long long)k * d.W);
+        const long long ir = at(d, d.iin[k], b);
+        out[ir] = -(g[ir] - s[t]);
+    } else if (t < ns + ne) {
+        const long long u = t - ns;
+        const int k = (int)(u / d.W), b = (int)(u - (long long)k * d.W);
+        const long long ir = at(d, d.ieq[k], b);
+        out[ir] = -(g[ir] - c_rhs[u]);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// direction: multiplier steps (elementwise) and per-column minima / dot products
+// q = 0 alpha_max candidates (min), 1 alpha_z candidates (min), 2 gx.dx, 3 gs.ds (sums)
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ double ftb_ratio(double v, double dv, bool mask, double ntau) {
+    return (mask && dv < 0.0) ? (ntau * v) / dv : INFINITY;
+}
+
+__global__ __launch_bounds__(CB) void k_direction(Dev d, Parts P, const double* __restrict__ x,
+                                                  const double* __restrict__ s, const double* __restrict__ dx,
+                                                  const double* __restrict__ ds, const double* __restrict__ zl,
+                                                  const double* __restrict__ zu, const double* __restrict__ vl,
+                                                  const double* __restrict__ vu, const double* __restrict__ gx,
+                                                  const double* __restrict__ gs, const double* __restrict__ mu,
+                                                  const double* __restrict__ tau, double* __restrict__ dzl,
+                                                  double* __restrict__ dzu, double* __restrict__ dvl,
+                                                  double* __restrict__ dvu, double* __restrict__ work) {
+    const int b = blockIdx.x * CB + threadIdx.x;
+    const int c = blockIdx.y;
+    if (b >= d.W) return;
+    int part, e0, e1;
+    chunk_of(P, c, part, e0, e1);
+    const double m_ = mu[b], nt = -tau[b];
+    double q0 = INFINITY, q1 = INFINITY, q2 = 0.0, q3 = 0.0;
+    if (part == 0) {
+        for (int e = e0; e < e1; ++e) {
+            double a, bb;
+            bool hl, hu;
+            xslacks(d, x, e, b, a, bb, hl, hu);
+            const long long i = at(d, e, b);
+            const double dxi = dx[i], zli = zl[i], zui = zu[i];
+            const double l = hl ? ((m_ / a) - zli) - ((zli / a) * dxi) : 0.0;
+            const double u = hu ? ((m_ / bb) - zui) + ((zui / bb) * dxi) : 0.0;
+            dzl[i] = l;
+            dzu[i] = u;
+            q0 = nmin(q0, nmin(ftb_ratio(a, dxi, hl, nt), ftb_ratio(bb, -dxi, hu, nt)));
+            q1 = nmin(q1, nmin(ftb_ratio(zli, l, hl, nt), ftb_ratio(zui, u, hu, nt)));
+            q2 += gx[i] * dxi;
+        }
+    } else {
+        for (int k = e0; k < e1; ++k) {
+            double cc, dd;
+            bool hl, hu;
+            sslacks(d, s, k, b, cc, dd, hl, hu);
+            const long long i = at(d, k, b);
+            const double dsi = ds[i], vli = vl[i], vui = vu[i];
+            const double l = hl ? ((m_ / cc) - vli) - ((vli / cc) * dsi) : 0.0;
+            const double u = hu ? ((m_ / dd) - vui) + ((vui / dd) * dsi) : 0.0;
+            dvl[i] = l;
+            dvu[i] = u;
+            q0 = nmin(q0, nmin(ftb_ratio(cc, dsi, hl, nt), ftb_ratio(dd, -dsi, hu, nt)));
+            q1 = nmin(q1, nmin(ftb_ratio(vli, l, hl, nt), ftb_ratio(vui, u, hu, nt)));
+            q3 += gs[i] * dsi;
+        }
+    }
+    const int NC = P.c0[4];
+    work[((long long)0 * NC + c) * d.W + b] = q0;
+    work[((long long)1 * NC + c) * d.W + b] = q1;
+    work[((long long)2 * NC + c) * d.W + b] = q2;
+    work[((long long)3 * NC + c) * d.W + b] = q3;
+}
+
+__global__ __launch_bounds__(CB) void k_direction_fold(int W, int NC, const double* __restrict__ work,
+                                                       double* __restrict__ out) {
+    const int b = blockIdx.x * CB + threadIdx.x;
+    if (b >= W) return;
+    double q0 = INFINITY, q1 = INFINITY, q2 = 0.0, q3 = 0.0;
+    for (int c = 0; c < NC; ++c) {
+        q0 = nmin(q0, work[((long long)0 * NC + c) * W + b]);
+        q1 = nmin(q1, work[((long long)1 * NC + c) * W + b]);
+        q2 += work[((long long)2 * NC + c) * W + b];
+        q3 += work[((long long)3 * NC + c) * W + b];
+    }
+    out[0 * W + b] = nmin(q0, 1.0);
+    out[1 * W + b] = nmin(q1, 1.0);
+    out[2 * W + b] = q2 + q3;
+}
+
+// ------------------------------------------------------------------------------------------
+// measures: q = 0 sum |r|, 1 sum log(slacks), 2 sum of one-sided slacks
+// parts: variables, slack rows, equality rows
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(CB) void k_measures(Dev d, Parts P, const double* __restrict__ x,
+                                                 const double* __restrict__ s, const double* __restrict__ g,
+                                                 const double* __restrict__ c_rhs, double* __restrict__ work) {
+    const int b = blockIdx.x * CB + threadIdx.x;
+    const int c = blockIdx.y;
+    if (b >= d.W) return;
+    int part, e0, e1;
+    chunk_of(P, c, part, e0, e1);
+    double th = 0.0, lg = 0.0, lin = 0.0;
+    if (part == 0) {
+        for (int e = e0; e < e1; ++e) {
+            double a, bb;
+            bool hl, hu;
+            xslacks(d, x, e, b, a, bb, hl, hu);
+            if (hl) lg += log(a);
+            if (hu) lg += log(bb);
+            if (hl && !hu) lin += a;
+            if (hu && !hl) lin += bb;
+        }
+    } else if (part == 1) {
+        for (int k = e0; k < e1; ++k) {
+            double cc, dd;
+            bool hl, hu;
+            sslacks(d, s, k, b, cc, dd, hl, hu);
+            if (hl) lg += log(cc);
+            if (hu) lg += log(dd);
+            if (hl && !hu) lin += cc;
+            if (hu && !hl) lin += dd;
+            th += fabs(g[at(d, d.iin[k], b)] - s[at(d, k, b)]);
+        }
+    } else {
+        for (int k = e0; k < e1; ++k) th += fabs(g[at(d, d.ieq[k], b)] - c_rhs[at(d, k, b)]);
+    }
+    const int NC = P.c0[4];
+    work[((long long)0 * NC + c) * d.W + b] = th;
+    work[((long long)1 * NC + c) * d.W + b] = lg;
+    work[((long long)2 * NC + c) * d.W + b] = lin;
+}
+
+__global__ __launch_bounds__(CB) void k_measures_fold(int W, int NC, const double* __restrict__ f,
+                                                      const double* __restrict__ mu, double kd,
+                                                      const double* __restrict__ work, double* __restrict__ out) {
+    const int b = blockIdx.x * CB + threadIdx.x;
+    if (b >= W) return;
+    double th = 0.0, lg = 0.0, lin = 0.0;
+    for (int c = 0; c < NC; ++c) {
+        th += work[((long long)0 * NC + c) * W + b];
+        lg += work[((long long)1 * NC + c) * W + b];
+        lin += work[((long long)2 * NC + c) * W + b];
+    }
+    const double m_ = mu[b];
+    out[0 * W + b] = th;
+    out[1 * W + b] = (f[b] - m_ * lg) + (kd * m_) * lin;
+}
+
+// ------------------------------------------------------------------------------------------
+// multipliers: z += az dz, then the kappa_sigma safeguard at the accepted slacks
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ double safeguard(double z, double m_, double ks, double sl) {
+    return nmin(nmax(z, m_ / (ks * sl)), (ks * m_) / sl);
+}
+
+__global__ __launch_bounds__(256) void k_multipliers(Dev d, const double* __restrict__ x, const double* __restrict__ s,
+                                                     const double* __restrict__ mu, const double* __restrict__ az,
+                                                     double ks, double* __restrict__ zl, double* __restrict__ zu,
+                                                     double* __restrict__ vl, double* __restrict__ vu,
+                                                     const double* __restrict__ dzl, const double* __restrict__ dzu,
+                                                     const double* __restrict__ dvl, const double* __restrict__ dvu) {
+    const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
+    const long long nx = (long long)d.n * d.W, ns = (long long)d.mi * d.W;
+    if (t < nx) {
+        const int e = (int)(t / d.W), b = (int)(t - (long long)e * d.W);
+        double a, bb;
+        bool hl, hu;
+        xslacks(d, x, e, b, a, bb, hl, hu);
+        const double m_ = mu[b], al = az[b];
+        const double l = zl[t] + al * dzl[t], u = zu[t] + al * dzu[t];
+        zl[t] = hl ? safeguard(l, m_, ks, a) : 0.0;
+        zu[t] = hu ? safeguard(u, m_, ks, bb) : 0.0;
+    } else if (t < nx + ns) {
+        const long long u0 = t - nx;
+        const int k = (int)(u0 / d.W), b = (int)(u0 - (long long)k * d.W);
+        double cc, dd;
+        bool hl, hu;
+        sslacks(d, s, k, b, cc, dd, hl, hu);
+        const double m_ = mu[b], al = az[b];
+        const double l = vl[u0] + al * dvl[u0], u = vu[u0] + al * dvu[u0];
+        vl[u0] = hl ? safeguard(l, m_, ks, cc) : 0.0;
+        vu[u0] = hu ? safeguard(u, m_, ks, dd) : 0.0;
+    }
+}
+
+int fail(int code, const std::string& m) {
+    ato_internal_set_error(m);
+    return code;
+}
+
+int check_launch(const char* what) {
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(ATO_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+    return ATO_OK;
+}
+
+bool make_dev(const ato_ipm_dims* d, const ato_ipm_bounds* bd, Dev& v) {
+    if (!d || !bd || d->n < 0 || d->m < 0 || d->mi < 0 || d->meq < 0 || d->mi + d->meq != d->m || d->W <= 0 ||
+        (d->mi && !d->iin) || (d->meq && !d->ieq) || (d->n && (!bd->xL || !bd->xU)) ||
+        (d->mi && (!bd->dL || !bd->dU)))
+        return false;
+    v = Dev{d->n, d->m, d->mi, d->meq, d->W, d->iin, d->ieq, bd->xL, bd->xU, bd->dL, bd->dU};
+    return true;
+}
+
+dim3 col_grid(int W, int NC) { return dim3((W + CB - 1) / CB, NC); }
+unsigned lin_blocks(long long cnt) { return (unsigned)((cnt + 255) / 256); }
+
+}  // namespace
+
+extern "C" {
+
+size_t ato_ipm_work_size(const ato_ipm_dims* d) {
+    if (!d || d->W <= 0) return 0;
+    const Parts P = make_parts(d->n, d->mi, d->meq, d->m);
+    return (size_t)QMAX * P.c0[4] * d->W;
+}
+
+int ato_ipm_errors(const ato_ipm_dims* d, const ato_ipm_bounds* bd, const double* x, const double* s,
+                   const double* g, const double* c_rhs, const double* sg, const double* y, const double* zl,
+                   const double* zu, const double* vl, const double* vu, const double* dual_x, const double* mu,
+                   const double* n_bounds, double s_max, double* work, double* out, void* stream) {
+    Dev v;
+    if (!make_dev(d, bd, v) || !work || !out || !mu || !n_bounds) return fail(ATO_ERR_ARG, "ato_ipm_errors: arguments");
+    const Parts P = make_parts(d->n, d->mi, d->meq, d->m);
+    auto st = static_cast<hipStream_t>(stream);
+    hipLaunchKernelGGL(k_errors, col_grid(d->W, P.c0[4]), dim3(CB), 0, st, v, P, x, s, g, c_rhs, sg, y, zl, zu, vl,
+                       vu, dual_x, mu, work);
+    hipLaunchKernelGGL(k_errors_fold, col_grid(d->W, 1), dim3(CB), 0, st, d->W, P.c0[4], d->m, s_max, n_bounds,
+                       work, out);
+    return check_launch("ato_ipm_errors");
+}
+
+int ato_ipm_rhs(const ato_ipm_dims* d, const ato_ipm_bounds* bd, const double* x, const double* s,
+                const double* g, const double* c_rhs, const double* gf, const double* jty, const double* y,
+                const double* zl, const double* zu, const double* vl, const double* vu, const double* mu,
+                double kappa_d, double* Sx, double* Ss, double* gx, double* gs, double* rhs_x, double* rhs_s,
+                double* rhs_y, void* stream) {
+    Dev v;
+    if (!make_dev(d, bd, v) || !mu) return fail(ATO_ERR_ARG, "ato_ipm_rhs: arguments");
+    auto st = static_cast<hipStream_t>(stream);
+    const long long cnt = (long long)(d->n + d->mi) * d->W;
+    if (cnt)
+        hipLaunchKernelGGL(k_rhs, dim3(lin_blocks(cnt)), dim3(256), 0, st, v, x, s, g, c_rhs, gf, jty, y, zl, zu, vl,
+                           vu, mu, kappa_d, Sx, Ss, gx, gs, rhs_x, rhs_s, rhs_y);
+    const long long cr = (long long)d->m * d->W;
+    if (cr) hipLaunchKernelGGL(k_resid_rows, dim3(lin_blocks(cr)), dim3(256), 0, st, v, g, s, c_rhs, rhs_y);
+    return check_launch("ato_ipm_rhs");
+}
+
+int ato_ipm_direction(const ato_ipm_dims* d, const ato_ipm_bounds* bd, const double* x, const double* s,
+                      const double* dx, const double* ds, const double* zl, const double* zu, const double* vl,
+                      const double* vu, const double* gx, const double* gs, const double* mu, const double* tau,
+                      double* dzl, double* dzu, double* dvl, double* dvu, double* work, double* out, void* stream) {
+    Dev v;
+    if (!make_dev(d, bd, v) || !work || !out || !mu || !tau) return fail(ATO_ERR_ARG, "ato_ipm_direction: arguments");
+    const Parts P = make_parts(d->n, d->mi, 0, 0);
+    auto st = static_cast<hipStream_t>(stream);
+    if (P.c0[4])
+        hipLaunchKernelGGL(k_direction, col_grid(d->W, P.c0[4]), dim3(CB), 0, st, v, P, x, s, dx, ds, zl, zu, vl, vu,
+                           gx, gs, mu, tau, dzl, dzu, dvl, dvu, work);
+    hipLaunchKernelGGL(k_direction_fold, col_grid(d->W, 1), dim3(CB), 0, st, d->W, P.c0[4], work, out);
+    return check_launch("ato_ipm_direction");
+}
+
+int ato_ipm_measures(const ato_ipm_dims* d, const ato_ipm_bounds* bd, const double* x, const double* s,
+                     const double* g, const double* c_rhs, const double* f, const double* mu, double kappa_d,
+                     double* work, double* out, void* stream) {
+    Dev v;
+    if (!make_dev(d, bd, v) || !work || !out || !mu || !f) return fail(ATO_ERR_ARG, "ato_ipm_measures: arguments");
+    const Parts P = make_parts(d->n, d->mi, d->meq, 0);
+    auto st = static_cast<hipStream_t>(stream);
+    if (P.c0[4])
+        hipLaunchKernelGGL(k_measures, col_grid(d->W, P.c0[4]), dim3(CB), 0, st, v, P, x, s, g, c_rhs, work);
+    hipLaunchKernelGGL(k_measures_fold, col_grid(d->W, 1), dim3(CB), 0, st, d->W, P.c0[4], f, mu, kappa_d, work, out);
+    return check_launch("ato_ipm_measures");
+}
+
+int ato_ipm_multipliers(const ato_ipm_dims* d, const ato_ipm_bounds* bd, const double* x, const double* s,
+                        const double* mu, const double* az, double kappa_sigma, double* zl, double* zu, double* vl,
+                        double* vu, const double* dzl, const double* dzu, const double* dvl, const double* dvu,
+                        void* stream) {
+    Dev v;
+    if (!make_dev(d, bd, v) || !mu || !az) return fail(ATO_ERR_ARG, "ato_ipm_multipliers: arguments");
+    auto st = static_cast<hipStream_t>(stream);
+    const long long cnt = (long long)(d->n + d->mi) * d->W;
+    if (cnt)
+        hipLaunchKernelGGL(k_multipliers, dim3(lin_blocks(cnt)), dim3(256), 0, st, v, x, s, mu, az, kappa_sigma, zl,
+                           zu, vl, vu, dzl, dzu, dvl, dvu);
+    return check_launch("ato_ipm_multipliers");
+}
+
+}  // extern "C"

@@ -87,12 +87,26 @@ class AtoProblemDesc(ctypes.Structure):
     ]
 
 
+class AtoIpmDims(ctypes.Structure):
+    ''' include/ato_ipm.h ato_ipm_dims '''
+    _fields_ = [('n', ctypes.c_int32), ('m', ctypes.c_int32), ('mi', ctypes.c_int32), ('meq', ctypes.c_int32),
+                ('iin', ctypes.c_void_p), ('ieq', ctypes.c_void_p), ('W', ctypes.c_int32)]
+
+
+class AtoIpmBounds(ctypes.Structure):
+    ''' include/ato_ipm.h ato_ipm_bounds '''
+    _fields_ = [('xL', ctypes.c_void_p), ('xU', ctypes.c_void_p), ('dL', ctypes.c_void_p), ('dU', ctypes.c_void_p)]
+
+
+IPM_SYMBOLS = ('ato_ipm_work_size', 'ato_ipm_errors', 'ato_ipm_rhs', 'ato_ipm_direction', 'ato_ipm_measures',
+               'ato_ipm_multipliers')
+
 EXPORTED_SYMBOLS = ('ato_create', 'ato_destroy', 'ato_sizes', 'ato_sparsity', 'ato_bounds',
                     'ato_reserve', 'ato_eval', 'ato_eval_f32', 'ato_hess_sparsity', 'ato_hess_eval',
                     'ato_mesh_create', 'ato_mesh_destroy', 'ato_mesh_signed_distance',
                     'ato_timing', 'ato_timing_read', 'ato_last_error', 'ato_version',
                     'ato_kkt_create', 'ato_kkt_destroy', 'ato_kkt_reserve', 'ato_kkt_factor', 'ato_kkt_solve',
-                    'ato_kkt_residual')
+                    'ato_kkt_residual') + IPM_SYMBOLS
 
 
 def library_path() -> str:
@@ -132,6 +146,16 @@ def declare(lib: ctypes.CDLL, prefix: str = 'ato') -> ctypes.CDLL:
                                          vp, vp]
         for fn in ('ato_kkt_create', 'ato_kkt_destroy', 'ato_kkt_reserve', 'ato_kkt_factor', 'ato_kkt_solve',
                    'ato_kkt_residual'):
+            getattr(lib, fn).restype = ctypes.c_int
+        dp, bp, d = ctypes.POINTER(AtoIpmDims), ctypes.POINTER(AtoIpmBounds), ctypes.c_double
+        lib.ato_ipm_work_size.argtypes = [dp]
+        lib.ato_ipm_work_size.restype = ctypes.c_size_t
+        lib.ato_ipm_errors.argtypes = [dp, bp] + [vp] * 12 + [vp, d, vp, vp, vp]
+        lib.ato_ipm_rhs.argtypes = [dp, bp] + [vp] * 12 + [d] + [vp] * 7 + [vp]
+        lib.ato_ipm_direction.argtypes = [dp, bp] + [vp] * 12 + [vp] * 4 + [vp, vp, vp]
+        lib.ato_ipm_measures.argtypes = [dp, bp] + [vp] * 6 + [d, vp, vp, vp]
+        lib.ato_ipm_multipliers.argtypes = [dp, bp, vp, vp, vp, vp, d] + [vp] * 8 + [vp]
+        for fn in IPM_SYMBOLS[1:]:
             getattr(lib, fn).restype = ctypes.c_int
         for fn in ('ato_create', 'ato_destroy', 'ato_sizes', 'ato_sparsity', 'ato_bounds', 'ato_reserve',
                    'ato_eval', 'ato_eval_f32', 'ato_hess_sparsity', 'ato_hess_eval', 'ato_timing',

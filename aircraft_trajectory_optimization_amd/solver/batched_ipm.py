@@ -98,6 +98,7 @@ class _SubsetDeviceEvaluator:
     def __init__(self, base: BatchedDeviceEvaluator, count: int):
         if not 0 < count <= base.batch:
             raise ValueError('subset size out of range')
+        self.base = base
         self.problem = base.bn.problem
         self.device, self.batch = base.device, int(count)
         self.n, self.m, self.nnz = base.n, base.m, base.nnz
@@ -120,6 +121,9 @@ class _SubsetDeviceEvaluator:
         self.problem.eval_ptrs(self.batch, self.w.data_ptr(), g=self.g.data_ptr(), jac=self.jac.data_ptr(),
                                f=self.f.data_ptr(), grad_f=self.gf.data_ptr(), stream=st.cuda_stream)
         return self.f.clone(), self.g.clone(), self.gf.clone(), self.jac.clone()
+
+    def subset(self, count: int) -> '_SubsetDeviceEvaluator':
+        return _SubsetDeviceEvaluator(self.base, count)
 
     def hess(self, X: torch.Tensor, lam: torch.Tensor, sigma: torch.Tensor) -> torch.Tensor:
         self.w.copy_(X)
@@ -220,7 +224,7 @@ class BatchedInteriorPoint:
         def per_inst(a):
             a = np.asarray(a, float)
             a = np.where(a >= INF, np.inf, np.where(a <= -INF, -np.inf, a))
-            return t(np.repeat(a[:, None], B, axis=1) if a.ndim == 1 else a.T if a.shape == (B, n) else a)
+            return t(np.repeat(a[:, None], B, axis=1) if a.ndim == 1 else a.T if a.shape == (B, n) else a).contiguous()
 
         self.lbx0, self.ubx0 = per_inst(lbx), per_inst(ubx)
         if self.lbx0.shape != (n, B):
@@ -237,8 +241,15 @@ class BatchedInteriorPoint:
         self.ubg0 = t(np.where(ubg >= INF, np.inf, ubg))
         for k_, v_ in _structure(ev, dev).items():
             setattr(self, k_, v_)
-        self.stats = {'factorizations': 0, 'solves': 0, 'evals': 0, 'hess': 0}
+        self.stats = {'factorizations': 0, 'solves': 0, 'evals': 0, 'hess': 0, 'compactions': 0}
         self.laps = _Laps(dev)
+        self.compact = True             # carry only the live columns once half of them have finished
+        # fused column kernels of the iteration's vector algebra on the device (libato, ato_ipm.h);
+        # on CPU (the tests' stand-ins) the same steps run as torch operations
+        self.vk = None
+        if torch.device(dev).type == 'cuda':
+            from aircraft_trajectory_optimization_amd.solver.ipm_device import DeviceIPMKernels
+            self.vk = DeviceIPMKernels(n, m, self.iin, self.ieq, dev)
 
     # ------------------------------------------------------------------ sparse products
     @staticmethod
@@ -355,6 +366,15 @@ class BatchedInteriorPoint:
             du = torch.maximum(du, dual_s.abs().amax(0))
         pr = r.abs().amax(0) if self.m else torch.zeros_like(du)
         return torch.maximum(torch.maximum(du / s_d, pr), co / s_c), du, pr, co
+
+    def _bd(self):
+        return self.vk.bounds(self.xL, self.xU, self.dL, self.dU)
+
+    def _measures(self, x, s, g, f, mu):
+        ''' filter measures (theta = sum |r|, barrier objective phi) per instance '''
+        if self.vk is not None:
+            return self.vk.measures(self._bd(), x, s, g, self.c_rhs, f, mu, self.o.kappa_d)
+        return self._resid(g, s).abs().sum(0), self._phi(f, x, s, mu)
 
     def _accept(self, theta, phi, gphi_d, alpha, tht, pht, F, nf):
         ''' filter acceptance per instance: (accepted, is_armijo_step) '''
@@ -554,11 +574,34 @@ class BatchedInteriorPoint:
         def add_filter(mask, th, ph):
             nonlocal F, nf
             pos = torch.clamp(nf, max=FILTER_MAX - 1)
-            rows = torch.arange(B, device=dev)
+            rows = torch.arange(F.shape[0], device=dev)
             entry = torch.stack([(1 - o.gamma_theta) * th, ph - o.gamma_phi * th], dim=1)
             cur = F[rows, pos]
             F[rows, pos] = torch.where(mask[:, None], entry, cur)
             nf = torch.where(mask, torch.clamp(nf + 1, max=FILTER_MAX), nf)
+
+        # ---- compaction: once at most half of the columns are still iterating (or waiting for a
+        # restoration), the solve continues on those columns only -- evaluator subset, KKT view,
+        # every per-instance tensor gathered. Columns are independent, so this changes which
+        # columns are carried, not what any instance computes. Results of the dropped columns are
+        # kept at full width (`out`). Not inside a restoration solve (its return test maps columns).
+        B0 = B
+        cols = torch.arange(B0, device=dev)          # original instance of every current column
+        keep = {k: getattr(self, k) for k in ('ev', 'kkt', 'B', 'lbx0', 'ubx0', 'lbg0', 'ubg0')}
+        can_compact = self.compact and stop_check is None and hasattr(self.ev, 'subset') and hasattr(self.kkt, 'view')
+        out = {'x': torch.zeros((n, B0), dtype=torch.float64, device=dev),
+               'lam_g': torch.zeros((m, B0), dtype=torch.float64, device=dev),
+               'lam_x': torch.zeros((n, B0), dtype=torch.float64, device=dev),
+               'status': torch.zeros(B0, dtype=torch.long, device=dev),
+               'iters': torch.zeros(B0, dtype=torch.long, device=dev)}
+        hist_row = torch.zeros((6, B0), dtype=torch.float64, device=dev)
+
+        def save(cols_, x_, y_, zl_, zu_, status_, iters_):
+            out['x'][:, cols_] = x_
+            out['lam_g'][:, cols_] = y_ * self.sg / self.sf
+            out['lam_x'][:, cols_] = (zu_ - zl_) / self.sf
+            out['status'][cols_] = status_
+            out['iters'][cols_] = iters_
 
         laps = self.laps
         laps.lap()
@@ -573,11 +616,34 @@ class BatchedInteriorPoint:
                 t_it = t_now
             resto_ran = False
             iters = torch.where(act, own, iters)
+            if can_compact and it and B > 1:
+                live = act | waiting
+                n_live = int(live.sum())
+                if 0 < n_live <= B // 2:
+                    save(cols, x, y, zl, zu, status, iters)
+                    sel = torch.nonzero(live).reshape(-1)
+                    (x, s, f, g, gf, jv, y, zl, zu, vl, vu, mu, tau, nf, dwl, n_acc, status, n_resto, own, waiting,
+                     iters, act) = self._compact(sel, (x, s, f, g, gf, jv, y, zl, zu, vl, vu, mu, tau, nf, dwl, n_acc,
+                                                      status, n_resto, own, waiting, iters, act))
+                    F = F.index_select(0, sel).contiguous()
+                    cols = cols.index_select(0, sel)
+                    self.ev = keep['ev'].subset(n_live)
+                    self.kkt = keep['kkt'].view(n_live)
+                    B = self.B = n_live
+                    sf, sg = self.sf, self.sg
+                    self.stats['compactions'] += 1
+                    laps.lap('compact')
             Js = jv * sg[self.jr]
-            dual_x = gf + self._JTy(Js, y) - zl + zu
-            E0, du, pr, co = self._errors(dual_x, g, x, s, y, zl, zu, vl, vu, 0.0)
-            pr_uns = (self._resid(g, s) / sg).abs().amax(0)
-            history.append(torch.stack([f / sf, pr, du, mu, E0, n_resto.double()]))
+            jty = self._JTy(Js, y)
+            dual_x = gf + jty - zl + zu
+            if self.vk is not None:
+                E0, du, pr, co, pr_uns = self.vk.errors(self._bd(), x, s, g, self.c_rhs, sg, y, zl, zu, vl, vu,
+                                                        dual_x, torch.zeros_like(mu), self.n_bounds, o.s_max)
+            else:
+                E0, du, pr, co = self._errors(dual_x, g, x, s, y, zl, zu, vl, vu, 0.0)
+                pr_uns = (self._resid(g, s) / sg).abs().amax(0)
+            hist_row[:, cols] = torch.stack([f / sf, pr, du, mu, E0, n_resto.double()])
+            history.append(hist_row.clone())
             if stop_check is not None:
                 stp = act & (own > 0) & stop_check(x)
                 status = torch.where(stp, torch.full_like(status, STOPPED), status)
@@ -605,7 +671,11 @@ class BatchedInteriorPoint:
             if bool(act.any()):
                 # ---- barrier update (monotone), per instance
                 for _ in range(100):
-                    Emu = self._errors(dual_x, g, x, s, y, zl, zu, vl, vu, mu)[0]
+                    if self.vk is not None:
+                        Emu = self.vk.errors(self._bd(), x, s, g, self.c_rhs, sg, y, zl, zu, vl, vu, dual_x, mu,
+                                             self.n_bounds, o.s_max)[0]
+                    else:
+                        Emu = self._errors(dual_x, g, x, s, y, zl, zu, vl, vu, mu)[0]
                     upd = act & (Emu <= o.kappa_eps * mu) & (mu > o.tol / 10)
                     if not bool(upd.any()):
                         break
@@ -618,14 +688,20 @@ class BatchedInteriorPoint:
                 W = self.ev.hess(x, y * sg, sf)
                 self.stats['hess'] += 1
                 laps.lap('hess')
-                a, b, c, d = self._slacks(x, s)
-                Sx = torch.where(self.hxl, zl / a, 0.0) + torch.where(self.hxu, zu / b, 0.0)
-                Ss = torch.where(self.hsl, vl / c, 0.0) + torch.where(self.hsu, vu / d, 0.0)
-                gx, gs = self._grad_phi(gf, x, s, mu)
-                r = self._resid(g, s)
-                rhs_x = -(gx + self._JTy(Js, y))
-                rhs_s = -(gs - y[self.iin])
-                rhs_y = -r
+                if self.vk is not None:
+                    Sx, Ss, gx, gs, rhs_x, rhs_s, rhs_y = self.vk.rhs(self._bd(), x, s, g, self.c_rhs, gf, jty, y, zl,
+                                                                      zu, vl, vu, mu, o.kappa_d)
+                    r = -rhs_y
+                    slk = None                   # bound slacks: only a second-order correction needs them
+                else:
+                    a, b, c, d = slk = self._slacks(x, s)
+                    Sx = torch.where(self.hxl, zl / a, 0.0) + torch.where(self.hxu, zu / b, 0.0)
+                    Ss = torch.where(self.hsl, vl / c, 0.0) + torch.where(self.hsu, vu / d, 0.0)
+                    gx, gs = self._grad_phi(gf, x, s, mu)
+                    r = self._resid(g, s)
+                    rhs_x = -(gx + jty)
+                    rhs_s = -(gs - y[self.iin])
+                    rhs_y = -r
                 laps.lap('rhs')
                 dx, ds, dy, delta_w, ok, ctx = self._kkt_step(W, Js, Sx, Ss, rhs_x, rhs_s, rhs_y, mu, dwl, act)
                 laps.lap('kkt_other')
@@ -634,18 +710,23 @@ class BatchedInteriorPoint:
                 act = act & ok
                 dwl = torch.where(act & (delta_w > 0), delta_w, dwl)
                 # ---- bound multiplier steps, fraction to the boundary
-                dzl = torch.where(self.hxl, mu / a - zl - zl / a * dx, 0.0)
-                dzu = torch.where(self.hxu, mu / b - zu + zu / b * dx, 0.0)
-                dvl = torch.where(self.hsl, mu / c - vl - vl / c * ds, 0.0)
-                dvu = torch.where(self.hsu, mu / d - vu + vu / d * ds, 0.0)
-                alpha_max = torch.minimum(torch.minimum(self._ftb(a, dx, self.hxl, tau), self._ftb(b, -dx, self.hxu, tau)),
-                                          torch.minimum(self._ftb(c, ds, self.hsl, tau), self._ftb(d, -ds, self.hsu, tau)))
-                alpha_z = torch.minimum(torch.minimum(self._ftb(zl, dzl, self.hxl, tau), self._ftb(zu, dzu, self.hxu, tau)),
-                                        torch.minimum(self._ftb(vl, dvl, self.hsl, tau), self._ftb(vu, dvu, self.hsu, tau)))
+                if self.vk is not None:
+                    dzl, dzu, dvl, dvu, alpha_max, alpha_z, gphi_d = self.vk.direction(
+                        self._bd(), x, s, dx, ds, zl, zu, vl, vu, gx, gs, mu, tau)
+                else:
+                    dzl = torch.where(self.hxl, mu / a - zl - zl / a * dx, 0.0)
+                    dzu = torch.where(self.hxu, mu / b - zu + zu / b * dx, 0.0)
+                    dvl = torch.where(self.hsl, mu / c - vl - vl / c * ds, 0.0)
+                    dvu = torch.where(self.hsu, mu / d - vu + vu / d * ds, 0.0)
+                    alpha_max = torch.minimum(
+                        torch.minimum(self._ftb(a, dx, self.hxl, tau), self._ftb(b, -dx, self.hxu, tau)),
+                        torch.minimum(self._ftb(c, ds, self.hsl, tau), self._ftb(d, -ds, self.hsu, tau)))
+                    alpha_z = torch.minimum(
+                        torch.minimum(self._ftb(zl, dzl, self.hxl, tau), self._ftb(zu, dzu, self.hxu, tau)),
+                        torch.minimum(self._ftb(vl, dvl, self.hsl, tau), self._ftb(vu, dvu, self.hsu, tau)))
+                    gphi_d = (gx * dx).sum(0) + (gs * ds).sum(0)
                 # ---- filter line search, all instances in lockstep
-                theta = r.abs().sum(0)
-                phi = self._phi(f, x, s, mu)
-                gphi_d = (gx * dx).sum(0) + (gs * ds).sum(0)
+                theta, phi = self._measures(x, s, g, f, mu)
                 neg = gphi_d < 0
                 mgd = torch.clamp(-gphi_d, min=1e-300)
                 t1 = o.gamma_phi * theta / mgd
@@ -693,9 +774,7 @@ class BatchedInteriorPoint:
                     laps.lap('ls_logic')
                     ft, gt, gft, jvt = self._eval(xt)
                     laps.lap('ls_eval')
-                    rt = self._resid(gt, st)
-                    tht = rt.abs().sum(0)
-                    pht = self._phi(ft, xt, st, mu)
+                    tht, pht = self._measures(xt, st, gt, ft, mu)
                     okt, armt = self._accept(theta, phi, gphi_d, alpha, tht, pht, F, nf)
                     okt = okt & pend
                     take(okt, alpha, xt, st, ft, gt, gft, jvt, armt, dy)
@@ -703,8 +782,10 @@ class BatchedInteriorPoint:
                     soc = pend & first & (tht >= theta)
                     if bool(soc.any()):
                         laps.lap('ls_logic')
-                        got = self._soc(soc, ctx, rhs_x, rhs_s, x, s, alpha, r, rt, theta, phi, gphi_d, F, nf, tau,
-                                        (a, b, c, d), mu, take)
+                        if slk is None:
+                            slk = self._slacks(x, s)
+                        got = self._soc(soc, ctx, rhs_x, rhs_s, x, s, alpha, r, self._resid(gt, st), theta, phi,
+                                        gphi_d, F, nf, tau, slk, mu, take)
                         pend = pend & ~got
                         laps.lap('soc')
                     first = first & False
@@ -722,14 +803,18 @@ class BatchedInteriorPoint:
                 jv = torch.where(m2, jvn, jv)
                 y = torch.where(m2, y + an * dyn, y)
                 az = torch.where(upd, alpha_z, torch.zeros_like(alpha_z))
-                zl, zu = zl + az * dzl, zu + az * dzu
-                vl, vu = vl + az * dvl, vu + az * dvu
-                a, b, c, d = self._slacks(x, s)
                 ks = o.kappa_sigma
-                zl = torch.where(self.hxl, torch.minimum(torch.maximum(zl, mu / (ks * a)), ks * mu / a), 0.0)
-                zu = torch.where(self.hxu, torch.minimum(torch.maximum(zu, mu / (ks * b)), ks * mu / b), 0.0)
-                vl = torch.where(self.hsl, torch.minimum(torch.maximum(vl, mu / (ks * c)), ks * mu / c), 0.0)
-                vu = torch.where(self.hsu, torch.minimum(torch.maximum(vu, mu / (ks * d)), ks * mu / d), 0.0)
+                if self.vk is not None:
+                    zl, zu, vl, vu = self.vk.multipliers(self._bd(), x, s, mu, az, ks, zl, zu, vl, vu, dzl, dzu, dvl,
+                                                         dvu)
+                else:
+                    zl, zu = zl + az * dzl, zu + az * dzu
+                    vl, vu = vl + az * dvl, vu + az * dvu
+                    a, b, c, d = self._slacks(x, s)
+                    zl = torch.where(self.hxl, torch.minimum(torch.maximum(zl, mu / (ks * a)), ks * mu / a), 0.0)
+                    zu = torch.where(self.hxu, torch.minimum(torch.maximum(zu, mu / (ks * b)), ks * mu / b), 0.0)
+                    vl = torch.where(self.hsl, torch.minimum(torch.maximum(vl, mu / (ks * c)), ks * mu / c), 0.0)
+                    vu = torch.where(self.hsu, torch.minimum(torch.maximum(vu, mu / (ks * d)), ks * mu / d), 0.0)
             own = own + stepping.long()
             laps.lap('accept')
             # ---- feasibility restoration: instances whose line search failed wait (frozen) and are
@@ -745,8 +830,7 @@ class BatchedInteriorPoint:
                 status = torch.where(cant, torch.full_like(status, LS_FAILED), status)
                 if bool(can.any()):
                     n_resto = n_resto + can.long()
-                    theta_w = self._resid(g, s).abs().sum(0)
-                    phi_w = self._phi(f, x, s, mu)
+                    theta_w, phi_w = self._measures(x, s, g, f, mu)
                     add_filter(can, theta_w, phi_w)
                     xr, okr = self._restore(can, x, g, mu, theta_w, F, nf)
                     resto_ran = True
@@ -771,20 +855,40 @@ class BatchedInteriorPoint:
                         act = act | okr
                 laps.lap('resto_post')
 
+        save(cols, x, y, zl, zu, status, iters)
+        self.stats['restorations'] = self.stats.get('restorations', 0) + int(n_resto.sum())
+        for k_, v_ in keep.items():                 # back to the full batch
+            setattr(self, k_, v_)
+        x = out['x']
         if o.honor_original_bounds:
             x = torch.minimum(torch.maximum(x, self.lbx0), self.ubx0)
         fu, _, _, _ = self.ev.eval(x)
-        st = status.cpu().numpy()
+        st = out['status'].cpu().numpy()
         # [lockstep iteration][f, inf_pr, inf_du, mu, E0, restorations so far][instance]
-        self.history = torch.stack(history).cpu().numpy() if history else np.zeros((0, 6, B))
-        self.stats['restorations'] = self.stats.get('restorations', 0) + int(n_resto.sum())
+        self.history = torch.stack(history).cpu().numpy() if history else np.zeros((0, 6, B0))
         if laps.on:
             self.stats['laps'] = dict(laps.t)
             if stop_check is None:
                 self.stats['iter_trace'] = trace
-        return BatchedIPMResult(x=x, f=fu, lam_g=y * sg / sf, lam_x=(zu - zl) / sf,
-                                status=[STATUS_NAMES[int(v)] for v in st], iters=iters.cpu().numpy(),
+        return BatchedIPMResult(x=x, f=fu, lam_g=out['lam_g'], lam_x=out['lam_x'],
+                                status=[STATUS_NAMES[int(v)] for v in st], iters=out['iters'].cpu().numpy(),
                                 stats=dict(self.stats))
+
+    # per-instance attributes of the solve (all [.., columns]; lbg0 / ubg0 may be shared [m, 1])
+    _INSTANCE_ATTRS = ('sf', 'sg', 'lbg_s', 'ubg_s', 'c_rhs', 'dL', 'dU', 'xL', 'xU', 'hxl', 'hxu', 'hsl', 'hsu',
+                       'dxl', 'dxu', 'dsl', 'dsu', 'n_bounds', 'lbx0', 'ubx0', 'theta_max', 'theta_min', 'lbg0', 'ubg0')
+
+    def _compact(self, sel, tensors):
+        ''' gather columns `sel` of the solver's per-instance attributes and of `tensors` '''
+        W = self.B
+
+        def take(t):
+            if torch.is_tensor(t) and t.dim() >= 1 and t.shape[-1] == W:
+                return t.index_select(t.dim() - 1, sel).contiguous()
+            return t
+        for k in self._INSTANCE_ATTRS:
+            setattr(self, k, take(getattr(self, k)))
+        return tuple(take(t) for t in tensors)
 
     def _soc(self, mask, ctx, rhs_x, rhs_s, x, s, alpha, r, rt, theta, phi, gphi_d, F, nf, tau, slk, mu, take):
         ''' second-order corrections (IPOPT A-5.5 - A-5.10) for the masked instances; returns the
@@ -810,8 +914,7 @@ class BatchedInteriorPoint:
             xt, st = x + am * dxs, s + am * dss
             ft, gt, gft, jvt = self._eval(xt)
             rt2 = self._resid(gt, st)
-            tht = rt2.abs().sum(0)
-            pht = self._phi(ft, xt, st, mu)
+            tht, pht = self._measures(xt, st, gt, ft, mu)
             ok, arm = self._accept(theta, phi, gphi_d, alpha, tht, pht, F, nf)
             ok = ok & cur
             take(ok, am, xt, st, ft, gt, gft, jvt, arm, dys)
@@ -862,8 +965,7 @@ class BatchedInteriorPoint:
                 xo = xr[:n]
             f2, g2, _, _ = self._eval(xo)
             s2 = self._push(g2[self.iin], self.dL, self.dU)
-            th = self._resid(g2, s2).abs().sum(0)
-            ph = self._phi(f2, xo, s2, mu)
+            th, ph = self._measures(xo, s2, g2, f2, mu)
             k = torch.arange(F.shape[1], device=dev)
             valid = k[None, :] < nf[:, None]
             in_f = (valid & (th[:, None] >= F[:, :, 0]) & (ph[:, None] >= F[:, :, 1])).any(1)
@@ -875,7 +977,7 @@ class BatchedInteriorPoint:
         # (restored instances, nested lockstep iterations) of every restoration phase
         self.stats.setdefault('resto_phases', []).append([int(R.sum()), int(len(sub.history))])
         for k2, v in sub.stats.items():
-            if k2 not in ('restorations', 'laps', 'resto_phases'):
+            if k2 not in ('restorations', 'laps', 'resto_phases', 'compactions'):
                 self.stats[k2] = self.stats.get(k2, 0) + v
         for k2, v in sub.laps.t.items():          # diagnostic split of the nested solve
             self.laps.t['resto:' + k2] = self.laps.t.get('resto:' + k2, 0.0) + v

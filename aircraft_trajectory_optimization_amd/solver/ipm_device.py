@@ -1,0 +1,138 @@
+'''
+Fused column kernels of the batched interior-point iteration (include/ato_ipm.h,
+csrc/ato_ipm.hip) for solver/batched_ipm.py on the device.
+
+Each method is one step of IPOPT's iteration (ref: drone3d/raceline/base_raceline.py:752-799,
+the solver behind ca.nlpsol) over W instance columns of [element][W] tensors -- the steps the
+batched solver otherwise spells out as tens of torch operations (its CPU path, which the
+tests use as the reference for these kernels). Loading fails loudly without libato.so.
+'''
+import ctypes
+from typing import Dict, Tuple
+
+import torch
+
+from aircraft_trajectory_optimization_amd import native
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+class DeviceIPMKernels:
+    def __init__(self, n: int, m: int, iin: torch.Tensor, ieq: torch.Tensor, device):
+        self.lib = native.load()
+        self.device = torch.device(device)
+        self.n, self.m = int(n), int(m)
+        self.iin = iin.to(device=self.device, dtype=torch.int32).contiguous()
+        self.ieq = ieq.to(device=self.device, dtype=torch.int32).contiguous()
+        self.mi, self.meq = len(self.iin), len(self.ieq)
+        self._dims: Dict[int, native.AtoIpmDims] = {}
+        self._work: Dict[int, torch.Tensor] = {}
+
+    # ------------------------------------------------------------------ plumbing
+    def dims(self, W: int):
+        d = self._dims.get(W)
+        if d is None:
+            d = native.AtoIpmDims(self.n, self.m, self.mi, self.meq, _p(self.iin) if self.mi else None,
+                                  _p(self.ieq) if self.meq else None, W)
+            self._dims[W] = d
+            size = int(self.lib.ato_ipm_work_size(ctypes.byref(d)))
+            self._work[W] = torch.empty(max(size, 1), dtype=torch.float64, device=self.device)
+        return ctypes.byref(d), self._work[W]
+
+    def _v(self, t, rows, W):
+        if t.dtype != torch.float64 or t.device != self.device or t.shape != (rows, W):
+            raise ValueError(f'IPM kernel operand: expected fp64 [{rows}, {W}] on {self.device}, got '
+                             f'{tuple(t.shape)} {t.dtype} {t.device}')
+        return t if t.is_contiguous() else t.contiguous()
+
+    def _c(self, t, W):
+        if t.dtype != torch.float64 or t.device != self.device or t.shape != (W,):
+            raise ValueError('IPM kernel per-column operand: expected fp64 [W]')
+        return t.contiguous()
+
+    @staticmethod
+    def bounds(xL, xU, dL, dU):
+        for t in (xL, xU, dL, dU):
+            if t.dtype != torch.float64 or t.dim() != 2 or not t.is_contiguous():
+                raise ValueError('IPM bounds must be contiguous fp64 [elements][W] tensors')
+        return native.AtoIpmBounds(_p(xL), _p(xU), _p(dL), _p(dU))
+
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def _check(self, rc, what):
+        if rc != 0:
+            raise RuntimeError(f'{what} failed ({rc}): {self.lib.ato_last_error().decode()}')
+
+    # ------------------------------------------------------------------ steps
+    def errors(self, bd, x, s, g, c_rhs, sg, y, zl, zu, vl, vu, dual_x, mu, n_bounds, s_max) -> Tuple[torch.Tensor, ...]:
+        ''' (E_mu, dual inf, primal inf, complementarity inf, max |r / sg|) per column '''
+        W = x.shape[1]
+        n, m, mi, me = self.n, self.m, self.mi, self.meq
+        d, work = self.dims(W)
+        ops = [self._v(x, n, W), self._v(s, mi, W), self._v(g, m, W), self._v(c_rhs, me, W), self._v(sg, m, W),
+               self._v(y, m, W), self._v(zl, n, W), self._v(zu, n, W), self._v(vl, mi, W), self._v(vu, mi, W),
+               self._v(dual_x, n, W), self._c(mu, W), self._c(n_bounds, W)]
+        out = torch.empty((5, W), dtype=torch.float64, device=self.device)
+        self._check(self.lib.ato_ipm_errors(d, ctypes.byref(bd), *[_p(t) for t in ops[:12]], _p(ops[12]),
+                                            float(s_max), _p(work), _p(out), self._stream()), 'ato_ipm_errors')
+        return tuple(out)
+
+    def rhs(self, bd, x, s, g, c_rhs, gf, jty, y, zl, zu, vl, vu, mu, kappa_d):
+        ''' (Sx, Ss, gx, gs, rhs_x, rhs_s, rhs_y) '''
+        W = x.shape[1]
+        n, m, mi, me = self.n, self.m, self.mi, self.meq
+        d, _ = self.dims(W)
+        ops = [self._v(x, n, W), self._v(s, mi, W), self._v(g, m, W), self._v(c_rhs, me, W), self._v(gf, n, W),
+               self._v(jty, n, W), self._v(y, m, W), self._v(zl, n, W), self._v(zu, n, W), self._v(vl, mi, W),
+               self._v(vu, mi, W), self._c(mu, W)]
+        e = dict(dtype=torch.float64, device=self.device)
+        outs = [torch.empty((n, W), **e), torch.empty((mi, W), **e), torch.empty((n, W), **e),
+                torch.empty((mi, W), **e), torch.empty((n, W), **e), torch.empty((mi, W), **e),
+                torch.empty((m, W), **e)]
+        self._check(self.lib.ato_ipm_rhs(d, ctypes.byref(bd), *[_p(t) for t in ops], float(kappa_d),
+                                         *[_p(t) for t in outs], self._stream()), 'ato_ipm_rhs')
+        return tuple(outs)
+
+    def direction(self, bd, x, s, dx, ds, zl, zu, vl, vu, gx, gs, mu, tau):
+        ''' (dzl, dzu, dvl, dvu, alpha_max, alpha_z, gphi_d) '''
+        W = x.shape[1]
+        n, mi = self.n, self.mi
+        d, work = self.dims(W)
+        ops = [self._v(x, n, W), self._v(s, mi, W), self._v(dx, n, W), self._v(ds, mi, W), self._v(zl, n, W),
+               self._v(zu, n, W), self._v(vl, mi, W), self._v(vu, mi, W), self._v(gx, n, W), self._v(gs, mi, W),
+               self._c(mu, W), self._c(tau, W)]
+        e = dict(dtype=torch.float64, device=self.device)
+        dz = [torch.empty((n, W), **e), torch.empty((n, W), **e), torch.empty((mi, W), **e),
+              torch.empty((mi, W), **e)]
+        out = torch.empty((3, W), **e)
+        self._check(self.lib.ato_ipm_direction(d, ctypes.byref(bd), *[_p(t) for t in ops], *[_p(t) for t in dz],
+                                               _p(work), _p(out), self._stream()), 'ato_ipm_direction')
+        return (*dz, out[0], out[1], out[2])
+
+    def measures(self, bd, x, s, g, c_rhs, f, mu, kappa_d):
+        ''' (theta, phi) per column '''
+        W = x.shape[1]
+        d, work = self.dims(W)
+        ops = [self._v(x, self.n, W), self._v(s, self.mi, W), self._v(g, self.m, W), self._v(c_rhs, self.meq, W),
+               self._c(f, W), self._c(mu, W)]
+        out = torch.empty((2, W), dtype=torch.float64, device=self.device)
+        self._check(self.lib.ato_ipm_measures(d, ctypes.byref(bd), *[_p(t) for t in ops], float(kappa_d), _p(work),
+                                              _p(out), self._stream()), 'ato_ipm_measures')
+        return out[0], out[1]
+
+    def multipliers(self, bd, x, s, mu, az, kappa_sigma, zl, zu, vl, vu, dzl, dzu, dvl, dvu):
+        ''' updated (zl, zu, vl, vu): new tensors '''
+        W = x.shape[1]
+        n, mi = self.n, self.mi
+        d, _ = self.dims(W)
+        z = [self._v(zl, n, W).clone(), self._v(zu, n, W).clone(), self._v(vl, mi, W).clone(),
+             self._v(vu, mi, W).clone()]
+        ops = [self._v(x, n, W), self._v(s, mi, W), self._c(mu, W), self._c(az, W)]
+        dz = [self._v(dzl, n, W), self._v(dzu, n, W), self._v(dvl, mi, W), self._v(dvu, mi, W)]
+        self._check(self.lib.ato_ipm_multipliers(d, ctypes.byref(bd), *[_p(t) for t in ops], float(kappa_sigma),
+                                                 *[_p(t) for t in z], *[_p(t) for t in dz], self._stream()),
+                    'ato_ipm_multipliers')
+        return tuple(z)

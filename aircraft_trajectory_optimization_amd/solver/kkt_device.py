@@ -210,6 +210,9 @@ class _KKTView:
     def residual(self, H, J, dx, dr, x, rhs, stream=None):
         return _residual(self.base, self.cap, H, J, dx, dr, x, rhs, stream)
 
+    def view(self, count: int) -> '_KKTView':
+        return _KKTView(self.base, count)
+
     def solve(self, x, instances=None, stream=None):
         b = self.base
         if x.dtype != torch.float64 or x.shape != (self.plan.dim, self.cap) or not x.is_contiguous() or \

@@ -1,0 +1,90 @@
+/*
+ * ato_ipm.h -- fused column kernels of the batched interior-point iteration (part of libato.so).
+ *
+ * What it replaces. IPOPT (ca.nlpsol('solver', 'ipopt', ...), ref: drone3d/raceline/
+ * base_raceline.py:752-799) runs its iteration's vector algebra -- optimality errors, barrier
+ * gradient and right-hand side, fraction-to-the-boundary step sizes, filter measures, bound
+ * multiplier updates -- on host vectors of one instance. The batched solver
+ * (solver/batched_ipm.py) runs the same algebra for W instances ("columns") at once; each entry
+ * point below does one of those steps in one or two launches instead of tens of elementwise
+ * tensor operations, with per-column reductions in a fixed order (deterministic).
+ *
+ * Every vector is a DEVICE array in the interleaved layout [element][W]: element e of column b
+ * is at e * W + b. Per-column scalars (mu, tau, f, ...) are device arrays [W]. Bounds are
+ * +-infinity where absent; a bound is present where it is finite. The slack of inequality
+ * row iin[i] is s[i]. IEEE operations are evaluated in the order of the host formulas (no
+ * contraction), so elementwise outputs equal solver/batched_ipm.py's bit for bit; sums are
+ * taken chunk by chunk in a fixed order.
+ */
+#ifndef ATO_IPM_H
+#define ATO_IPM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ato_ipm_dims {
+    int32_t n;                 /* variables                                          */
+    int32_t m;                 /* constraint rows                                    */
+    int32_t mi;                /* inequality rows (slacks)                           */
+    int32_t meq;               /* equality rows                                      */
+    const int32_t* iin;        /* [mi] device: row of every slack                   */
+    const int32_t* ieq;        /* [meq] device: equality rows                       */
+    int32_t W;                 /* columns (instances)                                */
+} ato_ipm_dims;
+
+typedef struct ato_ipm_bounds {
+    const double* xL;          /* [n][W] variable bounds (relaxed)                  */
+    const double* xU;
+    const double* dL;          /* [mi][W] slack bounds (relaxed)                    */
+    const double* dU;
+} ato_ipm_bounds;
+
+/* doubles of workspace the reductions below need for these dimensions */
+size_t ato_ipm_work_size(const ato_ipm_dims* d);
+
+/* Optimality errors (IPOPT E_mu; batched_ipm.py _errors + the unscaled primal infeasibility).
+ * dual_x = grad f + J^T y - zl + zu. out [5][W] = (E_mu, dual inf, primal inf, complementarity
+ * inf, max |r / sg|) with r the constraint residual (g - c_rhs on equality rows, g - s on
+ * slack rows) and s_max, n_bounds [W] the scaling of E_mu. */
+int ato_ipm_errors(const ato_ipm_dims* d, const ato_ipm_bounds* bd, const double* x, const double* s,
+                   const double* g, const double* c_rhs, const double* sg, const double* y, const double* zl,
+                   const double* zu, const double* vl, const double* vu, const double* dual_x, const double* mu,
+                   const double* n_bounds, double s_max, double* work, double* out, void* stream);
+
+/* Barrier Newton system pieces (batched_ipm.py solve: Sx, Ss, _grad_phi, right-hand side):
+ * Sx [n][W], Ss [mi][W], gx [n][W], gs [mi][W], rhs_x = -(gx + jty) [n][W],
+ * rhs_s = -(gs - y[iin]) [mi][W], rhs_y = -r [m][W]. jty = J^T y. */
+int ato_ipm_rhs(const ato_ipm_dims* d, const ato_ipm_bounds* bd, const double* x, const double* s,
+                const double* g, const double* c_rhs, const double* gf, const double* jty, const double* y,
+                const double* zl, const double* zu, const double* vl, const double* vu, const double* mu,
+                double kappa_d, double* Sx, double* Ss, double* gx, double* gs, double* rhs_x, double* rhs_s,
+                double* rhs_y, void* stream);
+
+/* Bound multiplier steps and step sizes (IPOPT fraction to the boundary): dzl, dzu [n][W],
+ * dvl, dvu [mi][W]; out [3][W] = (alpha_max of (x, s), alpha_z of the multipliers, the
+ * directional derivative gx^T dx + gs^T ds). */
+int ato_ipm_direction(const ato_ipm_dims* d, const ato_ipm_bounds* bd, const double* x, const double* s,
+                      const double* dx, const double* ds, const double* zl, const double* zu, const double* vl,
+                      const double* vu, const double* gx, const double* gs, const double* mu, const double* tau,
+                      double* dzl, double* dzu, double* dvl, double* dvu, double* work, double* out, void* stream);
+
+/* Filter measures of a point: out [2][W] = (theta = sum |r|, barrier objective phi). */
+int ato_ipm_measures(const ato_ipm_dims* d, const ato_ipm_bounds* bd, const double* x, const double* s,
+                     const double* g, const double* c_rhs, const double* f, const double* mu, double kappa_d,
+                     double* work, double* out, void* stream);
+
+/* Accepted step of the bound multipliers (in place): z += az dz, then IPOPT's kappa_sigma
+ * safeguard against the slacks of the accepted (x, s). */
+int ato_ipm_multipliers(const ato_ipm_dims* d, const ato_ipm_bounds* bd, const double* x, const double* s,
+                        const double* mu, const double* az, double kappa_sigma, double* zl, double* zu, double* vl,
+                        double* vu, const double* dzl, const double* dzu, const double* dvl, const double* dvu,
+                        void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ATO_IPM_H */

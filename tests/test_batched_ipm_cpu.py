@@ -6,6 +6,7 @@ converge early must stay frozen while the others iterate.
 '''
 import numpy as np
 import pytest
+import torch
 
 from aircraft_trajectory_optimization_amd.solver.batched_ipm import BatchedInteriorPoint
 from aircraft_trajectory_optimization_amd.solver.ipm import InteriorPointSolver, IPMOptions
@@ -63,3 +64,26 @@ def test_nested_dissection_order_follows_single_instance(cfg):
         assert abs(int(res.iters[b]) - ref.iters) <= 5
         assert np.abs(x[:, b] - ref.x).max() <= 1e-6 * max(1.0, np.abs(ref.x).max())
 
+
+
+def test_compaction_follows_full_width_solve():
+    ''' once at most half of the columns still iterate, the solver carries only those (evaluator
+    subset, KKT view, gathered state): every instance's status, iteration count, solution,
+    multipliers and per-iteration history equal the full-width solve's '''
+    spec = product_spec(track='fig8', model='point', use_quat=False, frame='global', N=7, K=2)
+    B = 4
+    W = _instances(spec, B, seed=3)
+    W[3, :spec.N] *= 0.4                          # a slower instance: the others finish first
+    runs = []
+    for compact in (False, True):
+        ev = HostBatchEvaluator(spec, B)
+        solver = BatchedInteriorPoint(ev, HostBlockKKT(ev), spec.lbw, spec.ubw, IPMOptions(max_iter=200))
+        solver.compact = compact
+        runs.append((solver.solve(W), solver.history))
+    (r0, h0), (r1, h1) = runs
+    assert r0.stats['compactions'] == 0 and r1.stats['compactions'] >= 1
+    assert r0.status == r1.status
+    assert [int(i) for i in r0.iters] == [int(i) for i in r1.iters]
+    for a, b in ((r0.x, r1.x), (r0.lam_g, r1.lam_g), (r0.lam_x, r1.lam_x), (r0.f, r1.f)):
+        assert torch.allclose(a, b, rtol=1e-12, atol=1e-12)
+    assert h0.shape == h1.shape and np.allclose(h0, h1, rtol=1e-12, atol=1e-12)

@@ -61,3 +61,23 @@ def test_kkt_plan_desc_layout(tmp_path):
     out = [int(v) for v in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
     assert out[:-1] == [getattr(AtoKKTPlanDesc, n).offset for n in names]
     assert out[-1] == ctypes.sizeof(AtoKKTPlanDesc)
+
+
+def test_ipm_struct_layout(tmp_path):
+    ''' the ctypes mirrors of ato_ipm_dims / ato_ipm_bounds against the C compiler's layout '''
+    import subprocess
+    inc = os.path.dirname(HEADERS[0])
+    body = ''
+    for ct, cname in ((native.AtoIpmDims, 'ato_ipm_dims'), (native.AtoIpmBounds, 'ato_ipm_bounds')):
+        body += ''.join(f'    printf("%zu\\n", offsetof({cname}, {f[0]}));\n' for f in ct._fields_)
+        body += f'    printf("%zu\\n", sizeof({cname}));\n'
+    src = tmp_path / 'ipm_layout.c'
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "ato_ipm.h"\nint main(void) {\n' + body +
+                   '    return 0;\n}\n')
+    exe = tmp_path / 'ipm_layout'
+    subprocess.run(['gcc', '-I', inc, str(src), '-o', str(exe)], check=True)
+    out = [int(v) for v in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    want = []
+    for ct in (native.AtoIpmDims, native.AtoIpmBounds):
+        want += [getattr(ct, f[0]).offset for f in ct._fields_] + [ctypes.sizeof(ct)]
+    assert out == want
