@@ -259,25 +259,34 @@ __device__ __forceinline__ void lane_set(double (&y)[NQ], int p, double v, int l
 // ------------------------------------------------------------------------------------------
 // factorisation
 // ------------------------------------------------------------------------------------------
-// column k of the block into c[0 .. 32T): thread (ti, tj) owns rows 32I+ti and columns 32J+tj,
-// 32J+16+tj of every lower tile (I, J)
-template <int T>
-__device__ __forceinline__ void extract_column(const double (&a)[T * (T + 1) / 2][2], int k, int ti, int tj,
+// entry h of a per-thread register row, h wave-uniform (a select chain: no indexed registers)
+template <int NC>
+__device__ __forceinline__ double pick(const double (&v)[NC], int h) {
+    double x = v[0];
+#pragma unroll
+    for (int q = 1; q < NC; ++q) x = blend(x, v[q], h == q ? ~0ull : 0ull);
+    return x;
+}
+
+// column k of the block into c[0 .. 32T): thread (ti, tj) of a workgroup of 32 NTJ threads owns
+// rows 32I+ti and the NC = 32 / NTJ columns 32J + h NTJ + tj (h < NC) of every lower tile (I, J)
+template <int T, int NC>
+__device__ __forceinline__ void extract_column(const double (&a)[T * (T + 1) / 2][NC], int k, int ti, int tj,
                                                double* __restrict__ c) {
-    const int K = k >> 5, kk = k & 31, kt = k & 15;
-    const unsigned long long hm = (k & 16) ? ~0ull : 0ull;
+    constexpr int NTJ = 32 / NC;
+    const int K = k >> 5, kk = k & 31, kt = kk % NTJ, h = kk / NTJ;
 #pragma unroll
     for (int KK = 0; KK < T; ++KK) {
         if (K == KK) {
             if (tj == kt) {
 #pragma unroll
-                for (int I = KK; I < T; ++I) c[32 * I + ti] = blend(a[slot(I, KK)][0], a[slot(I, KK)][1], hm);
+                for (int I = KK; I < T; ++I) c[32 * I + ti] = pick<NC>(a[slot(I, KK)], h);
             }
             if (ti == kk) {
 #pragma unroll
                 for (int J = 0; J < KK; ++J) {
-                    c[32 * J + tj] = a[slot(KK, J)][0];
-                    c[32 * J + 16 + tj] = a[slot(KK, J)][1];
+#pragma unroll
+                    for (int q = 0; q < NC; ++q) c[32 * J + q * NTJ + tj] = a[slot(KK, J)][q];
                 }
             }
         }
@@ -293,9 +302,11 @@ __global__ void k_inertia_zero(int batch, const int* __restrict__ list, int* __r
     inertia[3 * b + 2] = 0;
 }
 
-// W: waves per SIMD the register allocation targets (the _w variant below)
-template <int T, int W>
-__global__ __launch_bounds__(FT) __attribute__((amdgpu_waves_per_eu(W))) void k_front_factor_w(Plan P, Vals V, int f0, int batch, const int* __restrict__ list,
+// W: waves per SIMD the register allocation targets; FTT: threads per (front, instance) --
+// 512 (16 column owners per tile row, two columns each) or, for fronts of at most two tiles,
+// one wave (2 column owners, 16 columns each: no workgroup barrier is more than a wave's)
+template <int T, int W, int FTT>
+__global__ __launch_bounds__(FTT) __attribute__((amdgpu_waves_per_eu(W))) void k_front_factor_w(Plan P, Vals V, int f0, int batch, const int* __restrict__ list,
                                                      double* __restrict__ Lst, int2* __restrict__ piv,
                                                      double* __restrict__ dinv, int2* __restrict__ sinfo,
                                                      double* __restrict__ CB, int* __restrict__ inertia) {
@@ -304,6 +315,8 @@ __global__ __launch_bounds__(FT) __attribute__((amdgpu_waves_per_eu(W))) void k_
     constexpr int NQ = (NP + 63) / 64;
     constexpr int NS = T * (T + 1) / 2;
     constexpr int SR = NP + 1;                   // strip row stride (odd: conflict-free reads)
+    constexpr int NTJ = FTT / 32;                // column owners per tile row
+    constexpr int NC = 32 / NTJ;                 // columns per thread and tile
     extern __shared__ double smem[];
     double* strip = smem;                        // [32][SR]
     double* colb = strip + 32 * SR;              // [2 parity][2 (k, r)][NP]
@@ -320,7 +333,7 @@ __global__ __launch_bounds__(FT) __attribute__((amdgpu_waves_per_eu(W))) void k_
     const int p0 = P.pos_ptr[f];
     const int A = P.pos_ptr[f + 1] - p0;
     const int own = P.n_own[f];
-    double a[NS][2];
+    double a[NS][NC];
     double* Lb = Lst + (long long)b * P.l_size + P.l_off[f];
     int2* pv = piv + (long long)b * P.dim + P.piv_off[f];
     double* dv = dinv + ((long long)b * P.dim + P.piv_off[f]) * 3;
@@ -328,45 +341,59 @@ __global__ __launch_bounds__(FT) __attribute__((amdgpu_waves_per_eu(W))) void k_
     long long loff = 0;                          // running offset in the front's column stream
     KST_DECL(f == ATO_KKT_STAMP_FRONT && blockIdx.y == 0)
 
-    // ---- original entries (positions and values) into registers
-    const int e0 = P.ent_ptr[f * MAXT], e1 = P.ent_ptr[(f + 1) * MAXT];
-    int epos[EPT];
-    double eval[EPT];
+    // ---- original entries (positions and values) into registers (512 threads: all at once;
+    // one wave: strip by strip from the per-strip entry ranges)
+    int epos[FTT == FT ? EPT : 1];
+    double eval[FTT == FT ? EPT : 1];
+    if constexpr (FTT == FT) {
+        const int e0 = P.ent_ptr[f * MAXT], e1 = P.ent_ptr[(f + 1) * MAXT];
 #pragma unroll
-    for (int q = 0; q < EPT; ++q) {
-        const int e = e0 + tid + q * FT;
-        epos[q] = -1;
-        eval[q] = 0.0;
-        if (e < e1) {
-            epos[q] = P.ent_pos[e];
-            const int2 sc = P.ent_src[e];
-            eval[q] = src_value(V, sc.x, b) + src_value(V, sc.y, b);
+        for (int q = 0; q < EPT; ++q) {
+            const int e = e0 + tid + q * FT;
+            epos[q] = -1;
+            eval[q] = 0.0;
+            if (e < e1) {
+                epos[q] = P.ent_pos[e];
+                const int2 sc = P.ent_src[e];
+                eval[q] = src_value(V, sc.x, b) + src_value(V, sc.y, b);
+            }
         }
     }
     // ---- assemble strip by strip
 #pragma unroll
     for (int I = 0; I < T; ++I) {
         if (32 * I < A) {
-            for (int i = tid; i < 32 * SR; i += FT) strip[i] = 0.0;
+            for (int i = tid; i < 32 * SR; i += FTT) strip[i] = 0.0;
             __syncthreads();
+            auto put = [&](int ep, double ev) {
+                const int pa = ep >> 16, pb = ep & 0xffff;
+                if (ep >= 0 && (pa >> 5) == I) {
+                    strip[(pa & 31) * SR + pb] = ev;
+                    if ((pb >> 5) == I && pa != pb) strip[(pb & 31) * SR + pa] = ev;
+                }
+            };
+            if constexpr (FTT == FT) {
 #pragma unroll
-            for (int q = 0; q < EPT; ++q) {
-                const int pa = epos[q] >> 16, pb = epos[q] & 0xffff;
-                if (epos[q] >= 0 && (pa >> 5) == I) {
-                    strip[(pa & 31) * SR + pb] = eval[q];
-                    if ((pb >> 5) == I && pa != pb) strip[(pb & 31) * SR + pa] = eval[q];
+                for (int q = 0; q < EPT; ++q) put(epos[q], eval[q]);
+            } else {
+                for (int e = P.ent_ptr[f * MAXT + I] + tid; e < P.ent_ptr[f * MAXT + I + 1]; e += FTT) {
+                    const int2 sc = P.ent_src[e];
+                    put(P.ent_pos[e], src_value(V, sc.x, b) + src_value(V, sc.y, b));
                 }
             }
             __syncthreads();
 #pragma unroll
             for (int J = 0; J <= I; ++J) {
-                a[slot(I, J)][0] = strip[ti * SR + 32 * J + tj];
-                a[slot(I, J)][1] = strip[ti * SR + 32 * J + 16 + tj];
+#pragma unroll
+                for (int q = 0; q < NC; ++q) a[slot(I, J)][q] = strip[ti * SR + 32 * J + q * NTJ + tj];
             }
             __syncthreads();
         } else {
 #pragma unroll
-            for (int J = 0; J <= I; ++J) a[slot(I, J)][0] = a[slot(I, J)][1] = 0.0;
+            for (int J = 0; J <= I; ++J) {
+#pragma unroll
+                for (int q = 0; q < NC; ++q) a[slot(I, J)][q] = 0.0;
+            }
         }
     }
     // ---- extend-add of the children's contribution blocks (fixed child order: deterministic)
@@ -376,20 +403,21 @@ __global__ __launch_bounds__(FT) __attribute__((amdgpu_waves_per_eu(W))) void k_
         const int tqc = P.pos_ptr[c + 1] - pc - oc;
         const int* pm = P.parent_pos + pc + oc;
         const double* cbc = CB + (long long)b * P.cb_size + P.cb_off[c];
-        for (int i = tid; i < NP; i += FT) inv[i] = -1;
+        for (int i = tid; i < NP; i += FTT) inv[i] = -1;
         __syncthreads();
-        for (int q = tid; q < tqc; q += FT) inv[pm[q]] = q;
+        for (int q = tid; q < tqc; q += FTT) inv[pm[q]] = q;
         __syncthreads();
         int qr[T];
 #pragma unroll
         for (int I = 0; I < T; ++I) qr[I] = inv[32 * I + ti];
 #pragma unroll
         for (int J = 0; J < T; ++J) {
-            const int q0 = inv[32 * J + tj], q1 = inv[32 * J + 16 + tj];
 #pragma unroll
-            for (int I = J; I < T; ++I) {
-                if (qr[I] >= 0 && q0 >= 0) a[slot(I, J)][0] += cbc[(long long)qr[I] * tqc + q0];
-                if (qr[I] >= 0 && q1 >= 0) a[slot(I, J)][1] += cbc[(long long)qr[I] * tqc + q1];
+            for (int h = 0; h < NC; ++h) {
+                const int qc = inv[32 * J + h * NTJ + tj];
+#pragma unroll
+                for (int I = J; I < T; ++I)
+                    if (qr[I] >= 0 && qc >= 0) a[slot(I, J)][h] += cbc[(long long)qr[I] * tqc + qc];
             }
         }
         __syncthreads();
@@ -410,7 +438,7 @@ __global__ __launch_bounds__(FT) __attribute__((amdgpu_waves_per_eu(W))) void k_
         const int k = kc;
         double* ck = colb + (par * 2 + 0) * NP;
         double* cr = colb + (par * 2 + 1) * NP;
-        extract_column<T>(a, k, ti, tj, ck);
+        extract_column<T, NC>(a, k, ti, tj, ck);
         lds_barrier();
         KST(1);                  // extract + barrier (waits for the slowest wave's update)
         // lambda = max_{i eligible, i != k} |A_ik| and its index r
@@ -440,7 +468,7 @@ __global__ __launch_bounds__(FT) __attribute__((amdgpu_waves_per_eu(W))) void k_
         } else if (fabs(akk) >= BK_ALPHA * lam) {
             type = 0;
         } else {
-            extract_column<T>(a, r, ti, tj, cr);
+            extract_column<T, NC>(a, r, ti, tj, cr);
             lds_barrier();
             unsigned key2 = 0u;
 #pragma unroll
@@ -536,11 +564,11 @@ __global__ __launch_bounds__(FT) __attribute__((amdgpu_waves_per_eu(W))) void k_
         for (int pass = 0; pass < npass; ++pass) {
             const double* cc = pass == 1 ? cr : c0p;
             const double f0 = pass == 1 ? i01 : i00, f1 = pass == 1 ? i11 : i01;
-            double cj[T][2];
+            double cj[T][NC];
 #pragma unroll
             for (int J = 0; J < T; ++J) {
-                cj[J][0] = cc[32 * J + tj];
-                cj[J][1] = cc[32 * J + 16 + tj];
+#pragma unroll
+                for (int h = 0; h < NC; ++h) cj[J][h] = cc[32 * J + h * NTJ + tj];
             }
 #pragma unroll
             for (int I = 0; I < T; ++I) {
@@ -549,8 +577,8 @@ __global__ __launch_bounds__(FT) __attribute__((amdgpu_waves_per_eu(W))) void k_
                     const double li = type == 1 ? x0 * f0 + cr[32 * I + ti] * f1 : x0 * i00;
 #pragma unroll
                     for (int J = 0; J <= I; ++J) {
-                        a[slot(I, J)][0] = fma(-li, cj[J][0], a[slot(I, J)][0]);
-                        a[slot(I, J)][1] = fma(-li, cj[J][1], a[slot(I, J)][1]);
+#pragma unroll
+                        for (int h = 0; h < NC; ++h) a[slot(I, J)][h] = fma(-li, cj[J][h], a[slot(I, J)][h]);
                     }
                 }
             }
@@ -575,8 +603,8 @@ __global__ __launch_bounds__(FT) __attribute__((amdgpu_waves_per_eu(W))) void k_
 #pragma unroll
             for (int J = 0; J <= I; ++J) {
 #pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const int i = 32 * I + ti, j = 32 * J + 16 * h + tj;
+                for (int h = 0; h < NC; ++h) {
+                    const int i = 32 * I + ti, j = 32 * J + h * NTJ + tj;
                     // diagonal tiles hold both (i, j) and (j, i), which differ by rounding:
                     // only the lower one writes (one writer per entry, deterministic)
                     if (i >= own && i < A && j >= own && j < A && (I != J || i >= j)) {
@@ -948,11 +976,23 @@ constexpr int CUS = 256;
 template <int T>
 int launch_factor_level(const ato_kkt* h, const Plan& P, const Vals& V, int f0, int nf, int batch, const int* list,
                         int* inertia, hipStream_t st) {
-    auto k = k_front_factor_w<T, 1>;
-    if constexpr (T == 6)
-        if ((long long)nf * batch > CUS) k = k_front_factor_w<T, 4>;
-    hipLaunchKernelGGL(k, dim3(nf, batch), dim3(FT), factor_lds<T>(), st, P, V, f0, batch, list,
-                       h->d_L, h->d_piv, h->d_dinv, h->d_sinfo, h->d_cb, inertia);
+    // fronts of at most two tiles in a level of many workgroups: one wave each (throughput; B = 512
+    // factorisation 27.0 -> 24.8 ms); few workgroups (small batches): 512 threads each, whose
+    // shorter pivot steps set the latency (B = 1: 0.76 ms vs 0.87 ms with one wave)
+    bool one_wave = false;
+    if constexpr (T <= 2) {
+        one_wave = (long long)nf * batch >= 4 * CUS;
+        if (one_wave)
+            hipLaunchKernelGGL((k_front_factor_w<T, 1, 64>), dim3(nf, batch), dim3(64), factor_lds<T>(), st, P, V,
+                               f0, batch, list, h->d_L, h->d_piv, h->d_dinv, h->d_sinfo, h->d_cb, inertia);
+    }
+    if (!one_wave) {
+        auto k = k_front_factor_w<T, 1, FT>;
+        if constexpr (T == 6)
+            if ((long long)nf * batch > CUS) k = k_front_factor_w<T, 4, FT>;
+        hipLaunchKernelGGL(k, dim3(nf, batch), dim3(FT), factor_lds<T>(), st, P, V, f0, batch, list,
+                           h->d_L, h->d_piv, h->d_dinv, h->d_sinfo, h->d_cb, inertia);
+    }
     KKT_HIP(hipGetLastError());
     return ATO_OK;
 }

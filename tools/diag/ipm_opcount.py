@@ -55,9 +55,13 @@ rng = np.random.default_rng(0)
 W = np.repeat(spec.w0[None], B, axis=0)
 for b in range(1, B):
     W[b, :spec.N] *= 1 + 0.1 * rng.uniform(-1, 1, spec.N)
-ev = HostBatchEvaluator(spec, B)
+if '--device' in sys.argv:             # the device solver (fused kernels, ctypes calls not counted)
+    solver = batched_ipm.device_solver(spec, B, spec.lbw, spec.ubw, IPMOptions(max_iter=200))
+else:
+    ev = HostBatchEvaluator(spec, B)
+    solver = batched_ipm.BatchedInteriorPoint(ev, HostBlockKKT(ev), spec.lbw, spec.ubw, IPMOptions(max_iter=200))
 with Count():
-    res = batched_ipm.BatchedInteriorPoint(ev, HostBlockKKT(ev), spec.lbw, spec.ubw, IPMOptions(max_iter=200)).solve(W)
+    res = solver.solve(W)
 it = int(max(res.iters))
 tot = sum(COUNT.values())
 print(f'lockstep iterations ~{it}, operators {tot} ({tot / max(it, 1):.0f} per iteration)')
