@@ -593,10 +593,12 @@ class BatchedInteriorPoint:
                'lam_g': torch.zeros((m, B0), dtype=torch.float64, device=dev),
                'lam_x': torch.zeros((n, B0), dtype=torch.float64, device=dev),
                'status': torch.zeros(B0, dtype=torch.long, device=dev),
-               'iters': torch.zeros(B0, dtype=torch.long, device=dev)}
+               'iters': torch.zeros(B0, dtype=torch.long, device=dev),
+               'n_resto': torch.zeros(B0, dtype=torch.long, device=dev)}
         hist_row = torch.zeros((6, B0), dtype=torch.float64, device=dev)
 
-        def save(cols_, x_, y_, zl_, zu_, status_, iters_):
+        def save(cols_, x_, y_, zl_, zu_, status_, iters_, n_resto_):
+            out['n_resto'][cols_] = n_resto_
             out['x'][:, cols_] = x_
             out['lam_g'][:, cols_] = y_ * self.sg / self.sf
             out['lam_x'][:, cols_] = (zu_ - zl_) / self.sf
@@ -620,7 +622,7 @@ class BatchedInteriorPoint:
                 live = act | waiting
                 n_live = int(live.sum())
                 if 0 < n_live <= B // 2:
-                    save(cols, x, y, zl, zu, status, iters)
+                    save(cols, x, y, zl, zu, status, iters, n_resto)
                     sel = torch.nonzero(live).reshape(-1)
                     (x, s, f, g, gf, jv, y, zl, zu, vl, vu, mu, tau, nf, dwl, n_acc, status, n_resto, own, waiting,
                      iters, act) = self._compact(sel, (x, s, f, g, gf, jv, y, zl, zu, vl, vu, mu, tau, nf, dwl, n_acc,
@@ -855,8 +857,8 @@ class BatchedInteriorPoint:
                         act = act | okr
                 laps.lap('resto_post')
 
-        save(cols, x, y, zl, zu, status, iters)
-        self.stats['restorations'] = self.stats.get('restorations', 0) + int(n_resto.sum())
+        save(cols, x, y, zl, zu, status, iters, n_resto)
+        self.stats['restorations'] = self.stats.get('restorations', 0) + int(out['n_resto'].sum())
         for k_, v_ in keep.items():                 # back to the full batch
             setattr(self, k_, v_)
         x = out['x']
