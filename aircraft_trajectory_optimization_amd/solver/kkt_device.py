@@ -150,6 +150,10 @@ class DeviceKKT:
         ''' rhs - K x for every instance (x, rhs [dim][max_batch]); iterative-refinement residual '''
         return _residual(self, self.cap, H, J, dx, dr, x, rhs, stream)
 
+    def fork(self) -> 'DeviceKKT':
+        ''' a second factorisation with its own storage (the asynchronous restoration phase) '''
+        return DeviceKKT(self.plan, self.cap, self.device)
+
     def view(self, count: int) -> '_KKTView':
         ''' the same factor storage driven with [element][count] value arrays (instances 0 .. count-1
         of the view's own numbering use storage slots 0 .. count-1): the restoration phase runs

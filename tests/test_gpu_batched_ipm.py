@@ -109,3 +109,30 @@ def test_batched_device_solve_is_deterministic():
     r2 = device_solver(spec, 2, spec.lbw, spec.ubw, opts).solve(W)
     assert torch.equal(r1.x, r2.x)
     assert [int(i) for i in r1.iters] == [int(i) for i in r2.iters]
+
+
+def test_asynchronous_restoration_matches_synchronous():
+    ''' restoration phases in the worker thread (own stream, library handle and KKT storage) while
+    the other instances iterate: every instance ends with the status, iteration count and
+    solution of the synchronous solve (an instance's iterates do not depend on when its
+    restoration runs) '''
+    from aircraft_trajectory_optimization_amd.solver.batched_ipm import device_solver
+    from aircraft_trajectory_optimization_amd.tracks import make_spec
+    spec = make_spec(track='race', N=5, K=2)
+    B = 24
+    rng = np.random.default_rng(4)
+    W = np.repeat(spec.w0[None], B, axis=0)
+    for b in range(B):
+        W[b, :spec.N] *= 1 + 0.1 * rng.uniform(-1, 1, spec.N)
+    opts = IPMOptions(max_iter=150)
+    runs = []
+    for asynchronous in (False, True):
+        sol = device_solver(spec, B, spec.lbw, spec.ubw, opts)
+        sol.async_restoration = asynchronous
+        runs.append(sol.solve(W))
+    r0, r1 = runs
+    assert r1.stats.get('async_phases', 0) > 0 and 'async_phases' not in r0.stats
+    assert r0.stats['restorations'] > 0 and r0.stats['restorations'] == r1.stats['restorations']
+    assert r0.status == r1.status
+    assert [int(i) for i in r0.iters] == [int(i) for i in r1.iters]
+    assert torch.allclose(r0.x, r1.x, rtol=1e-9, atol=1e-9)
