@@ -606,8 +606,8 @@ class BatchedInteriorPoint:
         # stream, library handle and KKT storage while the other columns keep iterating; its
         # columns wait (frozen) until it is collected. Waiting does not change an instance's own
         # trajectory, so this changes when a restored instance resumes, not what it computes.
-        inflight = None                              # the phase in flight
-        infl = torch.zeros(B, dtype=torch.bool, device=dev)   # its columns
+        inflight = []                                # the phases in flight (at most ASYNC_PHASES)
+        infl = torch.zeros(B, dtype=torch.bool, device=dev)   # their columns
         use_async = (self.async_restoration and stop_check is None and self.vk is not None and can_compact
                      and hasattr(keep['ev'], 'fork') and hasattr(keep['kkt'], 'fork'))
 
@@ -675,7 +675,7 @@ class BatchedInteriorPoint:
             mx = act & (own >= o.max_iter)
             status = torch.where(mx, torch.full_like(status, MAX_ITER), status)
             act = act & ~mx
-            if not bool(act.any()) and not bool(waiting.any()) and inflight is None:
+            if not bool(act.any()) and not bool(waiting.any()) and not inflight:
                 break
             laps.lap('check')
             stepping = act.clone()
@@ -839,12 +839,20 @@ class BatchedInteriorPoint:
             act = act & ~resto
             n_act, n_wait = int(act.sum()), int(waiting.sum())
             done = None                              # (restored columns, their x, success) of a finished phase
-            if inflight is not None and (n_act == 0 or inflight['future'].done()):
-                R, xr, okr = self._resto_collect(inflight, cols, x, B0)
-                done = (R, xr, okr)
-                infl = infl & False
-                inflight = None
-            if done is None and inflight is None and n_wait and \
+            if inflight:
+                ready = [j for j in inflight if j['future'].done()]
+                if not ready and n_act == 0 and (not n_wait or len(inflight) >= self.ASYNC_PHASES):
+                    # nothing else can progress: wait for one
+                    import concurrent.futures as cf
+                    cf.wait([j['future'] for j in inflight], return_when=cf.FIRST_COMPLETED)
+                    ready = [j for j in inflight if j['future'].done()]
+                if ready:
+                    j = ready[0]
+                    inflight.remove(j)
+                    R, xr, okr = self._resto_collect(j, cols, x, B0)
+                    done = (R, xr, okr)
+                    infl = infl & ~R
+            if done is None and len(inflight) < self.ASYNC_PHASES and n_wait and \
                     (n_act == 0 or n_wait >= max(1, n_act // 8) or it % 10 == 9):
                 R = waiting.clone()
                 waiting = waiting & False
@@ -856,8 +864,8 @@ class BatchedInteriorPoint:
                     theta_w, phi_w = self._measures(x, s, g, f, mu)
                     add_filter(can, theta_w, phi_w)
                     if use_async and n_act >= 8:
-                        inflight = self._resto_launch(can, x, g, mu, theta_w, F, nf, cols, keep)
-                        infl = can.clone()
+                        inflight.append(self._resto_launch(can, x, g, mu, theta_w, F, nf, cols, keep, inflight))
+                        infl = infl | can
                     else:
                         xr, okr = self._restore(can, x, g, mu, theta_w, F, nf)
                         done = (can, xr, okr)
@@ -886,8 +894,8 @@ class BatchedInteriorPoint:
                     act = act | okr
                 laps.lap('resto_post')
 
-        if inflight is not None:                     # (the lockstep bound ended the loop first)
-            self._resto_collect(inflight, cols, x, B0)
+        for j in inflight:                           # (the lockstep bound ended the loop first)
+            self._resto_collect(j, cols, x, B0)
         if getattr(self, '_async_pool', None) is not None:
             self._async_pool.shutdown(wait=True)
             self._async_pool = None
@@ -1038,18 +1046,26 @@ class BatchedInteriorPoint:
         xr = torch.minimum(torch.maximum(res.x[:n], view.xL), view.xU)
         return xr, stopped, stats, dict(sub.laps.t)
 
-    def _resto_launch(self, R, x, g, mu, theta, F, nf, cols, keep):
-        ''' start the restoration of columns R in the worker thread (own stream, library handle, KKT
-        storage, kernels): inputs gathered here on the current stream '''
+    ASYNC_PHASES = 3                # restoration phases in flight at once (each: own handle, storage, stream)
+
+    def _resto_launch(self, R, x, g, mu, theta, F, nf, cols, keep, inflight):
+        ''' start the restoration of columns R in a worker thread (own stream, library handle, KKT
+        storage, kernels, not used by another phase in flight): inputs gathered here on the
+        current stream '''
         from concurrent.futures import ThreadPoolExecutor
         from aircraft_trajectory_optimization_amd.solver.ipm_device import DeviceIPMKernels
-        res = getattr(self, '_async_res', None)
+        sets = getattr(self, '_async_res', None)
+        if sets is None:
+            sets = self._async_res = []
+        busy = [id(j['res']) for j in inflight]
+        res = next((r for r in sets if id(r) not in busy), None)
         if res is None:
-            res = self._async_res = {'ev': keep['ev'].fork(), 'kkt': keep['kkt'].fork(),
-                                     'vk': DeviceIPMKernels(self.n, self.m, self.iin, self.ieq, self.dev),
-                                     'stream': torch.cuda.Stream(self.dev)}
+            res = {'ev': keep['ev'].fork(), 'kkt': keep['kkt'].fork(),
+                   'vk': DeviceIPMKernels(self.n, self.m, self.iin, self.ieq, self.dev),
+                   'stream': torch.cuda.Stream(self.dev)}
+            sets.append(res)
         if getattr(self, '_async_pool', None) is None:
-            self._async_pool = ThreadPoolExecutor(max_workers=1)
+            self._async_pool = ThreadPoolExecutor(max_workers=self.ASYNC_PHASES)
         job = self._resto_prepare(R, x, g, mu, theta, F, nf)
         job['orig'] = cols.index_select(0, job['sel'])
         self.stats['async_phases'] = self.stats.get('async_phases', 0) + 1
@@ -1064,7 +1080,7 @@ class BatchedInteriorPoint:
                 fin = torch.cuda.Event()
                 fin.record(st)
             return out, fin
-        return {'future': self._async_pool.submit(work), 'job': job}
+        return {'future': self._async_pool.submit(work), 'job': job, 'res': res}
 
     def _resto_collect(self, inflight, cols, x, B0):
         ''' wait for a restoration phase and map it to the current columns: (restored columns mask,
