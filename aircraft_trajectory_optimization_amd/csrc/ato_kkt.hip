@@ -51,6 +51,7 @@ struct ato_kkt {
     int2* d_piv = nullptr;           // [cap][dim] {p | type << 16, r}
     double* d_dinv = nullptr;        // [cap][dim][3]
     int2* d_sinfo = nullptr;         // [cap][F] {steps, used stream length of the front}
+    int32_t* d_spec = nullptr;       // [cap][dim] second column Bunch-Kaufman took for an own position last time
 };
 
 #ifdef ATO_KKT_STAMPS
@@ -78,8 +79,11 @@ int fail(int code, const std::string& m) {
 constexpr int FT = 512;                   // factor threads per (front, instance) (16 x 32 grid)
 constexpr int ST = 256;                   // solve threads per (front, instance)
 constexpr int EPT = 8;                    // entries per thread and front (<= 4096 per front)
+#ifndef ATO_KKT_SPEC
+#define ATO_KKT_SPEC 0
+#endif
 #ifndef ATO_KKT_CH
-#define ATO_KKT_CH 1024     // 16 KB ring: 5 solve workgroups per CU (64 KB: 2); B = 512 solve 11.1 -> 4.2 ms
+#define ATO_KKT_CH 512      // 8 KB ring: B = 512 solve 3.28 -> 3.01 ms against 16 KB (64 KB: 11.1 ms); B = 1 0.37 -> 0.38 ms
 #endif
 constexpr int CH = ATO_KKT_CH;            // doubles per ring chunk of the solve (2 x CH x 8 B LDS ring)
 constexpr int CPT = CH / ST;              // chunk doubles per thread
@@ -309,7 +313,8 @@ template <int T, int W, int FTT>
 __global__ __launch_bounds__(FTT) __attribute__((amdgpu_waves_per_eu(W))) void k_front_factor_w(Plan P, Vals V, int f0, int batch, const int* __restrict__ list,
                                                      double* __restrict__ Lst, int2* __restrict__ piv,
                                                      double* __restrict__ dinv, int2* __restrict__ sinfo,
-                                                     double* __restrict__ CB, int* __restrict__ inertia) {
+                                                     double* __restrict__ CB, int* __restrict__ inertia,
+                                                     int* __restrict__ spec) {
     constexpr int NP = 32 * T;
     constexpr int NW = (NP + 63) / 64;
     constexpr int NQ = (NP + 63) / 64;
@@ -321,6 +326,7 @@ __global__ __launch_bounds__(FTT) __attribute__((amdgpu_waves_per_eu(W))) void k
     double* strip = smem;                        // [32][SR]
     double* colb = strip + 32 * SR;              // [2 parity][2 (k, r)][NP]
     int* inv = reinterpret_cast<int*>(colb + 4 * NP);   // [NP] position -> child trailing index
+    int* s_spec = inv + NP;                              // [NP] guessed second column per own position
 
     const int f = f0 + blockIdx.x;
     const int bi = blockIdx.y;
@@ -337,6 +343,9 @@ __global__ __launch_bounds__(FTT) __attribute__((amdgpu_waves_per_eu(W))) void k
     double* Lb = Lst + (long long)b * P.l_size + P.l_off[f];
     int2* pv = piv + (long long)b * P.dim + P.piv_off[f];
     double* dv = dinv + ((long long)b * P.dim + P.piv_off[f]) * 3;
+    int* sp = spec + (long long)b * P.dim + P.piv_off[f];
+    if (ATO_KKT_SPEC)
+        for (int i = tid; i < own; i += FTT) s_spec[i] = sp[i];
     int npos = 0, nneg = 0, nzero = 0;
     long long loff = 0;                          // running offset in the front's column stream
     KST_DECL(f == ATO_KKT_STAMP_FRONT && blockIdx.y == 0)
@@ -439,6 +448,13 @@ __global__ __launch_bounds__(FTT) __attribute__((amdgpu_waves_per_eu(W))) void k
         double* ck = colb + (par * 2 + 0) * NP;
         double* cr = colb + (par * 2 + 1) * NP;
         extract_column<T, NC>(a, k, ti, tj, ck);
+        // speculative second column (ATO_KKT_SPEC): the r Bunch-Kaufman took for k in this storage
+        // slot's previous factorisation, extracted with column k -- a right guess saves the second
+        // barrier and changes nothing else. Measured: B = 512 24.8 -> 25.7 ms, B = 1 0.77 -> 0.81 ms
+        // (the extra extraction on every guessed step costs more than the barriers it saves); off.
+        const int sr = ATO_KKT_SPEC ? __builtin_amdgcn_readfirstlane(s_spec[k]) : -1;
+        const bool spec_ok = ATO_KKT_SPEC && sr >= 0 && sr < own && sr != k && live.get(sr);
+        if (spec_ok) extract_column<T, NC>(a, sr, ti, tj, cr);
         lds_barrier();
         KST(1);                  // extract + barrier (waits for the slowest wave's update)
         // lambda = max_{i eligible, i != k} |A_ik| and its index r
@@ -451,7 +467,11 @@ __global__ __launch_bounds__(FTT) __attribute__((amdgpu_waves_per_eu(W))) void k
             cv[q] = ck[i];
             if (i < own && i != k && lvq[q]) key = max(key, mag_key(cv[q], i));
         }
+#ifdef ATO_KKT_X_NOSEARCH     // DIAGNOSTIC timing only: no pivot search (results wrong)
+        key = 0u;
+#else
         key = wave_max_u32(key);
+#endif
         KST(5);                  // column read, magnitude keys, DPP max
         const int r = key ? 511 - (int)(key & 0x1FFu) : -1;
         const double akk = lane_pick<NQ>(cv, k);
@@ -467,9 +487,16 @@ __global__ __launch_bounds__(FTT) __attribute__((amdgpu_waves_per_eu(W))) void k
             type = akk == 0.0 ? 2 : 0;
         } else if (fabs(akk) >= BK_ALPHA * lam) {
             type = 0;
+#ifdef ATO_KKT_X_NOR            // DIAGNOSTIC timing only: never the second column (results wrong)
+        } else if (true) {
+            type = 0;
+#endif
         } else {
-            extract_column<T, NC>(a, r, ti, tj, cr);
-            lds_barrier();
+            if (!(spec_ok && r == sr)) {
+                extract_column<T, NC>(a, r, ti, tj, cr);
+                lds_barrier();
+            }
+            if (ATO_KKT_SPEC && tid == 0 && r != sr) sp[k] = r;
             unsigned key2 = 0u;
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
@@ -541,7 +568,11 @@ __global__ __launch_bounds__(FTT) __attribute__((amdgpu_waves_per_eu(W))) void k
         // from LDS rather than held in registers across the decision (frees the registers for a
         // second workgroup per CU).
         const double* c0p = use_r ? cr : ck;     // column p (1x1) or k (2x2)
+#ifdef ATO_KKT_X_NOSTORE      // DIAGNOSTIC timing only: no factor-column stores
+        if (false) {
+#else
         if (lvt) {
+#endif
             const int ci = cit;
             const double x0 = c0p[tid];
             if (type == 0) {
@@ -557,28 +588,33 @@ __global__ __launch_bounds__(FTT) __attribute__((amdgpu_waves_per_eu(W))) void k
         loff += (long long)nlive * ncol;
         KST(3);                  // pivot inverse, record, factor-column stores
         // Schur update: one rank-1 pass (1x1 pivot) or two (2x2 pivot), A -= l c^T with c the
-        // pivot column (pass 0: c0, pass 1: cr); tiles of dead rows are skipped, dead column
-        // tiles are updated too (skipping them per tile costs the compiler a select per entry:
-        // measured 2x slower)
+        // pivot column (pass 0: c0, pass 1: cr)
+#ifdef ATO_KKT_X_NOUPDATE     // DIAGNOSTIC timing only: no Schur update (results wrong)
+        const int npass = 0;
+#else
         const int npass = type == 0 ? 1 : type == 1 ? 2 : 0;
+#endif
         for (int pass = 0; pass < npass; ++pass) {
             const double* cc = pass == 1 ? cr : c0p;
             const double f0 = pass == 1 ? i01 : i00, f1 = pass == 1 ? i11 : i01;
-            double cj[T][NC];
-#pragma unroll
-            for (int J = 0; J < T; ++J) {
-#pragma unroll
-                for (int h = 0; h < NC; ++h) cj[J][h] = cc[32 * J + h * NTJ + tj];
-            }
+            // column-tile outer loop: column tiles without a live position are skipped (a uniform branch
+            // around a whole tile column; B = 512 24.8 -> 23.2 ms). Dead entries are never read again.
+            double li[T];
 #pragma unroll
             for (int I = 0; I < T; ++I) {
-                if (live.any_in_tile(I)) {
-                    const double x0 = c0p[32 * I + ti];
-                    const double li = type == 1 ? x0 * f0 + cr[32 * I + ti] * f1 : x0 * i00;
+                const double x0 = c0p[32 * I + ti];
+                li[I] = type == 1 ? x0 * f0 + cr[32 * I + ti] * f1 : x0 * i00;
+            }
 #pragma unroll
-                    for (int J = 0; J <= I; ++J) {
+            for (int J = 0; J < T; ++J) {
+                if (live.any_in_tile(J)) {
+                    double cj[NC];
 #pragma unroll
-                        for (int h = 0; h < NC; ++h) a[slot(I, J)][h] = fma(-li, cj[J][h], a[slot(I, J)][h]);
+                    for (int h = 0; h < NC; ++h) cj[h] = cc[32 * J + h * NTJ + tj];
+#pragma unroll
+                    for (int I = J; I < T; ++I) {
+#pragma unroll
+                        for (int h = 0; h < NC; ++h) a[slot(I, J)][h] = fma(-li[I], cj[h], a[slot(I, J)][h]);
                     }
                 }
             }
@@ -964,7 +1000,7 @@ __global__ __launch_bounds__(256) void k_kkt_residual(int dim, int batch, const 
 template <int T>
 size_t factor_lds() {
     constexpr int NP = 32 * T;
-    return sizeof(double) * (32 * (NP + 1) + 4 * NP) + sizeof(int) * NP;
+    return sizeof(double) * (32 * (NP + 1) + 4 * NP) + sizeof(int) * 2 * NP;
 }
 
 // Six-tile fronts hold 138 VGPRs: one 512-thread workgroup per CU. Allocated for four waves per
@@ -984,14 +1020,15 @@ int launch_factor_level(const ato_kkt* h, const Plan& P, const Vals& V, int f0, 
         one_wave = (long long)nf * batch >= 4 * CUS;
         if (one_wave)
             hipLaunchKernelGGL((k_front_factor_w<T, 1, 64>), dim3(nf, batch), dim3(64), factor_lds<T>(), st, P, V,
-                               f0, batch, list, h->d_L, h->d_piv, h->d_dinv, h->d_sinfo, h->d_cb, inertia);
+                               f0, batch, list, h->d_L, h->d_piv, h->d_dinv, h->d_sinfo, h->d_cb, inertia,
+                               h->d_spec);
     }
     if (!one_wave) {
         auto k = k_front_factor_w<T, 1, FT>;
         if constexpr (T == 6)
             if ((long long)nf * batch > CUS) k = k_front_factor_w<T, 4, FT>;
         hipLaunchKernelGGL(k, dim3(nf, batch), dim3(FT), factor_lds<T>(), st, P, V, f0, batch, list,
-                           h->d_L, h->d_piv, h->d_dinv, h->d_sinfo, h->d_cb, inertia);
+                           h->d_L, h->d_piv, h->d_dinv, h->d_sinfo, h->d_cb, inertia, h->d_spec);
     }
     KKT_HIP(hipGetLastError());
     return ATO_OK;
@@ -1088,8 +1125,9 @@ int upload(const V* host, size_t n, V** dev) {
 
 void free_storage(ato_kkt* h) {
     for (void* p : {(void*)h->d_L, (void*)h->d_cb, (void*)h->d_sc, (void*)h->d_piv, (void*)h->d_dinv,
-                    (void*)h->d_sinfo})
+                    (void*)h->d_sinfo, (void*)h->d_spec})
         (void)hipFree(p);
+    h->d_spec = nullptr;
     h->d_L = nullptr;
     h->d_cb = nullptr;
     h->d_sc = nullptr;
@@ -1206,6 +1244,8 @@ int ato_kkt_reserve(ato_kkt* h, int32_t max_batch) {
     KKT_HIP(hipMalloc((void**)&h->d_piv, sizeof(int2) * (size_t)h->dim * B));
     KKT_HIP(hipMalloc((void**)&h->d_dinv, sizeof(double) * 3 * (size_t)h->dim * B));
     KKT_HIP(hipMalloc((void**)&h->d_sinfo, sizeof(int2) * (size_t)h->F * B));
+    KKT_HIP(hipMalloc((void**)&h->d_spec, sizeof(int32_t) * (size_t)h->dim * B));
+    KKT_HIP(hipMemset(h->d_spec, 0xFF, sizeof(int32_t) * (size_t)h->dim * B));     // -1: no guess
     h->cap = max_batch;
     return ATO_OK;
 }
