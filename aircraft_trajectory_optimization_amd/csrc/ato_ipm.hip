@@ -430,6 +430,57 @@ bool make_dev(const ato_ipm_dims* d, const ato_ipm_bounds* bd, Dev& v) {
 dim3 col_grid(int W, int NC) { return dim3((W + CB - 1) / CB, NC); }
 unsigned lin_blocks(long long cnt) { return (unsigned)((cnt + 255) / 256); }
 
+// ------------------------------------------------------------------------------------------
+// filter acceptance of a trial point (batched_ipm.py _accept), one thread per column
+// ------------------------------------------------------------------------------------------
+// torch.pow(tensor, scalar) on the device: its special exponents, std::pow otherwise
+__device__ __forceinline__ double tpow(double x, double e) {
+    if (e == 2.0) return x * x;
+    if (e == 3.0) return x * x * x;
+    if (e == 0.5) return sqrt(x);
+    if (e == 1.0) return x;
+    return pow(x, e);
+}
+
+struct FilterPrm {
+    double s_phi, s_theta, delta, eta_phi, gamma_theta, gamma_phi;
+};
+
+__global__ __launch_bounds__(CB) void k_filter_accept(int W, int fmax, const double* __restrict__ theta,
+                                                      const double* __restrict__ phi,
+                                                      const double* __restrict__ gphi_d,
+                                                      const double* __restrict__ alpha,
+                                                      const double* __restrict__ tht, const double* __restrict__ pht,
+                                                      const double* __restrict__ F, const int64_t* __restrict__ nf,
+                                                      const double* __restrict__ theta_max,
+                                                      const double* __restrict__ theta_min,
+                                                      const uint8_t* __restrict__ pend,
+                                                      const uint8_t* __restrict__ first, FilterPrm o,
+                                                      uint8_t* __restrict__ ok_out, uint8_t* __restrict__ arm_out,
+                                                      uint8_t* __restrict__ soc_out) {
+    const int b = blockIdx.x * CB + threadIdx.x;
+    if (b >= W) return;
+    const double th = theta[b], ph = phi[b], gd = gphi_d[b], al = alpha[b], tt = tht[b], pt = pht[b];
+    const bool rej = !(tt <= theta_max[b]);
+    bool in_f = false;
+    const long long k1 = nf[b];
+    const double* Fb = F + (long long)b * fmax * 2;
+    const int kn = (int)(k1 < fmax ? k1 : fmax);
+    for (int k = 0; k < kn; ++k)
+        if (tt >= Fb[2 * k] && pt >= Fb[2 * k + 1]) in_f = true;
+    const double ngd = -gd;
+    const double mgd = ngd != ngd ? ngd : (ngd < 0.0 ? 0.0 : ngd);      // torch.clamp(min=0): NaN stays
+    const bool switching = (gd < 0.0) && (al * tpow(mgd, o.s_phi) > o.delta * tpow(th, o.s_theta));
+    const bool arm_case = (th <= theta_min[b]) && switching;
+    const bool ok_arm = pt <= ph + (o.eta_phi * al) * gd;
+    const bool ok_suf = (tt <= (1.0 - o.gamma_theta) * th) || (pt <= ph - o.gamma_phi * th);
+    const bool pd = pend[b] != 0;
+    const bool ok = pd && !rej && !in_f && (arm_case ? ok_arm : ok_suf);
+    ok_out[b] = ok ? 1 : 0;
+    arm_out[b] = (ok && arm_case) ? 1 : 0;
+    soc_out[b] = (pd && !ok && first[b] != 0 && tt >= th) ? 1 : 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -512,6 +563,23 @@ int ato_ipm_multipliers(const ato_ipm_dims* d, const ato_ipm_bounds* bd, const d
         hipLaunchKernelGGL(k_multipliers, dim3(lin_blocks(cnt)), dim3(256), 0, st, v, x, s, mu, az, kappa_sigma, zl,
                            zu, vl, vu, dzl, dzu, dvl, dvu);
     return check_launch("ato_ipm_multipliers");
+}
+
+int ato_ipm_filter_accept(int32_t W, int32_t fmax, const double* theta, const double* phi, const double* gphi_d,
+                          const double* alpha, const double* tht, const double* pht, const double* F,
+                          const int64_t* nf, const double* theta_max, const double* theta_min,
+                          const uint8_t* pend, const uint8_t* first, const double* prm, uint8_t* ok,
+                          uint8_t* arm, uint8_t* soc, void* stream) {
+    if (W < 0 || fmax < 0 || !prm) return fail(ATO_ERR_ARG, "ato_ipm_filter_accept: arguments");
+    if (W == 0) return 0;
+    if (!theta || !phi || !gphi_d || !alpha || !tht || !pht || (fmax && !F) || !nf || !theta_max || !theta_min ||
+        !pend || !first || !ok || !arm || !soc)
+        return fail(ATO_ERR_ARG, "ato_ipm_filter_accept: arguments");
+    const FilterPrm o{prm[0], prm[1], prm[2], prm[3], prm[4], prm[5]};
+    hipLaunchKernelGGL(k_filter_accept, dim3((W + CB - 1) / CB), dim3(CB), 0, static_cast<hipStream_t>(stream), W,
+                       fmax, theta, phi, gphi_d, alpha, tht, pht, F, nf, theta_max, theta_min, pend, first, o, ok,
+                       arm, soc);
+    return check_launch("ato_ipm_filter_accept");
 }
 
 }  // extern "C"

@@ -84,6 +84,13 @@ class BatchedDeviceEvaluator:
         self.counts['eval'] += 1
         return self.bn.f.clone(), self.bn.g.clone(), self.bn.grad_f.clone(), self.bn.jac.clone()
 
+    def eval_fg(self, X: torch.Tensor):
+        ''' f and g only (no Jacobian written): the line search's trial points '''
+        self.bn.w.copy_(X)
+        self.bn.evaluate(jac=False)
+        self.counts['eval'] += 1
+        return self.bn.f.clone(), self.bn.g.clone()
+
     def hess(self, X: torch.Tensor, lam: torch.Tensor, sigma: torch.Tensor) -> torch.Tensor:
         self.bn.w.copy_(X)
         self.counts['hess'] += 1
@@ -126,6 +133,13 @@ class _SubsetDeviceEvaluator:
         self.problem.eval_ptrs(self.batch, self.w.data_ptr(), g=self.g.data_ptr(), jac=self.jac.data_ptr(),
                                f=self.f.data_ptr(), grad_f=self.gf.data_ptr(), stream=st.cuda_stream)
         return self.f.clone(), self.g.clone(), self.gf.clone(), self.jac.clone()
+
+    def eval_fg(self, X: torch.Tensor):
+        self.w.copy_(X)
+        st = torch.cuda.current_stream(self.device)
+        self.problem.eval_ptrs(self.batch, self.w.data_ptr(), g=self.g.data_ptr(), f=self.f.data_ptr(),
+                               grad_f=self.gf.data_ptr(), stream=st.cuda_stream)
+        return self.f.clone(), self.g.clone()
 
     def subset(self, count: int) -> '_SubsetDeviceEvaluator':
         return _SubsetDeviceEvaluator(self.base, count)
@@ -290,6 +304,17 @@ class BatchedInteriorPoint:
         f, g, gf, jv = self.ev.eval(x)
         self.stats['evals'] += 1
         return f * self.sf, g * self.sg, gf * self.sf, jv
+
+    def _eval_fg(self, x):
+        ''' scaled f and g at a line-search trial point: what the filter test needs. The gradient
+        and the Jacobian are evaluated once at the accepted point instead (evaluators with
+        eval_fg skip the Jacobian stores, 210 MB per trial at B = 512). '''
+        if hasattr(self.ev, 'eval_fg'):
+            f, g = self.ev.eval_fg(x)
+        else:
+            f, g, _, _ = self.ev.eval(x)
+        self.stats['evals'] += 1
+        return f * self.sf, g * self.sg
 
     def _relax(self, lo, hi):
         r = self.o.bound_relax_factor
@@ -755,20 +780,16 @@ class BatchedInteriorPoint:
                 pend = act.clone()
                 resto = torch.zeros(B, dtype=torch.bool, device=dev)
                 first = torch.ones(B, dtype=torch.bool, device=dev)
-                # accepted trial state
-                xn, sn, fn, gn, gfn, jvn = x.clone(), s.clone(), f.clone(), g.clone(), gf.clone(), jv.clone()
+                # accepted trial state (f, g, grad f and J are evaluated once at the accepted point)
+                xn, sn = x.clone(), s.clone()
                 an, dyn = torch.zeros_like(alpha), dy.clone()
                 armn = torch.zeros(B, dtype=torch.bool, device=dev)
 
-                def take(mask, al, xt, st, ft, gt, gft, jvt, arm, dyt):
-                    nonlocal xn, sn, fn, gn, gfn, jvn, an, dyn, armn
+                def take(mask, al, xt, st, arm, dyt):
+                    nonlocal xn, sn, an, dyn, armn
                     m2 = mask[None, :]
                     xn = torch.where(m2, xt, xn)
                     sn = torch.where(m2, st, sn)
-                    fn = torch.where(mask, ft, fn)
-                    gn = torch.where(m2, gt, gn)
-                    gfn = torch.where(m2, gft, gfn)
-                    jvn = torch.where(m2, jvt, jvn)
                     an = torch.where(mask, al, an)
                     dyn = torch.where(m2, dyt, dyn)
                     armn = torch.where(mask, arm, armn)
@@ -788,14 +809,18 @@ class BatchedInteriorPoint:
                     xt = x + alpha * dx
                     st = s + alpha * ds
                     laps.lap('ls_logic')
-                    ft, gt, gft, jvt = self._eval(xt)
+                    ft, gt = self._eval_fg(xt)
                     laps.lap('ls_eval')
                     tht, pht = self._measures(xt, st, gt, ft, mu)
-                    okt, armt = self._accept(theta, phi, gphi_d, alpha, tht, pht, F, nf)
-                    okt = okt & pend
-                    take(okt, alpha, xt, st, ft, gt, gft, jvt, armt, dy)
+                    if self.vk is not None:          # one launch: the filter test and the SOC candidates
+                        okt, armt, soc = self.vk.filter_accept(theta, phi, gphi_d, alpha, tht, pht, F, nf,
+                                                               self.theta_max, self.theta_min, pend, first, o)
+                    else:
+                        okt, armt = self._accept(theta, phi, gphi_d, alpha, tht, pht, F, nf)
+                        okt = okt & pend
+                        soc = pend & ~okt & first & (tht >= theta)
+                    take(okt, alpha, xt, st, armt, dy)
                     pend = pend & ~okt
-                    soc = pend & first & (tht >= theta)
                     if bool(soc.any()):
                         laps.lap('ls_logic')
                         if slk is None:
@@ -813,10 +838,12 @@ class BatchedInteriorPoint:
                 m2 = upd[None, :]
                 x = torch.where(m2, xn, x)
                 s = torch.where(m2, sn, s)
-                f = torch.where(upd, fn, f)
-                g = torch.where(m2, gn, g)
-                gf = torch.where(m2, gfn, gf)
-                jv = torch.where(m2, jvn, jv)
+                fe, ge, gfe, jve = self._eval(x)
+                f = torch.where(upd, fe, f)
+                g = torch.where(m2, ge, g)
+                gf = torch.where(m2, gfe, gf)
+                jv = torch.where(m2, jve, jv)
+                laps.lap('ls_eval')
                 y = torch.where(m2, y + an * dyn, y)
                 az = torch.where(upd, alpha_z, torch.zeros_like(alpha_z))
                 ks = o.kappa_sigma
@@ -956,12 +983,16 @@ class BatchedInteriorPoint:
             am = torch.minimum(torch.minimum(self._ftb(a, dxs, self.hxl, tau), self._ftb(b, -dxs, self.hxu, tau)),
                                torch.minimum(self._ftb(c, dss, self.hsl, tau), self._ftb(d, -dss, self.hsu, tau)))
             xt, st = x + am * dxs, s + am * dss
-            ft, gt, gft, jvt = self._eval(xt)
+            ft, gt = self._eval_fg(xt)
             rt2 = self._resid(gt, st)
             tht, pht = self._measures(xt, st, gt, ft, mu)
-            ok, arm = self._accept(theta, phi, gphi_d, alpha, tht, pht, F, nf)
-            ok = ok & cur
-            take(ok, am, xt, st, ft, gt, gft, jvt, arm, dys)
+            if self.vk is not None:
+                ok, arm, _ = self.vk.filter_accept(theta, phi, gphi_d, alpha, tht, pht, F, nf, self.theta_max,
+                                                   self.theta_min, cur, torch.zeros_like(cur), o)
+            else:
+                ok, arm = self._accept(theta, phi, gphi_d, alpha, tht, pht, F, nf)
+                ok = ok & cur
+            take(ok, am, xt, st, arm, dys)
             got = got | ok
             cur = cur & ~ok & ~(tht > o.kappa_soc * theta_old)
             theta_old = tht
@@ -1221,6 +1252,17 @@ class _RestorationEvaluator:
         jr[self.pe] = -1.0
         jr[self.pe + 1] = 1.0
         return fr, gr, gfr, jr
+
+    def eval_fg(self, X):
+        n, m = self.n0, self.m
+        x, p, nn = X[:n], X[n:n + m], X[n + m:]
+        if hasattr(self.base, 'eval_fg'):
+            f, g = self.base.eval_fg(x)
+        else:
+            f, g, _, _ = self.base.eval(x)
+        d = x - self.x_ref
+        fr = self.rho * (p.sum(0) + nn.sum(0)) + 0.5 * self.zeta * (self.dr2 * d * d).sum(0)
+        return fr, self.sg * g - p + nn
 
     def hess(self, X, lam, sigma):
         H0 = self.base.hess(X[:self.n0].contiguous(), (lam * self.sg).contiguous(), torch.zeros_like(sigma))

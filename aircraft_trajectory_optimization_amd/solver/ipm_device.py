@@ -29,6 +29,7 @@ class DeviceIPMKernels:
         self.mi, self.meq = len(self.iin), len(self.ieq)
         self._dims: Dict[int, native.AtoIpmDims] = {}
         self._work: Dict[int, torch.Tensor] = {}
+        self._prm: Dict[tuple, torch.Tensor] = {}   # filter parameters (device), by value
 
     # ------------------------------------------------------------------ plumbing
     def dims(self, W: int):
@@ -136,3 +137,25 @@ class DeviceIPMKernels:
                                                  *[_p(t) for t in z], *[_p(t) for t in dz], self._stream()),
                     'ato_ipm_multipliers')
         return tuple(z)
+
+    def filter_accept(self, theta, phi, gphi_d, alpha, tht, pht, F, nf, theta_max, theta_min, pend, first, o):
+        ''' (ok, arm, soc) bool [W]: the filter test of a trial point for the searching columns
+        (batched_ipm.py _accept, `& pend`) and the columns that try a second-order correction '''
+        W = theta.shape[0]
+        cols = [self._c(t, W) for t in (theta, phi, gphi_d, alpha, tht, pht, theta_max, theta_min)]
+        if F.dtype != torch.float64 or F.shape[0] != W or F.dim() != 3 or F.shape[2] != 2:
+            raise ValueError('filter: expected fp64 [W, fmax, 2]')
+        F = F.contiguous()
+        nf = nf.to(torch.int64).contiguous()
+        pend, first = pend.to(torch.bool).contiguous(), first.to(torch.bool).contiguous()
+        key = (o.s_phi, o.s_theta, o.delta, o.eta_phi, o.gamma_theta, o.gamma_phi)
+        prm = self._prm.get(key)
+        if prm is None:
+            prm = self._prm[key] = torch.tensor(key, dtype=torch.float64, device=self.device)
+        out = torch.empty((3, W), dtype=torch.bool, device=self.device)
+        th, ph, gd, al, tt, pt, tmax, tmin = cols
+        self._check(self.lib.ato_ipm_filter_accept(W, F.shape[1], _p(th), _p(ph), _p(gd), _p(al), _p(tt), _p(pt),
+                                                   _p(F), _p(nf), _p(tmax), _p(tmin), _p(pend), _p(first), _p(prm),
+                                                   _p(out[0]), _p(out[1]), _p(out[2]), self._stream()),
+                    'ato_ipm_filter_accept')
+        return out[0], out[1], out[2]

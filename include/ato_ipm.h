@@ -84,6 +84,20 @@ int ato_ipm_multipliers(const ato_ipm_dims* d, const ato_ipm_bounds* bd, const d
                         double* vu, const double* dzl, const double* dzu, const double* dvl, const double* dvu,
                         void* stream);
 
+/* Filter line-search acceptance test of a trial point (batched_ipm.py _accept and the trial
+ * bookkeeping around it; IPOPT A-5.4 - A-5.5, Waechter & Biegler 2006 eqs. (18)-(20)), one
+ * thread per column. theta, phi: measures of the current iterate; gphi_d: barrier directional
+ * derivative; alpha: trial step; tht, pht: measures of the trial point; F [W][fmax][2] the
+ * filter entries (theta, phi) of every column, nf [W] (int64) how many are valid; theta_max,
+ * theta_min [W]; pend, first [W] (bytes 0/1): columns still searching, first trial of the
+ * search. prm = {s_phi, s_theta, delta, eta_phi, gamma_theta, gamma_phi}. Outputs (bytes 0/1,
+ * [W]): ok = pend and accepted, arm = ok and the Armijo (f-type) case, soc = pend, not
+ * accepted, first trial and tht >= theta (a second-order correction is tried). */
+int ato_ipm_filter_accept(int32_t W, int32_t fmax, const double* theta, const double* phi, const double* gphi_d,
+                          const double* alpha, const double* tht, const double* pht, const double* F,
+                          const int64_t* nf, const double* theta_max, const double* theta_min,
+                          const uint8_t* pend, const uint8_t* first, const double* prm, uint8_t* ok,
+                          uint8_t* arm, uint8_t* soc, void* stream);
 #ifdef __cplusplus
 }
 #endif
