@@ -441,15 +441,16 @@ class BatchedInteriorPoint:
             need = mask & torch.isfinite(rmax) & (rmax > 1e-10 * scale)
             if not bool(need.any()):
                 break
-            corr = res.clone()
+            corr = res
             self.laps.lap('kkt_refine')
             self.kkt.solve(corr, _idx(need))
             self.laps.lap('kkt_solve')
             self.stats['solves'] += 1
             x = torch.where(need[None, :], x + corr, x)
+        else:                                        # x changed after the last residual
+            rmax = self._residual(H, Js, dx, dr, x, rhs).abs().amax(0)
         # IPOPT (residual_ratio_singular): unrefinable solves count as singular matrices
-        res = self._residual(H, Js, dx, dr, x, rhs).abs().amax(0)
-        self.last_solve_ok = torch.isfinite(res) & (res <= 1e-5 * scale)
+        self.last_solve_ok = torch.isfinite(rmax) & (rmax <= 1e-5 * scale)
         self.laps.lap('kkt_refine')
         return x
 

@@ -151,7 +151,7 @@ def test_filter_accept_matches_torch_formulation():
     from aircraft_trajectory_optimization_amd.solver.batched_ipm import BatchedInteriorPoint, FILTER_MAX
     from aircraft_trajectory_optimization_amd.solver.ipm import IPMOptions
     from aircraft_trajectory_optimization_amd.solver.ipm_device import DeviceIPMKernels
-    dev = torch.device('cuda')
+    dev = torch.device('cuda', torch.cuda.current_device())
     W = 777
     g = torch.Generator().manual_seed(3)
     r = lambda *s: torch.rand(*s, generator=g, dtype=torch.float64)     # noqa: E731

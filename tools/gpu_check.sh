@@ -67,11 +67,13 @@ for s in $STEPS; do
                done
                run bench_cur 200 python bench.py --steps 50 --warmup 10 --no-cpu-baseline --no-solve ;;
         kktphase) ATO_LIB_PATH=$PWD/tools/diag/_lib/libato_stamps.so run kkt_phase 120 python tools/diag/kkt_phase.py ;;
+        ipmktests) run pytest_ipmk 300 python -u -m pytest tests/test_gpu_ipm_kernels.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider ;;
         kkttests) run pytest_kkt 300 python -u -m pytest tests/test_gpu_kkt.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider ;;
         solve) run solve_b512 600 python tools/solve_batched.py --batch 512 --max-iter 200 --no-host --out "$OUT/solve_b512.json" ;;
         solveprof) run solveprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/solveprof" -o run -- \
                    python tools/solve_batched.py --batch 512 --max-iter 60 --no-host --out "$OUT/solveprof.json" ;;
         solvelaps) ATO_IPM_PROFILE=1 run solvelaps 600 python tools/solve_batched.py --batch 512 --max-iter 60 --no-host --out "$OUT/solvelaps.json" ;;
+        solvelaps200) ATO_IPM_PROFILE=1 run solvelaps200 600 python tools/solve_batched.py --batch 512 --max-iter 200 --no-host --out "$OUT/solvelaps200.json" ;;
         listpmc) run listpmc 120 rocprofv3 -L ;;
         mb)    run mb_store 120 ./tools/mb_store ;;
         mbpmc) run mb_fetch 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/mb_fetch" -o run -- ./tools/mb_store
