@@ -214,3 +214,33 @@ def test_obstacle_point_raceline_on_gpu():
     assert res.feasible
     d = np.array([s.d for s in res.states])
     assert np.isfinite(d).all()
+
+
+def test_paired_kernel_matches_generic_kernel():
+    ''' whole 64-instance chunks take the paired-store kernel (interleaved layout); its g, J, f and
+    grad f equal the generic kernel's (instance-major layout) bit for bit, over repeated launches
+    and a smaller batch on the same library handle '''
+    spec, _, W, _ = _racetrack(192)
+    a = _batched(spec, 192)
+    b = _batched(spec, 192, layout=native.ATO_LAYOUT_INSTANCE_MAJOR)
+    for bn in (a, b):
+        bn.set_w(W)
+        bn.evaluate()
+    for x, y in zip(a.results(), b.results()):
+        np.testing.assert_array_equal(x, y)
+    f0 = a.results()[2].copy()
+    for rep in range(3):                       # repeated launches
+        a.f.zero_()
+        a.evaluate()
+        np.testing.assert_array_equal(a.results()[2], f0)
+    # a smaller batch on the same library handle, then the full batch again
+    wt = torch.as_tensor(np.ascontiguousarray(W[:64].T), device=a.w.device)
+    f64 = torch.zeros(64, dtype=torch.float64, device=a.w.device)
+    g64 = torch.zeros((a.g.shape[0], 64), dtype=torch.float64, device=a.w.device)
+    gf64 = torch.zeros((a.grad_f.shape[0], 64), dtype=torch.float64, device=a.w.device)
+    a.problem.eval_ptrs(64, wt.data_ptr(), g=g64.data_ptr(), f=f64.data_ptr(), grad_f=gf64.data_ptr())
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(f64.cpu().numpy(), f0[:64])
+    a.f.zero_()
+    a.evaluate()
+    np.testing.assert_array_equal(a.results()[2], f0)
