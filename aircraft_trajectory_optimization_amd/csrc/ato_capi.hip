@@ -193,7 +193,10 @@ static int eval_impl(ato_handle* h, int32_t batch, int32_t layout, const T* w, T
     hipError_t e = hipSuccess;
     ato::with_model(p, [&]<class M>() {
         hipEvent_t* ev = nullptr;
-        if ((size_t)(h->timed_calls + 1) * 3 <= h->events.size()) ev = &h->events[(size_t)h->timed_calls++ * 3];
+        const bool sample = h->timing_stride <= 1 || h->timing_seen % h->timing_stride == 0;
+        if (!h->events.empty()) ++h->timing_seen;
+        if (sample && (size_t)(h->timed_calls + 1) * 3 <= h->events.size())
+            ev = &h->events[(size_t)h->timed_calls++ * 3];
         e = ato::launch_eval<M, T>(p, batch, layout, w, g, jac, grad_f, f, (T*)h->d_fpart, (hipStream_t)stream,
                                    ev);
     });
@@ -206,11 +209,18 @@ extern "C" int ato_timing(ato_handle* h, int32_t max_calls) {
     for (hipEvent_t e : h->events) ATO_HIP(hipEventDestroy(e));
     h->events.clear();
     h->timed_calls = 0;
+    h->timing_seen = 0;
     for (int i = 0; i < 3 * max_calls; ++i) {
         hipEvent_t e;
         ATO_HIP(hipEventCreate(&e));
         h->events.push_back(e);
     }
+    return ATO_OK;
+}
+
+extern "C" int ato_timing_stride(ato_handle* h, int32_t stride) {
+    if (!h || stride < 1) return fail(ATO_ERR_ARG, "bad timing stride");
+    h->timing_stride = stride;
     return ATO_OK;
 }
 

@@ -20,6 +20,8 @@ struct ato_handle {
     int32_t reserved = 0;
     std::vector<hipEvent_t> events;   // 3 per timed call
     int32_t timed_calls = 0;
+    int32_t timing_stride = 1;        // events on every timing_stride-th evaluation
+    int64_t timing_seen = 0;          // evaluations since ato_timing
     // Hessian of the Lagrangian (built on first use)
     bool hess_ready = false;
     ato::HessLayout HL;

@@ -104,7 +104,7 @@ IPM_SYMBOLS = ('ato_ipm_work_size', 'ato_ipm_errors', 'ato_ipm_rhs', 'ato_ipm_di
 EXPORTED_SYMBOLS = ('ato_create', 'ato_destroy', 'ato_sizes', 'ato_sparsity', 'ato_bounds',
                     'ato_reserve', 'ato_eval', 'ato_eval_f32', 'ato_hess_sparsity', 'ato_hess_eval',
                     'ato_mesh_create', 'ato_mesh_destroy', 'ato_mesh_signed_distance',
-                    'ato_timing', 'ato_timing_read', 'ato_last_error', 'ato_version',
+                    'ato_timing', 'ato_timing_read', 'ato_timing_stride', 'ato_last_error', 'ato_version',
                     'ato_kkt_create', 'ato_kkt_destroy', 'ato_kkt_reserve', 'ato_kkt_factor', 'ato_kkt_solve',
                     'ato_kkt_residual') + IPM_SYMBOLS
 
@@ -137,6 +137,7 @@ def declare(lib: ctypes.CDLL, prefix: str = 'ato') -> ctypes.CDLL:
         lib.ato_mesh_signed_distance.argtypes = [vp, ctypes.c_int32, vp, vp, vp, vp]
         lib.ato_timing.argtypes = [vp, ctypes.c_int32]
         lib.ato_timing_read.argtypes = [vp, _c_double_p, _c_double_p, i32p]
+        lib.ato_timing_stride.argtypes = [vp, ctypes.c_int32]
         lib.ato_kkt_create.argtypes = [vp, ctypes.POINTER(vp)]
         lib.ato_kkt_destroy.argtypes = [vp]
         lib.ato_kkt_reserve.argtypes = [vp, ctypes.c_int32]
@@ -160,7 +161,7 @@ def declare(lib: ctypes.CDLL, prefix: str = 'ato') -> ctypes.CDLL:
             getattr(lib, fn).restype = ctypes.c_int
         for fn in ('ato_create', 'ato_destroy', 'ato_sizes', 'ato_sparsity', 'ato_bounds', 'ato_reserve',
                    'ato_eval', 'ato_eval_f32', 'ato_hess_sparsity', 'ato_hess_eval', 'ato_timing',
-                   'ato_timing_read', 'ato_mesh_create', 'ato_mesh_destroy', 'ato_mesh_signed_distance'):
+                   'ato_timing_read', 'ato_timing_stride', 'ato_mesh_create', 'ato_mesh_destroy', 'ato_mesh_signed_distance'):
             getattr(lib, fn).restype = ctypes.c_int
     return lib
 
@@ -330,6 +331,10 @@ class NativeProblem:
     def timing_start(self, max_calls: int):
         ''' record HIP events around the kernels of the next max_calls evaluations '''
         self._check(self.lib.ato_timing(self.handle, int(max_calls)))
+
+    def timing_stride(self, stride: int):
+        ''' events on every stride-th evaluation only (ato_timing_stride) '''
+        self._check(self.lib.ato_timing_stride(self.handle, int(stride)))
 
     def timing_read(self):
         ''' (sum of Jacobian-kernel ms, sum of cost-reduce ms, calls) since timing_start '''

@@ -27,6 +27,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = 'SQP iters/sec (batched) + lap-time err vs CasADi, 50×4 collocation'
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
+TIMING_STRIDE = 10         # kernel-timing events on every 10th timed step
 
 
 def parse():
@@ -137,7 +138,11 @@ def main():
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
-    bn.problem.timing_start(args.steps)
+    # kernel durations from HIP events on the evaluation stream, recorded on every TIMING_STRIDE-th
+    # step of the timed loop: each recorded step adds three event packets (about 10 us of gaps at
+    # B = 512, tools/diag/step_gaps.py), which would otherwise be part of every measured step
+    bn.problem.timing_stride(TIMING_STRIDE)
+    bn.problem.timing_start((args.steps + TIMING_STRIDE - 1) // TIMING_STRIDE)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -149,6 +154,7 @@ def main():
     elapsed = max_over_ranks(t1 - t0, dev)
     k_ms, r_ms, calls = bn.problem.timing_read()
     bn.problem.timing_start(0)
+    bn.problem.timing_stride(1)
 
     # per-instance summary {lap-time guess sum(h), cost f, max equality residual}, all-gathered (RCCL)
     g, _, f, _ = bn.results()
@@ -191,6 +197,7 @@ def main():
                          'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
                          'kernel': 'k_eval', 'kernel_avg_us': kernel_s * 1e6,
                          'reduce_avg_us': r_ms / max(calls, 1) * 1e3,
+                         'timed_launches': calls, 'timing_stride': TIMING_STRIDE,
                          'algorithmic_bytes_per_launch': B * bytes_per_eval},
             'cpu_baseline': None,
         }

@@ -166,6 +166,11 @@ int ato_mesh_signed_distance(ato_mesh* mesh, int32_t n, const double* points, do
  * waits for the recorded events and returns the summed durations (ms) and the call count. */
 int ato_timing(ato_handle* h, int32_t max_calls);
 int ato_timing_read(ato_handle* h, double* eval_ms, double* reduce_ms, int32_t* calls);
+/* Sample the timing: while on, only every stride-th ato_eval (counted from the last ato_timing
+ * call) records its events (stride 1, the default: every call). Each recorded call puts three
+ * event packets into the stream, about 10 us of gaps at the benchmark size; sampling keeps the
+ * kernel durations measured inside a timed loop without slowing the loop itself. */
+int ato_timing_stride(ato_handle* h, int32_t stride);
 
 const char* ato_last_error(void);
 
