@@ -422,10 +422,12 @@ class BatchedInteriorPoint:
         ok = ~rej & ~in_f & torch.where(arm_case, ok_arm, ok_suf)
         return ok, ok & arm_case
 
-    def _solve(self, rhs, mask, H, Js, dx, dr):
+    def _solve(self, rhs, mask, H, Js, dx, dr, idx=None):
         ''' K x = rhs for the masked instances with their current factors, iterative refinement
-        (IPOPT: residual ratio 1e-10, at most 10 steps) '''
-        idx = _idx(mask)
+        (IPOPT: residual ratio 1e-10, at most 10 steps); idx: the masked instances' indices when
+        the caller has them already '''
+        if idx is None:
+            idx = _idx(mask)
         x = rhs.clone()
         if len(idx) == 0:
             self.last_solve_ok = torch.zeros_like(mask)
@@ -488,22 +490,24 @@ class BatchedInteriorPoint:
         dx_used = torch.zeros((n, B), dtype=torch.float64, device=self.dev)
         dr_used = torch.zeros((m, B), dtype=torch.float64, device=self.dev)
         dw_out = zeros.clone()
-        while bool(pend.any()):
+        pidx = _idx(pend)
+        while len(pidx):
             Ds_tot = Ss + delta_w
             dr = (-delta_c).expand(m, B).clone()
             dr[self.iin] -= 1.0 / Ds_tot
             dx = Sx + delta_w
             self.laps.lap('kkt_other')
-            inertia = self.kkt.factor(W, Js, dx, dr, _idx(pend))
+            inertia = self.kkt.factor(W, Js, dx, dr, pidx)
             self.laps.lap('kkt_factor')
             self.stats['factorizations'] += 1
             ok = (inertia[:, 0] == n) & (inertia[:, 1] == m) & (inertia[:, 2] == 0)
             sing = inertia[:, 2] > 0
             good = pend & ok & ~sing
-            if bool(good.any()):
+            gidx = _idx(good)
+            if len(gidx):
                 ry = rhs_y.clone()
                 ry[self.iin] += rhs_s / Ds_tot
-                xs = self._solve(torch.cat([rhs_x, ry]), good, W, Js, dx, dr)
+                xs = self._solve(torch.cat([rhs_x, ry]), good, W, Js, dx, dr, idx=gidx)
                 fin = torch.isfinite(xs).all(0) & self.last_solve_ok
                 sing = sing | (good & ~fin)
                 good = good & fin
@@ -525,6 +529,7 @@ class BatchedInteriorPoint:
             first = first & ~bad
             fail = bad & (delta_w > o.delta_w_max)
             pend = bad & ~fail
+            pidx = _idx(pend)
         dxs, dy = sol[:n], sol[n:]
         ds = (rhs_s + dy[self.iin]) / Ds_used
         ctx = (W, Js, dx_used, dr_used, Ds_used)
@@ -701,7 +706,8 @@ class BatchedInteriorPoint:
             mx = act & (own >= o.max_iter)
             status = torch.where(mx, torch.full_like(status, MAX_ITER), status)
             act = act & ~mx
-            if not bool(act.any()) and not bool(waiting.any()) and not inflight:
+            any_act, any_wait = torch.stack([act.any(), waiting.any()]).tolist()     # one synchronisation
+            if not any_act and not any_wait and not inflight:
                 break
             laps.lap('check')
             stepping = act.clone()
@@ -710,7 +716,7 @@ class BatchedInteriorPoint:
                 import sys
                 print(f'[batched ipm{" resto" if stop_check is not None else ""}] iter {it}: '
                       f'{int(act.sum())} active, {int((status == OPTIMAL).sum())} optimal', file=sys.stderr, flush=True)
-            if bool(act.any()):
+            if any_act:
                 # ---- barrier update (monotone), per instance
                 for _ in range(100):
                     if self.vk is not None:
@@ -798,14 +804,16 @@ class BatchedInteriorPoint:
                 laps.lap('direction')
                 for _ls in range(200):
                     failed = pend & ~(alpha >= alpha_min)
-                    if bool(failed.any()):
+                    # one host synchronisation per trial for both tests
+                    any_failed, any_left = torch.stack([failed.any(), (pend & ~failed).any()]).tolist()
+                    if any_failed:
                         if allow_restoration:
                             resto = resto | failed
                         else:
                             status = torch.where(failed, torch.full_like(status, LS_FAILED), status)
                             act = act & ~failed
                         pend = pend & ~failed
-                    if not bool(pend.any()):
+                    if not any_left:
                         break
                     xt = x + alpha * dx
                     st = s + alpha * ds
@@ -822,7 +830,7 @@ class BatchedInteriorPoint:
                         soc = pend & ~okt & first & (tht >= theta)
                     take(okt, alpha, xt, st, armt, dy)
                     pend = pend & ~okt
-                    if bool(soc.any()):
+                    if _ls == 0 and bool(soc.any()):     # corrections only after the first trial step
                         laps.lap('ls_logic')
                         if slk is None:
                             slk = self._slacks(x, s)
@@ -865,7 +873,7 @@ class BatchedInteriorPoint:
             # restored together, so one nested batched solve serves many of them
             waiting = waiting | resto
             act = act & ~resto
-            n_act, n_wait = int(act.sum()), int(waiting.sum())
+            n_act, n_wait = torch.stack([act.sum(), waiting.sum()]).tolist()
             done = None                              # (restored columns, their x, success) of a finished phase
             if inflight:
                 ready = [j for j in inflight if j['future'].done()]
