@@ -76,6 +76,11 @@ for s in $STEPS; do
                    python tools/solve_batched.py --batch 512 --max-iter 60 --no-host --out "$OUT/solveprof.json" ;;
         solvelaps) ATO_IPM_PROFILE=1 run solvelaps 600 python tools/solve_batched.py --batch 512 --max-iter 60 --no-host --out "$OUT/solvelaps.json" ;;
         solvelaps200) ATO_IPM_PROFILE=1 run solvelaps200 600 python tools/solve_batched.py --batch 512 --max-iter 200 --no-host --out "$OUT/solvelaps200.json" ;;
+        solveab) for v in base cur base cur; do
+                   if [ $v = base ]; then lp=$PWD/tools/diag/_lib/libato_base.so; else lp=; fi
+                   ATO_LIB_PATH=$lp run solve_$v 600 python tools/solve_batched.py --batch 512 --max-iter 200 --no-host --out "$OUT/solve_$v.json"
+                   cp "$OUT/solve_$v.json" "$OUT/solve_${v}_$(date +%s).json"
+               done ;;
         listpmc) run listpmc 120 rocprofv3 -L ;;
         mb)    run mb_store 120 ./tools/mb_store ;;
         mbpmc) run mb_fetch 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/mb_fetch" -o run -- ./tools/mb_store
