@@ -244,3 +244,21 @@ def test_paired_kernel_matches_generic_kernel():
     a.f.zero_()
     a.evaluate()
     np.testing.assert_array_equal(a.results()[2], f0)
+
+
+def test_timing_stride_samples_every_nth_evaluation():
+    ''' ato_timing_stride: with stride 3, seven evaluations record events on calls 0, 3 and 6 only,
+    and their kernel durations are positive (the bench samples its timed loop this way) '''
+    spec, _, W, _ = _racetrack(64)
+    bn = _batched(spec, 64)
+    bn.set_w(W)
+    bn.evaluate()
+    bn.problem.timing_stride(3)
+    bn.problem.timing_start(3)
+    for _ in range(7):
+        bn.evaluate()
+    torch.cuda.synchronize()
+    k_ms, r_ms, calls = bn.problem.timing_read()
+    bn.problem.timing_start(0)
+    bn.problem.timing_stride(1)
+    assert calls == 3 and k_ms > 0.0 and r_ms >= 0.0
