@@ -1008,6 +1008,9 @@ size_t factor_lds() {
 // share a CU and overlap their pivot chains: B = 512 factorisation 37.3 -> 28.1 ms, B = 1 0.77 ->
 // 0.80 ms. So the four-wave variant runs when the level has more workgroups than the chip has CUs.
 constexpr int CUS = 256;
+#ifndef ATO_KKT_LEAF_FTT
+#define ATO_KKT_LEAF_FTT 256
+#endif
 
 template <int T>
 int launch_factor_level(const ato_kkt* h, const Plan& P, const Vals& V, int f0, int nf, int batch, const int* list,
@@ -1023,6 +1026,19 @@ int launch_factor_level(const ato_kkt* h, const Plan& P, const Vals& V, int f0, 
                                f0, batch, list, h->d_L, h->d_piv, h->d_dinv, h->d_sinfo, h->d_cb, inertia,
                                h->d_spec);
     }
+#if ATO_KKT_LEAF_FTT == 256
+    // Six-tile fronts (the interval leaves): 256 threads, one wave per SIMD, four columns per thread
+    // and tile (about 220 VGPRs). Every wave runs the pivot search and decision, so four waves do
+    // that work instead of eight, and no SIMD interleaves two waves of the same front's chain.
+    if constexpr (T == 6) {
+        if (!one_wave) {
+            hipLaunchKernelGGL((k_front_factor_w<T, 2, 256>), dim3(nf, batch), dim3(256), factor_lds<T>(), st, P, V,
+                               f0, batch, list, h->d_L, h->d_piv, h->d_dinv, h->d_sinfo, h->d_cb, inertia,
+                               h->d_spec);
+            one_wave = true;
+        }
+    }
+#endif
     if (!one_wave) {
         auto k = k_front_factor_w<T, 1, FT>;
         if constexpr (T == 6)

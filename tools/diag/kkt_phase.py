@@ -1,7 +1,8 @@
 '''
 DIAGNOSTIC (GPU): shader-clock split of the pivot steps of the KKT factorisation, recorded by
-the workgroup of front 0 (the first interval leaf) of instance 0 in a stamps build
-(tools/diag/kkt_variants.py stamps -DATO_KKT_STAMPS).
+the workgroup of front ATO_KKT_STAMP_FRONT (default 0; the first interval leaf is front 50 since the
+pre-front split) of instance 0 in a stamps build (tools/diag/kkt_variants.py stamps -DATO_KKT_STAMPS
+-DATO_KKT_STAMP_FRONT=50); ATO_PHASE_B sets the batch (default 1).
 
     ATO_LIB_PATH=tools/diag/_lib/libato_stamps.so python tools/diag/kkt_phase.py
 '''
@@ -26,7 +27,7 @@ def main():
     from aircraft_trajectory_optimization_amd.solver.kkt_plan import build_plan
     from aircraft_trajectory_optimization_amd.tracks import make_spec
     spec = make_spec(track='race', frame='parametric', N=50, K=4)
-    B = 1
+    B = int(os.environ.get('ATO_PHASE_B', '1'))
     bn = BatchedNLP(spec, B)
     W, _, _ = seeded_instances(spec, np.arange(B))
     bn.set_w(W)

@@ -66,7 +66,12 @@ for s in $STEPS; do
                    ATO_LIB_PATH=$PWD/$v run "bench_$n" 200 python bench.py --steps 50 --warmup 10 --no-cpu-baseline --no-solve
                done
                run bench_cur 200 python bench.py --steps 50 --warmup 10 --no-cpu-baseline --no-solve ;;
-        kktphase) ATO_LIB_PATH=$PWD/tools/diag/_lib/libato_stamps.so run kkt_phase 120 python tools/diag/kkt_phase.py ;;
+        kktphase) ATO_LIB_PATH=$PWD/tools/diag/_lib/libato_stamps.so run kkt_phase 120 python tools/diag/kkt_phase.py
+               ATO_PHASE_B=512 ATO_LIB_PATH=$PWD/tools/diag/_lib/libato_stamps.so run kkt_phase512 120 python tools/diag/kkt_phase.py ;;
+        kktab) for b in 512 64 1; do
+                   ATO_LIB_PATH=$PWD/tools/diag/_lib/libato_base.so run kkt_base_b$b 200 python tools/bench_kkt.py --batch $b --reps 7 --out "$OUT/kkt_base_b$b.json"
+                   run kkt_cur_b$b 200 python tools/bench_kkt.py --batch $b --reps 7 --out "$OUT/kkt_cur_b$b.json"
+               done ;;
         kktq)  run kkt_b512 200 python tools/bench_kkt.py --batch 512 --out "$OUT/kkt_b512.json"
                run kkt_b1 200 python tools/bench_kkt.py --batch 1 --out "$OUT/kkt_b1.json" ;;
         ipmktests) run pytest_ipmk 300 python -u -m pytest tests/test_gpu_ipm_kernels.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider ;;
