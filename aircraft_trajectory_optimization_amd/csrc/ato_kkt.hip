@@ -1011,6 +1011,9 @@ constexpr int CUS = 256;
 #ifndef ATO_KKT_LEAF_FTT
 #define ATO_KKT_LEAF_FTT 256
 #endif
+#ifndef ATO_KKT_SMALL_FTT
+#define ATO_KKT_SMALL_FTT 256
+#endif
 
 template <int T>
 int launch_factor_level(const ato_kkt* h, const Plan& P, const Vals& V, int f0, int nf, int batch, const int* list,
@@ -1033,6 +1036,18 @@ int launch_factor_level(const ato_kkt* h, const Plan& P, const Vals& V, int f0, 
     if constexpr (T == 6) {
         if (!one_wave) {
             hipLaunchKernelGGL((k_front_factor_w<T, 2, 256>), dim3(nf, batch), dim3(256), factor_lds<T>(), st, P, V,
+                               f0, batch, list, h->d_L, h->d_piv, h->d_dinv, h->d_sinfo, h->d_cb, inertia,
+                               h->d_spec);
+            one_wave = true;
+        }
+    }
+#endif
+#if ATO_KKT_SMALL_FTT == 256
+    // fronts of at most two tiles in levels of few workgroups (small batches, restoration phases):
+    // 256 threads, one wave per SIMD (the same reasoning as the leaves)
+    if constexpr (T <= 2) {
+        if (!one_wave) {
+            hipLaunchKernelGGL((k_front_factor_w<T, 1, 256>), dim3(nf, batch), dim3(256), factor_lds<T>(), st, P, V,
                                f0, batch, list, h->d_L, h->d_piv, h->d_dinv, h->d_sinfo, h->d_cb, inertia,
                                h->d_spec);
             one_wave = true;
