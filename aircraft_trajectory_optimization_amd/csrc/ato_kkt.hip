@@ -77,7 +77,7 @@ int fail(int code, const std::string& m) {
     } while (0)
 
 constexpr int FT = 512;                   // factor threads per (front, instance) (16 x 32 grid)
-constexpr int ST = 256;                   // solve threads per (front, instance)
+constexpr int ST = 128;                   // solve threads per (front, instance): two waves (256: B = 512 solve 3.02 ms, 128: 2.63 ms)
 constexpr int EPT = 8;                    // entries per thread and front (<= 4096 per front)
 #ifndef ATO_KKT_SPEC
 #define ATO_KKT_SPEC 0
@@ -87,6 +87,8 @@ constexpr int EPT = 8;                    // entries per thread and front (<= 40
 #endif
 constexpr int CH = ATO_KKT_CH;            // doubles per ring chunk of the solve (2 x CH x 8 B LDS ring)
 constexpr int CPT = CH / ST;              // chunk doubles per thread
+// a factor column (two for a 2x2 pivot: 2 x 32 T doubles) must fit in the two resident chunks
+static_assert(CH >= 2 * 32 * 8, "solve ring chunk smaller than the largest column pair");
 constexpr int MAXT = 8;                   // strips per front in ent_ptr
 constexpr double BK_ALPHA = 0.64038820320220756872767623199676;   // (1 + sqrt(17)) / 8
 constexpr int SRC_SHIFT = 29;
