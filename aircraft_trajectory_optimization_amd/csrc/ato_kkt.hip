@@ -874,8 +874,7 @@ __global__ __launch_bounds__(ST) void k_front_bwd(Plan P, int f0, int batch, con
     constexpr int NQ = (NP + 63) / 64;
     __shared__ double ring_buf[2 * CH];
     __shared__ double cvec[NP];
-    __shared__ int2 s_piv[NP];
-    __shared__ double s_dinv[3 * NP];
+    __shared__ int2 s_piv[NP];     // (the backward sweep needs no inverse pivot blocks: 4.6 KB less LDS)
     __shared__ int s_done;
 
     const int bi = blockIdx.y;
@@ -892,7 +891,7 @@ __global__ __launch_bounds__(ST) void k_front_bwd(Plan P, int f0, int batch, con
 
     // own: the forward (D-scaled) values; trailing: final values of the ancestors' positions
     for (int i = tid; i < NP; i += ST) cvec[i] = i < F.A ? F.xb[(long long)P.pos_index[F.p0 + i] * se] : 0.0;
-    stage_records(F.pv, F.dvp, F.steps, tid, s_piv, s_dinv);
+    for (int u = tid; u < F.steps; u += ST) s_piv[u] = F.pv[u];
     ring_load(F.Lb, F.total, clast, stage_r, tid);
     ring_store(ring.buf, clast, stage_r, tid);
     ring_load(F.Lb, F.total, clast - 1, stage_r, tid);
