@@ -2,18 +2,22 @@
 ORACLE (test infrastructure only): collocation coefficients.
 
 Restates drone3d/utils/discretization_utils.py:8-51. tau_0 = 0 plus the K Gauss-Legendre
-roots on (0, 1) (CasADi collocation_points(K, 'legendre'), tabulated in CasADi to 16
-decimal places; here numpy's Gauss-Legendre rule rounded to 16 decimal places).
+roots on (0, 1) (CasADi collocation_points(K, 'legendre'), tabulated in CasADi to 20 digits,
+i.e. the nearest doubles of the roots; here the roots are found to 40 digits with mpmath and
+rounded once).
 '''
 import numpy as np
 
-# the K = 4 table as printed from the reference's CasADi build (SURVEY.md A1)
-CASADI_LEGENDRE_K4 = [0.0694318442029737, 0.3300094782075719, 0.6699905217924281, 0.9305681557970262]
+# K = 4: (x + 1) / 2 for the roots x = +-sqrt(3/7 -+ 2/7 sqrt(6/5)) of P_4, rounded once
+CASADI_LEGENDRE_K4 = [0.06943184420297371, 0.33000947820757187, 0.6699905217924281, 0.9305681557970263]
 
 
 def legendre_roots(K):
-    x, _ = np.polynomial.legendre.leggauss(K)
-    return [float(f'{v:.16f}') for v in sorted((x + 1) / 2)]
+    import mpmath
+    with mpmath.workdps(40):
+        guess, _ = np.polynomial.legendre.leggauss(K)
+        roots = [mpmath.findroot(lambda z: mpmath.legendre(K, z), mpmath.mpf(float(g))) for g in guess]
+        return [float((r + 1) / 2) for r in sorted(roots)]
 
 
 def coefficients(K):

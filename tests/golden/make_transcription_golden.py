@@ -1,0 +1,290 @@
+#!/usr/bin/env python
+'''
+Golden fixtures of the REFERENCE's own transcription ("optional stronger pin").
+
+TEST INFRASTRUCTURE, build container only (the reference never reaches the GPU box). It imports
+/root/reference's drone3d package -- base_raceline.py, drone_raceline.py, point_raceline.py,
+drone_models.py, point_model.py, dynamics_model.py, rotations.py, spline_centerline.py,
+base_centerline.py, discretization_utils.py, interp.py, mesh_obstacle.py (ObstacleFreeTube) --
+against the arithmetic-only CasADi stand-in in tests/golden/standin/ (CasADi is not installed,
+SURVEY F8), with inert modules in place of the renderer (OpenGL / imgui: visualization.objects,
+visualization.utils) and of trimesh (the tube below is given, not searched). The reference
+classes are constructed exactly as scripts/ and utils/solve_util.py:29-75 construct them; the
+NLP they build (raceline.nlp['w'], ['g'], ['J'], solver_w0 / lbw / ubw / lbg / ubg) is then
+evaluated at seeded points:
+    g(w) and f(w) by plain float evaluation of the expression graph,
+    dg/dw and grad f(w) by complex-step differentiation of the same graph (exact to rounding).
+Each case is written to tests/golden/transcription/<name>.npz. Cases use the same keyword
+dictionary as tests/helpers.product_spec / oracle_nlp, so the tests compare like with like.
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_transcription_golden.py [--only NAME]
+'''
+import argparse
+import json
+import os
+import sys
+import time
+import types
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+OUT = os.path.join(HERE, 'transcription')
+REFERENCE = os.environ.get('ATO_REFERENCE', '/root/reference')
+
+# scenario waypoints (data of scripts/race.py:12-14, scripts/fig_8.py:10-12, scripts/obstacles.py:14-16)
+TRACKS = {'race': ([[-1.1, 9.2, 9.2, -4.5, -4.5, 4.75, -2.8],
+                    [-1.6, 6.6, -4, -6, -6, -0.9, 6.8],
+                    [3.6, 1.0, 1.2, 3.5, 0.8, 1.2, 1.2]], 'square'),
+          'fig8': ([[0, 5, 0, -5, 0, 5, 0, -5],
+                    [0, 1, 2, 1, 0, -1, -2, -1],
+                    [10, 5, 0, -5, -10, -5, 0, 5]], 'circle'),
+          'obstacles': ([[-5, -2.75, -0.66, 2.95, 8.67, 9.2, 1.57, -2.39, -4.7, -2.39, 4.23, -2.66],
+                         [4.5, -0.08, -1.36, 1.25, 6.69, -3.6, -6.43, -6, -6.43, -6.23, -0.66, 6.66],
+                         [1.2, 2.815, 3.9, 2.815, 1.0, 1.0, 2.815, 3.9, 2.815, 1.0, 1.0, 1.0]], 'circle')}
+
+CASES = {
+    # collocation, parametric frame
+    'race_param_esp_K2': dict(track='race', N=4, K=2),
+    'race_param_esp_K4': dict(track='race', N=3, K=4),
+    'fig8_param_esp_K7': dict(track='fig8', N=3, K=7),
+    'fig8_param_ypr_K3': dict(track='fig8', N=3, K=3, use_quat=False),
+    'race_param_esp_rel_K2': dict(track='race', N=3, K=2, global_r=False),
+    'race_param_ypr_rel_K2': dict(track='race', N=3, K=2, use_quat=False, global_r=False),
+    'race_param_fixcenter_K3': dict(track='race', N=3, K=3, fix_gate_center=True),
+    'race_param_point_K2': dict(track='race', model='point', N=3, K=2, use_quat=False),
+    'fig8_param_point_rel_K2': dict(track='fig8', model='point', N=3, K=2, use_quat=False, global_r=False),
+    # collocation, global frame (N rounded up to a multiple of the gate phases)
+    'race_global_esp_K2': dict(track='race', frame='global', N=7, K=2),
+    'fig8_global_ypr_K2': dict(track='fig8', frame='global', N=8, K=2, use_quat=False),
+    'race_global_point_K2': dict(track='race', frame='global', model='point', N=7, K=2, use_quat=False),
+    # RK4 multiple shooting (use_rk4: N*K steps, scripts/race.py). The reference indexes Z[n+1] for a
+    # gate inside the last step (base_raceline.py:1019) and raises there, so, as in race.py (490 steps),
+    # no gate falls in the last step
+    'race_param_esp_rk4': dict(track='race', N=7, K=2, rk4=True),
+    'race_global_esp_rk4': dict(track='race', frame='global', N=7, K=1, rk4=True),
+    'race_global_ypr_rk4': dict(track='race', frame='global', N=7, K=1, rk4=True, use_quat=False),
+    'race_param_point_rk4': dict(track='race', model='point', N=7, K=2, rk4=True, use_quat=False),
+    'fig8_param_ypr_rel_rk4': dict(track='fig8', N=8, K=2, rk4=True, use_quat=False, global_r=False),
+    # open (non-periodic) lines
+    'race_open_param_esp_K3': dict(track='race', N=4, K=3, closed=False),
+    'race_open_global_ypr_K3': dict(track='race', frame='global', N=6, K=3, closed=False, use_quat=False),
+    'race_open_param_point_K3': dict(track='race', model='point', N=4, K=3, closed=False, use_quat=False),
+    # obstacle sphere rows (ObstacleFreeTube.add_constraints_parametric, mesh_obstacle.py:219-237)
+    'race_param_esp_spheres_K2': dict(track='race', N=4, K=2, spheres=1),
+    'race_param_point_spheres_K2': dict(track='race', model='point', N=3, K=3, use_quat=False, spheres=2),
+    # point-mass warm start of the drone guess (drone_raceline.py:158-274)
+    'race_param_esp_warm_K2': dict(track='race', N=4, K=2, warm=1),
+    'fig8_param_esp_warm_K3': dict(track='fig8', N=3, K=3, warm=2),
+    'race_global_esp_warm_K2': dict(track='race', frame='global', N=7, K=2, warm=3),
+    'obst_global_ypr_warm_K2': dict(track='obstacles', frame='global', N=36, K=2, use_quat=False, warm=4),
+    'obst_param_ypr_warm_K2': dict(track='obstacles', N=36, K=2, use_quat=False, warm=5),
+    # the reference refuses this guess (vertical drop between race gates 3 and 4: the heading jumps,
+    # drone_raceline.py:223-235); the fixture records the refusal
+    'race_global_ypr_warm_refused': dict(track='race', frame='global', N=21, K=2, use_quat=False, warm=4),
+}
+
+
+def _inert_module(name):
+    ''' a module whose every attribute is an inert class (renderer / mesh-library stand-in) '''
+    mod = types.ModuleType(name)
+
+    def __getattr__(attr):
+        if attr.startswith('__'):
+            raise AttributeError(attr)
+        return type(attr, (), {'__init__': lambda self, *a, **k: None})
+    mod.__getattr__ = __getattr__
+    mod.__path__ = []
+    return mod
+
+
+def _import_reference():
+    sys.path.insert(0, os.path.join(HERE, 'standin'))
+    sys.path.insert(0, REFERENCE)
+    for name in ('drone3d.visualization.objects', 'drone3d.visualization.utils', 'trimesh', 'trimesh.proximity',
+                 'imgui', 'glfw', 'OpenGL', 'OpenGL.GL'):
+        sys.modules[name] = _inert_module(name)
+    import casadi  # noqa: F401  (the stand-in)
+    assert casadi.__version__.endswith('standin'), casadi.__file__
+
+
+def _ref_line(track, closed):
+    from drone3d.centerlines.base_centerline import GateShape
+    from drone3d.centerlines.spline_centerline import SplineCenterline, SplineCenterlineConfig
+    x, shape = TRACKS[track]
+    cfg = SplineCenterlineConfig(x=np.array(x, float))
+    cfg.closed = closed
+    cfg.gate_shape = GateShape.SQUARE if shape == 'square' else GateShape.CIRCLE
+    return SplineCenterline(cfg)
+
+
+def _configs(line, frame, N, K, rk4, fix_gate_center):
+    ''' as utils/solve_util.py:29-66 builds them '''
+    from drone3d.raceline.base_raceline import GlobalRacelineConfig, ParametricRacelineConfig
+    if frame == 'global':
+        cfg = GlobalRacelineConfig(verbose=False, N=N, K=K, v0=1.0, use_rk4=rk4)
+        cfg.closed = line.config.closed
+        cfg.gate_xi, cfg.gate_xj, cfg.gate_xk = line.config.x[0], line.config.x[1], line.config.x[2]
+    else:
+        cfg = ParametricRacelineConfig(verbose=False, N=N, K=K, v0=1.0, use_rk4=rk4)
+        cfg.closed = line.config.closed
+        cfg.fixed_gates = line.config.s[:-1] if line.config.closed else line.config.s
+    cfg.fix_gate_center = fix_gate_center
+    return cfg
+
+
+def _point_solution(pt, seed):
+    ''' a synthetic point-mass "solution" for the warm start: the point NLP's w0 with a smooth
+    thrust profile (gravity compensation plus a rotating lateral part) and random input rates '''
+    rng = np.random.default_rng(seed)
+    x = np.array(pt.solver_w0, float)
+    N, K1 = pt.config.N, pt.config.K + 1
+    P = N * K1
+    nv = 12
+    phase = np.linspace(0, 2 * np.pi, P, endpoint=False) + rng.uniform(0, 2 * np.pi)
+    for i in range(P):
+        base = N + i * nv
+        x[base + 6:base + 9] = [2.0 * np.sin(phase[i]), 2.0 * np.cos(phase[i]), 9.81 + rng.normal(0, 0.5)]
+        x[base + 9:base + 12] = rng.normal(0, 1.0, 3)
+        x[base + 3:base + 6] *= 1.0 + 0.2 * rng.random()
+    return x
+
+
+def build_reference(cfg):
+    ''' the reference raceline object of one case (NLP built, not solved) '''
+    from drone3d.pytypes import DroneConfig, PointConfig
+    from drone3d.raceline import drone_raceline as dr
+    from drone3d.raceline import point_raceline as pr
+    from drone3d.obstacles.mesh_obstacle import ObstacleFreeTube
+    track, model = cfg.get('track', 'race'), cfg.get('model', 'drone')
+    frame, N, K = cfg.get('frame', 'parametric'), cfg['N'], cfg['K']
+    use_quat, global_r = cfg.get('use_quat', True), cfg.get('global_r', True)
+    rk4, closed = cfg.get('rk4', False), cfg.get('closed', True)
+    line = _ref_line(track, closed)
+    conf = _configs(line, frame, N, K, rk4, cfg.get('fix_gate_center', False))
+    extra = {}
+    if cfg.get('spheres'):
+        # a given tube (the mesh search itself is pinned separately): one sphere per node s
+        rng = np.random.default_rng(100 + cfg['spheres'])
+        probe = (pr.ParametricPointRaceline if model == 'point' else dr.ParametricDroneRaceline)
+        s_nodes = np.array([probe._get_s(_SProbe(line, conf), n, k) for n in range(N) for k in range(K + 1)])
+        P = len(s_nodes)
+        veh = DroneConfig(global_r=global_r, use_quat=use_quat) if model == 'drone' else PointConfig(global_r=global_r)
+        ball_p = np.stack([s_nodes, rng.normal(0, 0.4, P), rng.normal(0, 0.4, P)], axis=1)
+        ball_r = rng.uniform(0.2, 1.5, P)
+        tube = ObstacleFreeTube(line, np.zeros((P, 3)), ball_r, np.zeros((P, 3)), ball_p, veh.collision_radius)
+        if model == 'point':
+            obj = pr.ParametricObstaclePointRaceline(line, conf, veh, None, tube=tube)
+        else:
+            obj = dr.ParametricObstacleDroneRaceline(line, conf, veh, None, tube=tube, generate_ws=False)
+        extra['spheres'] = np.stack([ball_p[:, 1], ball_p[:, 2], np.maximum(ball_r - veh.collision_radius, 0.01)],
+                                    axis=1)
+        return obj, extra
+    if cfg.get('warm'):
+        pconf = conf.copy()
+        pcls = pr.GlobalPointRaceline if frame == 'global' else pr.ParametricPointRaceline
+        point = pcls(line, pconf, PointConfig(global_r=global_r))
+        xp = _point_solution(point, cfg['warm'])
+        ws = point._unpack_soln({'x': xp})
+        veh = DroneConfig(global_r=global_r, use_quat=use_quat)
+        dcls = dr.GlobalDroneRaceline if frame == 'global' else dr.ParametricDroneRaceline
+        extra['x_point'] = xp
+        try:
+            obj = dcls(line, conf, veh, ws_raceline=ws, ws_model=point.model, generate_ws=False)
+        except NotImplementedError as exc:
+            extra['error'] = np.array(f'NotImplementedError: {exc}')
+            return None, extra
+        extra['ws_first_r'] = np.array(obj._first_ws_r, float)
+        extra['ws_last_r'] = np.array(obj._last_ws_r, float)
+        return obj, extra
+    if model == 'drone':
+        veh = DroneConfig(global_r=global_r, use_quat=use_quat)
+        cls = dr.GlobalDroneRaceline if frame == 'global' else dr.ParametricDroneRaceline
+        return cls(line, conf, veh, generate_ws=False), extra
+    veh = PointConfig(global_r=global_r)
+    cls = pr.GlobalPointRaceline if frame == 'global' else pr.ParametricPointRaceline
+    return cls(line, conf, veh), extra
+
+
+class _SProbe:
+    ''' just enough state for BaseParametricRaceline._get_s (base_raceline.py:972-984) '''
+
+    def __init__(self, line, conf):
+        self.line, self.config, self.nlp = line, conf, {}
+
+
+def _points(w0, N, rng, n=2, scale=0.05):
+    ''' seeded evaluation points near w0 (same rule as tests/helpers.random_w) '''
+    W = []
+    for _ in range(n):
+        w = w0 + scale * rng.standard_normal(w0.shape)
+        w[:N] = np.abs(w0[:N]) * (1 + 0.2 * rng.random(N))
+        W.append(w)
+    return np.array(W)
+
+
+def evaluate_nlp(obj, W):
+    ''' g, f (float evaluation) and J, grad f (complex step) of the reference NLP at the rows of W '''
+    import casadi as ca
+    w_sym = obj.nlp['w'].entries()
+    g_ent = ca.vertcat(obj.nlp['g']).entries() if obj.nlp['g'].numel() else []
+    f_ent = ca._to_mat(obj.nlp['J']).entries()
+    order = ca._topo(list(g_ent) + list(f_ent))
+    nw = len(w_sym)
+    G, F, GF, JD = [], [], [], []
+    for w in W:
+        val = ca.evaluate(order, {s.id: float(v) for s, v in zip(w_sym, w)})
+        G.append([float(val[e.id]) if isinstance(e, ca._N) else float(e) for e in g_ent])
+        F.append(float(val[f_ent[0].id]) if isinstance(f_ent[0], ca._N) else float(f_ent[0]))
+        hstep = 1e-100
+        leaf = {}
+        for j, (s, v) in enumerate(zip(w_sym, w)):
+            a = np.full(nw, complex(v))
+            a[j] += 1j * hstep
+            leaf[s.id] = a
+        val = ca.evaluate(order, leaf)
+        Jd = np.zeros((len(g_ent), nw))
+        for i, e in enumerate(g_ent):
+            if isinstance(e, ca._N):
+                Jd[i] = np.imag(val[e.id]) / hstep
+        JD.append(Jd)
+        GF.append(np.imag(val[f_ent[0].id]) / hstep if isinstance(f_ent[0], ca._N) else np.zeros(nw))
+    return np.array(G), np.array(F), np.array(GF), np.array(JD)
+
+
+def make_case(name, cfg, seed):
+    t0 = time.time()
+    obj, extra = build_reference(cfg)
+    if obj is None:
+        np.savez_compressed(os.path.join(OUT, f'{name}.npz'), cfg=np.array(json.dumps(cfg)), **extra)
+        print(f'{name}: {extra["error"]}', flush=True)
+        return
+    w0 = np.array(obj.solver_w0, float)
+    N = obj.config.N
+    W = _points(w0, N, np.random.default_rng(seed))
+    G, F, GF, JD = evaluate_nlp(obj, W)
+    nz = np.nonzero(np.any(JD != 0, axis=0))
+    out = dict(cfg=np.array(json.dumps(cfg)), nw=np.array(len(w0)), ng=np.array(G.shape[1]),
+               N_ref=np.array(N), K_ref=np.array(obj.config.K),
+               w0=w0, lbw=np.array(obj.solver_lbw, float), ubw=np.array(obj.solver_ubw, float),
+               lbg=np.array(obj.solver_lbg, float), ubg=np.array(obj.solver_ubg, float),
+               W=W, G=G, F=F, GF=GF, J_row=nz[0].astype(np.int32), J_col=nz[1].astype(np.int32),
+               J_val=JD[:, nz[0], nz[1]], **extra)
+    np.savez_compressed(os.path.join(OUT, f'{name}.npz'), **out)
+    print(f'{name}: nw={len(w0)} ng={G.shape[1]} nnz={len(nz[0])} ({time.time() - t0:.1f} s)', flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--only', default=None)
+    a = ap.parse_args()
+    _import_reference()
+    os.makedirs(OUT, exist_ok=True)
+    for i, (name, cfg) in enumerate(CASES.items()):
+        if a.only and a.only != name:
+            continue
+        make_case(name, cfg, seed=1000 + i)
+
+
+if __name__ == '__main__':
+    main()

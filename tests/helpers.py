@@ -22,13 +22,15 @@ def oracle_line(track, closed=True):
 
 
 def oracle_nlp(track='race', model='drone', frame='parametric', N=50, K=4, use_quat=True, global_r=True,
-               fix_gate_center=False, quat_flip=False, spheres=None, v0=1.0, h0=1, rk4=False, closed=True):
+               fix_gate_center=False, quat_flip=False, spheres=None, v0=1.0, h0=1, rk4=False, closed=True,
+               euler_wraps=0.0):
     from oracle.ref_transcription import RefNLP
     line = oracle_line(track, closed)
     veh = {'use_quat': use_quat, 'global_r': global_r} if model == 'drone' else {'global_r': global_r}
     fixed = (line.s[:-1] if closed else line.s) if frame == 'parametric' else None
     return RefNLP(line, model, frame, N, K, veh=veh, fix_gate_center=fix_gate_center, fixed_gates=fixed,
-                  quat_flip=quat_flip, spheres=spheres, v0=v0, h0=h0, rk4=rk4, closed=closed)
+                  quat_flip=quat_flip, spheres=spheres, v0=v0, h0=h0, rk4=rk4, closed=closed,
+                  euler_wraps=euler_wraps)
 
 
 def random_w(spec_or_nlp, rng, scale=0.05):
@@ -187,3 +189,37 @@ def var_stages(spec):
     st[:spec.N] = np.arange(spec.N)
     st[spec.N:] = np.repeat(np.arange(spec.P) // spec.K1, spec.nv)
     return st
+
+
+# ------------------------------------------------------------------ golden fixtures of the reference's own transcription
+GOLDEN_DIR = os.path.join(REPO, 'tests', 'golden', 'transcription')
+
+
+def golden_names():
+    return sorted(f[:-4] for f in os.listdir(GOLDEN_DIR) if f.endswith('.npz'))
+
+
+def golden_case(name):
+    ''' (fixture dict, keyword arguments for product_spec / oracle_nlp) of one golden case
+    (tests/golden/make_transcription_golden.py). Warm-started cases carry the closure sign /
+    Euler wraps the reference derives from its first and last guessed attitude
+    (drone_raceline.py:81-95). '''
+    import json
+    d = dict(np.load(os.path.join(GOLDEN_DIR, f'{name}.npz')))
+    cfg = json.loads(str(d['cfg']))
+    kw = {k: v for k, v in cfg.items() if k not in ('spheres', 'warm')}
+    if 'spheres' in d:
+        kw['spheres'] = d['spheres']
+    if 'ws_first_r' in d:
+        first, last = d['ws_first_r'], d['ws_last_r']
+        if kw.get('use_quat', True):
+            kw['quat_flip'] = bool(np.linalg.norm(first - last) > 1)
+        else:
+            kw['euler_wraps'] = float(np.round((last - first)[0] / 2 / np.pi))
+    return d, kw
+
+
+def golden_jacobian(d, i):
+    J = np.zeros((int(d['ng']), int(d['nw'])))
+    J[d['J_row'], d['J_col']] = d['J_val'][i]
+    return J
