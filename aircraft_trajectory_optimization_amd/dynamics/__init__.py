@@ -1,0 +1,11 @@
+'''
+Host (numpy) vehicle models with the reference's model-operator surface
+(drone3d/dynamics: f_zdot, f_zdot_full, f_param_terms, f_R, f_T, f_Fg, f_vg, f_Tp,
+get_rk4_dynamics, step, state packing and bounds). The device evaluates the same equations in
+csrc/ato_models.hpp.
+'''
+from aircraft_trajectory_optimization_amd.dynamics.drone_models import DroneModel, ParametricDroneModel  # noqa: F401
+from aircraft_trajectory_optimization_amd.dynamics.dynamics_model import DynamicsModel, \
+    InterpolatedDynamicsModel, ParametricDynamicsModel  # noqa: F401
+from aircraft_trajectory_optimization_amd.dynamics.point_model import ParametricPointModel, PointModel  # noqa: F401
+from aircraft_trajectory_optimization_amd.dynamics.rotations import Parameterization, Reference, Rotation  # noqa: F401

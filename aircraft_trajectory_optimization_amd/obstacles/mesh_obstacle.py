@@ -10,7 +10,7 @@ brute-force largest-empty-sphere search (nr = 5 radii x nth = 8 angles around ea
 '''
 import ctypes
 import os
-from typing import Optional, Tuple
+from typing import Dict, Optional, Tuple
 
 import numpy as np
 
@@ -131,3 +131,25 @@ class ObstacleFreeTube:
     def sphere_table(self, node_s: np.ndarray) -> np.ndarray:
         ''' [P, 3] table consumed by the sphere rows of the HIP programs '''
         return np.array([self.sphere(s) for s in node_s], float)
+
+    def get_vertex_objects(self, ubo=None) -> Dict[str, 'TubeDrawable']:
+        ''' the drawables the reference's viewer adds for the tube (mesh_obstacle.py:239-275), as data:
+        instance centres, scales and (planning tube) orientations '''
+        # pylint: disable=unused-argument
+        P = self.ball_center.shape[0]
+        Rp = np.stack([self.line.p2Rp(float(s)) for s in self.ball_p[:, 0]]) if P else np.zeros((0, 3, 3))
+        return {
+            'Planning Tube': TubeDrawable(self.ball_center, np.maximum(self.ball_r - self.collision_r, 0.01), Rp),
+            'Free-Space Spheres': TubeDrawable(self.ball_center, self.ball_r),
+            'Sphere Centers': TubeDrawable(self.ball_center, np.full(P, 0.05)),
+            'Sphere Contact Points': TubeDrawable(self.ball_tangent_pts, np.full(P, 0.05)),
+        }
+
+
+class TubeDrawable:
+    ''' instanced drawable as plain data (no renderer in this build) '''
+
+    def __init__(self, centers, scales, orientations=None):
+        self.centers = np.asarray(centers, float)
+        self.scales = np.asarray(scales, float)
+        self.orientations = orientations

@@ -22,8 +22,7 @@ from typing import Dict, List, Optional, Tuple
 import numpy as np
 
 from aircraft_trajectory_optimization_amd.centerlines.base_centerline import BaseCenterline
-from aircraft_trajectory_optimization_amd.pytypes import DroneConfig, DroneState, GlobalEulerAngles, \
-    GlobalQuaternion, PointConfig, PointState, RelativeEulerAngles, RelativeQuaternion
+from aircraft_trajectory_optimization_amd.pytypes import DroneConfig, PointConfig
 from aircraft_trajectory_optimization_amd.raceline.config import GlobalRacelineConfig, \
     ParametricRacelineConfig, RacelineConfig, RacelineResults
 from aircraft_trajectory_optimization_amd.raceline.problem import ProblemSpec
@@ -34,61 +33,14 @@ from aircraft_trajectory_optimization_amd.utils.discretization_utils import inte
 _SOLUTIONS: Dict[int, Tuple[ProblemSpec, np.ndarray, RacelineResults]] = {}
 
 
-class RacelineModel:
-    ''' the parts of the reference DynamicsModel the scripts and viewers use '''
-
-    def __init__(self, spec: ProblemSpec):
-        self.spec = spec
-        self.config = spec.vehicle
-
-    def get_empty_state(self):
-        return DroneState() if self.spec.is_drone else PointState()
-
-    def _R_global(self, z) -> np.ndarray:
-        sp_, v = self.spec, self.spec.vehicle
-        if sp_.is_drone:
-            if v.use_quat:
-                q = GlobalQuaternion()
-                q.from_vec(z[3:7])
-                R = q.R()
-            else:
-                e = GlobalEulerAngles()
-                e.from_vec(z[3:6])
-                R = e.R()
-            if sp_.param and not v.global_r:
-                R = self.spec.line.p2Rp(z[0]) @ R
-            return R
-        if sp_.param and not v.global_r:
-            return self.spec.line.p2Rp(z[0])
-        return np.eye(3)
-
-    def zu2state(self, state, z, u, last_q=None):
-        ''' node state, input (drone_models.py:162-183, :306-328; point_model.py) '''
-        sp_ = self.spec
-        state.u.from_vec(u)
-        if sp_.param:
-            state.p.from_vec(z[:3])
-            state.x.from_vec(sp_.line.p2x(*z[:3]))
-        else:
-            state.x.from_vec(z[:3])
-        if sp_.is_drone:
-            nr = 4 if sp_.vehicle.use_quat else 3
-            if sp_.vehicle.use_quat:
-                state.r = GlobalQuaternion() if sp_.vehicle.global_r else RelativeQuaternion()
-            else:
-                state.r = GlobalEulerAngles() if sp_.vehicle.global_r else RelativeEulerAngles()
-            state.r.from_vec(z[3:3 + nr])
-            state.v.from_vec(z[3 + nr:6 + nr])
-            state.w.from_vec(z[6 + nr:9 + nr])
-        else:
-            state.v.from_vec(z[3:6])
-        if sp_.is_drone and sp_.vehicle.use_quat and not sp_.param:
-            state.q.from_vec(z[3:7])
-        else:
-            state.q.from_mat(self._R_global(z))
-            if last_q is not None and np.linalg.norm(last_q - state.q.to_vec()) > 1.8:
-                state.q.from_vec(-state.q.to_vec())
-        return state.q.to_vec()
+def make_model(spec: ProblemSpec):
+    ''' the dynamics model of a problem, as the reference's _get_model builds it
+    (drone_raceline.py:314-316, :353-357; point_raceline.py:51-68) '''
+    from aircraft_trajectory_optimization_amd.dynamics import DroneModel, ParametricDroneModel, \
+        ParametricPointModel, PointModel
+    if spec.is_drone:
+        return ParametricDroneModel(spec.vehicle, spec.line) if spec.param else DroneModel(spec.vehicle)
+    return ParametricPointModel(spec.vehicle, spec.line) if spec.param else PointModel(spec.vehicle)
 
 
 class _Raceline:
@@ -117,7 +69,7 @@ class _Raceline:
                                 sphere_table=self.sphere_table)
         if w_guess is not None:
             self.spec.w0, self.spec.lbw, self.spec.ubw = w_guess
-        self.model = RacelineModel(self.spec)
+        self.model = make_model(self.spec)
         self.evaluator = factory(self.spec)
         self.global_frame = not self.spec.param
         self.solve_time = self.ipopt_time = self.feval_time = 0.0
@@ -154,14 +106,13 @@ class _Raceline:
         nodes = x[N:].reshape(N * K1, sp_.nv)
         Z, U, dU = nodes[:, :nz], nodes[:, nz:nz + nu], nodes[:, nz + nu:]
         states = []
-        last_q = None
         for n in range(N):
             for k in range(K1):
                 i = n * K1 + k
                 st = self.model.get_empty_state()
                 st.t = float(t0[n] + sp_.tau[k] * h[n])
-                last_q = self.model.zu2state(st, Z[i], U[i], last_q)
-                st.du.from_vec(dU[i])
+                self.model.zu2state(st, Z[i], U[i])
+                self.model.du2state(st, dU[i])
                 states.append(st)
         if sp_.rk4:
             zi, ui, dui = interpolate_linear(h, Z), interpolate_linear(h, U), interpolate_linear(h, dU)
@@ -193,7 +144,7 @@ def _point_guess(solver_cls, line, config, vehicle_config: DroneConfig, generate
     if ws_raceline is None or id(ws_raceline) not in _SOLUTIONS:
         return ws_solver, ws_raceline, None, None
     pspec, x, _ = _SOLUTIONS[id(ws_raceline)]
-    return ws_solver, ws_raceline, RacelineModel(pspec), (pspec, x)
+    return ws_solver, ws_raceline, make_model(pspec), (pspec, x)
 
 
 class _DroneRaceline(_Raceline):
@@ -262,6 +213,10 @@ class _ObstacleMixin:
     def _after_setup(self):
         if self.calc_tube_time > 0:
             self.setup_time -= self.calc_tube_time
+
+    def triangulate_setup_info(self, ubo=None) -> Dict[str, object]:
+        ''' drawables of the obstacle-free tube (base_raceline.py:1329-1331) '''
+        return self.tube.get_vertex_objects(ubo)
 
     def _unpack(self, x, feasible) -> RacelineResults:
         out = super()._unpack(x, feasible)

@@ -274,12 +274,95 @@ def make_case(name, cfg, seed):
     print(f'{name}: nw={len(w0)} ng={G.shape[1]} nnz={len(nz[0])} ({time.time() - t0:.1f} s)', flush=True)
 
 
+MODELS = {
+    # name: (class, vehicle kwargs, parametric track or None)
+    'drone_global_esp': ('DroneModel', dict(global_r=True, use_quat=True), None),
+    'drone_global_ypr': ('DroneModel', dict(global_r=True, use_quat=False), None),
+    'drone_param_esp': ('ParametricDroneModel', dict(global_r=True, use_quat=True), 'race'),
+    'drone_param_esp_rel': ('ParametricDroneModel', dict(global_r=False, use_quat=True), 'fig8'),
+    'drone_param_ypr_rel': ('ParametricDroneModel', dict(global_r=False, use_quat=False), 'race'),
+    'point_global': ('PointModel', dict(global_r=True), None),
+    'point_param': ('ParametricPointModel', dict(global_r=True), 'race'),
+    'point_param_rel': ('ParametricPointModel', dict(global_r=False), 'fig8'),
+}
+
+
+def make_models(seed=7):
+    ''' the reference's model operator (dynamics_model.py:150-198, :262-349; drone_models.py;
+    point_model.py) at seeded states: f_zdot, f_zdot_full, f_param_terms, f_R, f_T, f_Fg, f_vg, f_Tp '''
+    from drone3d.pytypes import DroneConfig, PointConfig
+    from drone3d.dynamics import drone_models, point_model
+    rng = np.random.default_rng(seed)
+    out = {}
+    for name, (cls_name, vkw, track) in MODELS.items():
+        mod = drone_models if cls_name.startswith(('Drone', 'ParametricDrone')) else point_model
+        cls = getattr(mod, cls_name)
+        veh = (DroneConfig if 'Drone' in cls_name else PointConfig)(**vkw)
+        model = cls(veh, _ref_line(track, True)) if track else cls(veh)
+        nz = model.f_zdot.size_in(0)[0]
+        nu = model.f_zdot.size_in(1)[0]
+        Z, U, res = [], [], {k: [] for k in ('zdot', 'zdot_full', 'terms', 'R', 'T', 'Fg', 'vg', 'Tp')}
+        for _ in range(4):
+            z = rng.normal(0, 0.5, nz)
+            if track:
+                z[0] = rng.uniform(0.2, 6.8)
+            if nz == 13:
+                z[3:7] = z[3:7] + np.array([0, 0, 0, 1.0])
+            u = rng.uniform(0.5, 5.0, nu)
+            Z.append(z)
+            U.append(u)
+            res['zdot'].append(np.array(model.f_zdot(z, u), float).reshape(-1))
+            res['R'].append(np.array(model.f_R(z, u), float).reshape(3, 3))
+            res['T'].append(np.array(model.f_T(z, u), float).reshape(-1))
+            res['Fg'].append(np.array(model.f_Fg(z, u), float).reshape(-1))
+            res['vg'].append(np.array(model.f_vg(z, u), float).reshape(-1))
+            if track:
+                terms = np.array(model.f_param_terms(z[0]), float).reshape(-1)
+                res['terms'].append(terms)
+                res['zdot_full'].append(np.array(model.f_zdot_full(z, u, terms), float).reshape(-1))
+                res['Tp'].append(np.array(model.f_Tp(z, u), float).reshape(-1))
+        out[f'{name}/Z'] = np.array(Z)
+        out[f'{name}/U'] = np.array(U)
+        for k, v in res.items():
+            if v:
+                out[f'{name}/{k}'] = np.array(v)
+    np.savez_compressed(os.path.join(HERE, 'models.npz'), **out)
+    print(f'models: {len(MODELS)} models', flush=True)
+
+
+def make_cpc():
+    ''' utils/cpc_utils.py:14-101 on the reference's CPC trajectories, both tracks '''
+    from drone3d.utils.cpc_utils import package_cpc_data_as_raceline
+    from drone3d.utils.load_utils import get_assets_file
+    out = {}
+    for name, track, clip in (('race', 'race', True), ('fig8', 'fig8', False), ('fig8_clip', 'fig8', True)):
+        csv = 'cpc_race_raceline.csv' if track == 'race' else 'cpc_warmstart_raceline.csv'
+        res, model = package_cpc_data_as_raceline(get_assets_file(csv), _ref_line(track, True), clip=clip)
+        t = np.array([s.t for s in res.states])
+        tq = np.linspace(-0.2, float(t[-1]) + 0.2, 41)
+        out[f'{name}/time'] = np.array(res.time)
+        out[f'{name}/t'] = t
+        out[f'{name}/x'] = np.array([s.x.to_vec() for s in res.states])
+        out[f'{name}/q'] = np.array([s.q.to_vec() for s in res.states])
+        out[f'{name}/tq'] = tq
+        out[f'{name}/z'] = np.array([res.z_interp(v) for v in tq])
+        out[f'{name}/u'] = np.array([res.u_interp(v) for v in tq])
+        out[f'{name}/du'] = np.array([res.du_interp(v) for v in tq])
+        out[f'{name}/R'] = np.array([model.f_R(res.z_interp(v), res.u_interp(v)) for v in tq[::8]])
+    np.savez_compressed(os.path.join(HERE, 'cpc.npz'), **out)
+    print('cpc: done', flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--only', default=None)
     a = ap.parse_args()
     _import_reference()
     os.makedirs(OUT, exist_ok=True)
+    if a.only in (None, 'models'):
+        make_models()
+    if a.only in (None, 'cpc'):
+        make_cpc()
     for i, (name, cfg) in enumerate(CASES.items()):
         if a.only and a.only != name:
             continue

@@ -74,3 +74,84 @@ def test_solve_util_unsolved_returns_guess(cpu_evaluator):
     solver, guess = solve_util(line=_fig8_line(), global_frame=True, drone=False, solve=False, N=7, verbose=False)
     assert not guess.feasible and guess.label == 'Global PM'
     assert guess.states[0].x.to_vec().shape == (3,)
+
+
+def test_script_surface_resolves():
+    ''' every module, name and call scripts/{race,fig_8,fig_8_cpc,obstacles,no_obstacles}.py use '''
+    import importlib
+    names = {
+        'drone3d.pytypes': ['DroneConfig'],
+        'drone3d.centerlines.base_centerline': ['GateShape'],
+        'drone3d.centerlines.spline_centerline': ['SplineCenterline', 'SplineCenterlineConfig'],
+        'drone3d.visualization.drone_raceline_fig': ['DroneRacelineWindow'],
+        'drone3d.utils.load_utils': ['get_assets_file'],
+        'drone3d.utils.cpc_utils': ['package_cpc_data_as_raceline'],
+        'drone3d.utils.solve_util': ['solve_util'],
+        'drone3d.raceline.base_raceline': ['ParametricRacelineConfig', 'GlobalRacelineConfig', 'RacelineResults'],
+        'drone3d.raceline.drone_raceline': ['ParametricObstacleDroneRaceline', 'GlobalDroneRaceline',
+                                            'ParametricDroneRaceline'],
+        'drone3d.obstacles.mesh_obstacle': ['MeshObstacle', 'ObstacleFreeTube'],
+        'drone3d.dynamics.dynamics_model': ['DynamicsModel', 'ParametricDynamicsModel',
+                                            'InterpolatedDynamicsModel'],
+        'drone3d.dynamics.drone_models': ['DroneModel', 'ParametricDroneModel'],
+        'drone3d.dynamics.point_model': ['PointModel', 'ParametricPointModel'],
+    }
+    for mod, attrs in names.items():
+        m = importlib.import_module(mod)
+        for a in attrs:
+            assert hasattr(m, a), f'{mod}.{a}'
+    from drone3d.raceline.drone_raceline import ParametricObstacleDroneRaceline
+    assert callable(getattr(ParametricObstacleDroneRaceline, 'triangulate_setup_info'))
+    from drone3d.utils.load_utils import get_assets_file
+    import os
+    for f in ('cpc_race_raceline.csv', 'cpc_warmstart_raceline.csv'):
+        assert os.path.exists(get_assets_file(f))
+
+
+def test_headless_window_calls_of_obstacles_py():
+    ''' obstacles.py:57-68: window.ubo, add_object, update_projection, run '''
+    from drone3d.visualization.drone_raceline_fig import DroneRacelineWindow
+    from aircraft_trajectory_optimization_amd.obstacles.mesh_obstacle import ObstacleFreeTube
+    line = _fig8_line()
+    window = DroneRacelineWindow(line, [], [], obstacles={'Environment': object()}, fullscreen=False, run=False)
+    P = 6
+    s = np.linspace(0.1, 6.0, P)
+    tube = ObstacleFreeTube(line, np.zeros((P, 3)), np.full(P, 0.6), np.zeros((P, 3)),
+                            np.stack([s, np.zeros(P), np.zeros(P)], 1), 0.4)
+    objs = tube.get_vertex_objects(window.ubo)
+    assert set(objs) == {'Planning Tube', 'Free-Space Spheres', 'Sphere Centers', 'Sphere Contact Points'}
+    for name, obj in objs.items():
+        window.add_object(name, obj, show=False)
+    window.update_projection()
+    window.run()
+    assert window.should_close and len(window.objects) == 4
+    np.testing.assert_allclose(objs['Planning Tube'].scales, 0.2)
+
+
+def test_solver_model_is_the_dynamics_operator(cpu_evaluator):
+    ''' solver.model / ws_model are the reference's model classes (f_zdot, f_R, f_T, f_vg ...) '''
+    from drone3d.utils.solve_util import solve_util
+    from aircraft_trajectory_optimization_amd.dynamics import ParametricDroneModel, ParametricPointModel
+    solver, guess = solve_util(line=_fig8_line(), global_frame=False, drone=True, use_quaternion=True,
+                               solve=False, N=6, verbose=False)
+    assert isinstance(solver.model, ParametricDroneModel)
+    st = guess.states[0]
+    z, u = solver.model.state2zu(st)
+    assert solver.model.f_zdot(z, u).shape == (13,)
+    np.testing.assert_allclose(solver.model.f_R(z, u) @ solver.model.f_R(z, u).T, np.eye(3), atol=1e-12)
+    _, pguess = solve_util(line=_fig8_line(), global_frame=False, drone=False, solve=False, N=6, verbose=False)
+    assert pguess.states[0].q.to_vec().shape == (4,)
+    assert isinstance(solvers.make_model(solvers.ProblemSpec(_fig8_line(), _pconfig(), _pveh(), 'parametric')),
+                      ParametricPointModel)
+
+
+def _pconfig():
+    from drone3d.raceline.base_raceline import ParametricRacelineConfig
+    c = ParametricRacelineConfig(verbose=False, N=4, K=2)
+    c.closed = True
+    return c
+
+
+def _pveh():
+    from aircraft_trajectory_optimization_amd.pytypes import PointConfig
+    return PointConfig(global_r=True)
