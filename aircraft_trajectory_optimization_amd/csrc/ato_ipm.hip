@@ -656,7 +656,7 @@ int ato_ipm_filter_accept(int32_t W, int32_t fmax, const double* theta, const do
     if (!theta || !phi || !gphi_d || !alpha || !tht || !pht || (fmax && !F) || !nf || !theta_max || !theta_min ||
         !pend || !first || !ok || !arm || !soc)
         return fail(ATO_ERR_ARG, "ato_ipm_filter_accept: arguments");
-    const FilterPrm o{prm[0], prm[1], prm[2], prm[3], prm[4], prm[5]};
+    const FilterPrm o{prm[0], prm[1], prm[2], prm[3], prm[4], prm[5]};   // prm: host array (ato_ipm.h)
     hipLaunchKernelGGL(k_filter_accept, dim3((W + CB - 1) / CB), dim3(CB), 0, static_cast<hipStream_t>(stream), W,
                        fmax, theta, phi, gphi_d, alpha, tht, pht, F, nf, theta_max, theta_min, pend, first, o, ok,
                        arm, soc);

@@ -931,7 +931,13 @@ class BatchedInteriorPoint:
                 laps.lap('resto_post')
 
         for j in inflight:                           # (the lockstep bound ended the loop first)
-            self._resto_collect(j, cols, x, B0)
+            R, xr, okr = self._resto_collect(j, cols, x, B0)
+            # the phase finished after the last lockstep iteration: restored columns keep their
+            # restored point, but none of them iterated again (MAX_ITER); failed ones LS_FAILED
+            x = torch.where((R & okr)[None, :], xr, x)
+            status = torch.where(R & okr & (status == RUNNING), torch.full_like(status, MAX_ITER), status)
+            status = torch.where(R & ~okr & (status == RUNNING), torch.full_like(status, LS_FAILED), status)
+        status = torch.where(status == RUNNING, torch.full_like(status, MAX_ITER), status)
         if getattr(self, '_async_pool', None) is not None:
             self._async_pool.shutdown(wait=True)
             self._async_pool = None
@@ -1106,6 +1112,9 @@ class BatchedInteriorPoint:
             sets.append(res)
         if getattr(self, '_async_pool', None) is None:
             self._async_pool = ThreadPoolExecutor(max_workers=self.ASYNC_PHASES)
+        if getattr(self, '_resto_structure', None) is None:
+            # built here, on the calling thread, before any worker can need it
+            self._resto_structure = _RestorationStructure(keep['ev'])
         job = self._resto_prepare(R, x, g, mu, theta, F, nf)
         job['orig'] = cols.index_select(0, job['sel'])
         self.stats['async_phases'] = self.stats.get('async_phases', 0) + 1

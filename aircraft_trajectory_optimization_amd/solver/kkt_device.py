@@ -100,12 +100,14 @@ class DeviceKKT:
         if rc != 0:
             raise RuntimeError(f'libato KKT error {rc}: {self.lib.ato_last_error().decode()}')
 
-    def _list(self, idx: Optional[Sequence[int]]):
+    def _list(self, idx: Optional[Sequence[int]], cap: Optional[int] = None):
+        ''' device instance list; entries must lie in [0, cap) (the library does not bound-check) '''
+        cap = self.cap if cap is None else cap
         if idx is None:
-            return None, self.cap
+            return None, cap
         idx = np.asarray(idx, dtype=np.int32).reshape(-1)
-        if len(idx) and (idx.min() < 0 or idx.max() >= self.cap):
-            raise ValueError(f'instance index out of range [0, {self.cap})')
+        if len(idx) and (idx.min() < 0 or idx.max() >= cap):
+            raise ValueError(f'instance index out of range [0, {cap})')
         t = torch.as_tensor(idx, device=self.device)
         return t, len(idx)
 
@@ -201,7 +203,7 @@ class _KKTView:
             if t.dtype != torch.float64 or t.dim() != 2 or t.shape[1] != self.cap or t.device != self.device:
                 raise ValueError('KKT view values must be fp64 [elements][count] tensors on the KKT device')
         self._keep_vals = (H, J, dx, dr)
-        lst, nb = b._list(instances)
+        lst, nb = b._list(instances, self.cap)
         if instances is None:
             nb = self.cap
         st = stream if stream is not None else torch.cuda.current_stream(self.device)
@@ -222,7 +224,7 @@ class _KKTView:
         if x.dtype != torch.float64 or x.shape != (self.plan.dim, self.cap) or not x.is_contiguous() or \
                 x.device != self.device:
             raise ValueError('x must be a contiguous fp64 [dim][count] tensor on the KKT device')
-        lst, nb = b._list(instances)
+        lst, nb = b._list(instances, self.cap)
         if instances is None:
             nb = self.cap
         st = stream if stream is not None else torch.cuda.current_stream(self.device)

@@ -27,7 +27,8 @@ diagonal by interval, almost every row touches one interval or two neighbouring 
            the interval interiors (all other variables of the interval and the rows touching
            only it): independent fronts, all eliminated in parallel; the anchors pin nothing
            inside a leaf, so the collocation defects there determine the later nodes and the
-           leaf blocks stay non-singular. Separators are joined by recursive bisection, the
+           leaf blocks stay non-singular (interior rows that touch only anchors join the
+           separator). Separators are joined by recursive bisection, the
            border rows (loop closure, equal step sizes: rows spanning non-neighbouring
            intervals) form the root. The critical path of one factorisation is one leaf plus
            log2(N) separators instead of the whole chain. Variable / row pairs isolated inside an
@@ -147,6 +148,13 @@ def _fronts_nd(n, var_stage, lo, hi, j_row_ptr, j_col, split_pairs=True):
     jc = np.asarray(j_col)
     sel = link[jr] & (var_stage[jc] == hi[jr])
     anchor[jc[sel]] = True
+    # interior rows whose every entry sits on anchors (e.g. a global-frame gate row on Z[n,0][:3],
+    # whose position the continuity rows make anchors) have no variable inside the leaf: in the
+    # leaf their own column would hold only the row diagonal (a zero pivot for an equality row,
+    # i.e. a spurious singular KKT). They join the separator that owns their anchors instead.
+    has_inner = np.zeros(m, bool)
+    has_inner[jr[interior[jr] & ~anchor[jc]]] = True
+    anchor_only = interior & ~has_inner & (lo >= 1)
     own: List[np.ndarray] = []
     children: List[List[int]] = []
     # isolated pairs: an interior variable whose only Jacobian entry is in an interior row of its
@@ -177,7 +185,8 @@ def _fronts_nd(n, var_stage, lo, hi, j_row_ptr, j_col, split_pairs=True):
             children.append([])
     leaf_id = []
     for st in range(S):                          # leaves
-        inner = np.concatenate([np.nonzero((var_stage == st) & ~anchor)[0], n + np.nonzero(interior & (lo == st))[0]])
+        inner = np.concatenate([np.nonzero((var_stage == st) & ~anchor)[0],
+                                n + np.nonzero(interior & ~anchor_only & (lo == st))[0]])
         if len(pre[st]):
             inner = inner[~np.isin(inner, pre[st])]
         leaf_id.append(len(own))
@@ -185,7 +194,8 @@ def _fronts_nd(n, var_stage, lo, hi, j_row_ptr, j_col, split_pairs=True):
         children.append([pre_id[st]] if pre_id[st] >= 0 else [])
 
     def sep(j):
-        return np.concatenate([np.nonzero((var_stage == j) & anchor)[0], n + np.nonzero(link & (hi == j))[0]])
+        return np.concatenate([np.nonzero((var_stage == j) & anchor)[0],
+                               n + np.nonzero((link | anchor_only) & (hi == j))[0]])
 
     def build(a, b):                            # subtree over intervals a..b (boundaries a+1..b)
         if a == b:

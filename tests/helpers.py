@@ -223,3 +223,31 @@ def golden_jacobian(d, i):
     J = np.zeros((int(d['ng']), int(d['nw'])))
     J[d['J_row'], d['J_col']] = d['J_val'][i]
     return J
+
+
+# ------------------------------------------------------------------ KKT certificate against the oracle
+def kkt_certificate(nlp, x, lam_g, lam_x, lbw, ubw):
+    '''
+    First-order optimality of x for the reference NLP as the ORACLE states it (not the product's
+    evaluator): {primal, dual, compl} in unscaled quantities.
+      primal  max violation of lbg <= g(x) <= ubg and lbw <= x <= ubw
+      dual    |grad f + J^T lam_g + lam_x|_inf            (IPOPT's sign convention)
+      compl   max over active-multiplier constraints of |multiplier| * distance to its bound
+    '''
+    x = np.asarray(x, float)
+    lam_g, lam_x = np.asarray(lam_g, float), np.asarray(lam_x, float)
+    g = nlp.g(x)
+    lbg, ubg = np.asarray(nlp.lbg, float), np.asarray(nlp.ubg, float)
+    lbw, ubw = np.asarray(lbw, float), np.asarray(ubw, float)
+    primal = max(np.max(np.maximum(lbg - g, 0), initial=0), np.max(np.maximum(g - ubg, 0), initial=0),
+                 np.max(np.maximum(lbw - x, 0), initial=0), np.max(np.maximum(x - ubw, 0), initial=0))
+    dual = np.abs(nlp.grad_lagrangian(x, lam_g, 1.0) + lam_x).max()
+
+    def comp(v, lam, lo, hi):
+        eq = lo == hi
+        with np.errstate(invalid='ignore'):
+            up = np.where((lam > 0) & np.isfinite(hi) & ~eq, lam * np.maximum(hi - v, 0), 0)
+            dn = np.where((lam < 0) & np.isfinite(lo) & ~eq, -lam * np.maximum(v - lo, 0), 0)
+        return max(np.max(up, initial=0), np.max(dn, initial=0))
+    compl = max(comp(g, lam_g, lbg, ubg), comp(x, lam_x, lbw, ubw))
+    return {'primal': float(primal), 'dual': float(dual), 'compl': float(compl)}

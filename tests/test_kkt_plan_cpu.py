@@ -68,3 +68,23 @@ def test_plan_racetrack_full_size_fits_device_tiles():
     assert (np.diff(plan.ent_ptr[::8]) <= 4096).all()
     chain = build_plan(ev.nw, ev.ng, var_stages(spec), ev.j_row_ptr, ev.j_col, ev.h_row_ptr, ev.h_col, 'chain')
     assert chain.n_fronts == 51 and chain.tiles == 8
+
+
+@pytest.mark.parametrize('cfg', [dict(track='race', frame='global', N=7, K=2),
+                                 dict(track='fig8', frame='global', N=8, K=3, use_quat=False),
+                                 dict(track='race', N=5, K=3)], ids=['race-global', 'fig8-global-ypr', 'race'])
+def test_equality_rows_with_zero_diagonal_are_not_singular(cfg):
+    ''' delta_c = 0 (IPOPT's first try): equality rows carry dr = 0. With W = diag(dx) > 0 and J of
+    full row rank, K has inertia (n, m, 0); rows whose entries all sit on separator anchors (global
+    gate rows on Z[n,0][:3]) must not be eliminated inside a leaf, where they would be zero pivots '''
+    spec = product_spec(**cfg)
+    ev, _, jv, dx, _ = random_kkt_values(spec, 3)
+    H = np.zeros(len(ev.h_col))
+    dr = np.where(ev.lbg == ev.ubg, 0.0, -1e-2)
+    plan = build_plan(ev.nw, ev.ng, var_stages(spec), ev.j_row_ptr, ev.j_col, ev.h_row_ptr, ev.h_col)
+    f = Factor(plan, H, jv, dx, dr)
+    assert f.inertia == (ev.nw, ev.ng, 0)
+    K = dense_kkt(plan, H, jv, dx, dr, ev.h_row_ptr, ev.h_col, ev.j_row_ptr, ev.j_col)
+    rhs = np.random.default_rng(2).standard_normal(plan.dim)
+    x = f.solve(rhs)
+    assert np.abs(K @ x - rhs).max() <= 1e-8 * max(1.0, np.abs(K).max())
