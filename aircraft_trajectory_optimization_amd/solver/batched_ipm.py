@@ -537,11 +537,15 @@ class BatchedInteriorPoint:
 
     # ------------------------------------------------------------------ solve
     def solve(self, X0, mu0: Optional[torch.Tensor] = None, active: Optional[torch.Tensor] = None,
-              stop_check=None, allow_restoration: bool = True, progress: int = 0) -> BatchedIPMResult:
+              stop_check=None, allow_restoration: bool = True, progress: int = 0,
+              on_iteration=None) -> BatchedIPMResult:
         '''
         X0 [n, B] (or [B, n]). active: instances to iterate (default all); mu0: initial barrier
         per instance; stop_check(x) -> [B] bool ends an instance with status 'stopped' (the
-        restoration phase's return test).
+        restoration phase's return test). on_iteration(it, n_step): called once per lockstep
+        iteration with the number of instances taking a step in it (host value already fetched
+        by the iteration's own synchronisation), and once more as on_iteration(it, -1) when the
+        loop ends (benchmark windows).
         '''
         o = self.o
         self._progress = progress
@@ -706,9 +710,12 @@ class BatchedInteriorPoint:
             mx = act & (own >= o.max_iter)
             status = torch.where(mx, torch.full_like(status, MAX_ITER), status)
             act = act & ~mx
-            any_act, any_wait = torch.stack([act.any(), waiting.any()]).tolist()     # one synchronisation
+            n_step, n_wt = torch.stack([act.sum(), waiting.sum()]).tolist()     # one synchronisation
+            any_act, any_wait = n_step > 0, n_wt > 0
             if not any_act and not any_wait and not inflight:
                 break
+            if on_iteration is not None:
+                on_iteration(it, int(n_step))
             laps.lap('check')
             stepping = act.clone()
             resto = torch.zeros(B, dtype=torch.bool, device=dev)
@@ -930,6 +937,8 @@ class BatchedInteriorPoint:
                     act = act | okr
                 laps.lap('resto_post')
 
+        if on_iteration is not None:
+            on_iteration(it, -1)
         for j in inflight:                           # (the lockstep bound ended the loop first)
             R, xr, okr = self._resto_collect(j, cols, x, B0)
             # the phase finished after the last lockstep iteration: restored columns keep their

@@ -1,18 +1,29 @@
 #!/usr/bin/env python
 '''
-Benchmark of the hot path: batched evaluation of the collocation NLP's g(w), dg/dw (all
-structural entries), f(w) and grad f(w) -- what IPOPT asks CasADi for on every iterate of
-the reference (base_raceline.py:165, :182-189).
+Benchmark of BASELINE.json's metric: "SQP iters/sec (batched) + lap-time err vs CasADi, 50x4
+collocation" -- the batched interior-point (SQP-type) solve of the racetrack 50 x 4 drone NLP
+whose every iteration evaluates g(w), dg/dw, f, grad f and the Hessian on the GPU (the hot path:
+what IPOPT asks CasADi for on every iterate of the reference, base_raceline.py:165, :182-189),
+factorises and solves the KKT systems on the GPU, and runs the line search.
 
-Workload (BASELINE.json configs[2]): racetrack of scripts/race.py, parametric frame,
-quaternion drone (13 states, 4 inputs), global attitude, square gates, closed loop,
-N = 50 intervals, K = 4 Legendre collocation, fp64, B = 512 seeded instances per GPU
-(SURVEY 8(d) config 3 generator). One step = one ato_eval over the whole batch, inputs
-resident in HBM. Multi-GPU: one process per GPU, instances sharded (weak scaling), no
-collective inside the timed region; per-instance summaries are all-gathered over RCCL
-afterwards.
+Workload (BASELINE.json configs[2]): racetrack of scripts/race.py,
+parametric frame, quaternion drone (13 states, 4 inputs), global attitude, square gates, closed
+loop, N = 50, K = 4 Legendre collocation, fp64, B = 512 seeded COLD starts per GPU
+(raceline/instances.py), IPOPT's max_iter = 1000 (base_raceline.py:54).
 
-    python bench.py [--gpus N --steps K --warmup W --batch B]
+One step = one lockstep iteration of the batched solver over its batch. The solve starts from the
+cold starts; lockstep iterations [W, W + K) are timed (device synchronised at both ends; the
+first W are the warmup); value = instance-iterations in the window of all ranks / slowest rank's
+window time. The solve then runs to completion (every instance optimal / acceptable / max_iter /
+failed), and the full solve is reported beside it (sqp_full: it/s over the whole solve,
+converged solves/s, statuses, lap times, KKT errors). Multi-GPU: one process per GPU, instances
+sharded (weak scaling), no communication while solving; per-instance 32-byte records
+{lap, KKT error, iterations, status} are all-gathered over RCCL afterwards.
+
+Also measured: the evaluation kernel alone (ato_eval over the same batch, `evals`, with the
+k_eval HBM roofline from >= 10 sampled launches) and the CPU baselines (rank 0, N = 1).
+
+    python bench.py [--gpus N --steps K --warmup W --batch B --max-iter 1000]
 '''
 import argparse
 import json
@@ -27,92 +38,154 @@ sys.path.insert(0, ROOT)
 
 METRIC = 'SQP iters/sec (batched) + lap-time err vs CasADi, 50×4 collocation'
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
-TIMING_STRIDE = 10         # kernel-timing events on every 10th timed step
+SPEC_KW = dict(track='race', model='drone', frame='parametric', N=50, K=4, use_quat=True, global_r=True)
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=50)
-    ap.add_argument('--warmup', type=int, default=10)
+    ap.add_argument('--steps', type=int, default=200, help='timed lockstep SQP iterations')
+    ap.add_argument('--warmup', type=int, default=10, help='untimed lockstep iterations before the window')
     ap.add_argument('--batch', type=int, default=512, help='instances per GPU')
-    ap.add_argument('--dtype', choices=['f64', 'f32'], default='f64')
+    ap.add_argument('--max-iter', type=int, default=1000, help="IPOPT's max_iter (base_raceline.py:54)")
+    ap.add_argument('--eval-steps', type=int, default=50)
+    ap.add_argument('--eval-warmup', type=int, default=10)
+    ap.add_argument('--dtype', choices=['f64', 'f32'], default='f64', help='evaluation-kernel bench dtype')
     ap.add_argument('--layout', choices=['interleaved', 'instance'], default='interleaved')
-    ap.add_argument('--cpu-seconds', type=float, default=15.0, help='budget of the oracle CPU baseline')
+    ap.add_argument('--cpu-seconds', type=float, default=15.0, help='budget of the CPU baselines')
     ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--no-solve', action='store_true', help='skip the interior-point solves (batched and single)')
-    ap.add_argument('--solve-batch', type=int, default=512, help='instances of the batched interior-point solve')
-    ap.add_argument('--solve-max-iter', type=int, default=200)
+    ap.add_argument('--no-solve', action='store_true', help='evaluation kernel only')
+    ap.add_argument('--no-single', action='store_true', help='skip the B = 1 re-solve of instance 0')
     ap.add_argument('--traffic-json', default=os.path.join(ROOT, 'profiles', 'traffic_latest.json'))
     return ap.parse_args()
 
 
-def cpu_baseline(spec_kwargs, W, budget_s):
+def eval_bench(spec, W, args, dev, world):
     '''
-    SURVEY 8(d): the build's C++ CPU twin of ato_eval -- the same segment programs compiled with
-    g++ -O3 (tests/native/hostcheck.cpp, OpenMP over instances) -- timed on the host cores of the
-    same box on the same instances: one thread and all threads of this process' share
-    (OMP_NUM_THREADS). The numpy restatement (oracle, complex-step Jacobian) is reported beside it.
+    ato_eval over the batch (inputs resident in HBM): evals/s and the k_eval roofline. Kernel
+    durations come from HIP events recorded inside the library on the evaluation stream, on
+    every stride-th step so that >= 10 launches are sampled (each recorded step adds ~10 us of
+    event gaps, tools/diag/step_gaps.py, which the other steps do not pay).
+    '''
+    import torch
+    import torch.distributed as dist
+    from aircraft_trajectory_optimization_amd import native
+    from aircraft_trajectory_optimization_amd.raceline.batched import BatchedNLP
+    from aircraft_trajectory_optimization_amd.raceline.shard import max_over_ranks
+    B = W.shape[0]
+    dtype = torch.float64 if args.dtype == 'f64' else torch.float32
+    layout = native.ATO_LAYOUT_INTERLEAVED if args.layout == 'interleaved' else native.ATO_LAYOUT_INSTANCE_MAJOR
+    bn = BatchedNLP(spec, B, dtype=dtype, layout=layout, device=dev)
+    bn.set_w(W)
+    nw, ng, nnz = bn.sizes
+    for _ in range(args.eval_warmup):
+        bn.evaluate()
+    stride = max(1, args.eval_steps // 10)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    bn.problem.timing_stride(stride)
+    bn.problem.timing_start((args.eval_steps + stride - 1) // stride)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.eval_steps):
+        bn.evaluate()
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    elapsed = max_over_ranks(t1 - t0, dev)
+    k_ms, r_ms, calls = bn.problem.timing_read()
+    bn.problem.timing_start(0)
+    bn.problem.timing_stride(1)
+    g, _, f, _ = bn.results()
+    assert np.isfinite(g).all() and np.isfinite(f).all(), 'non-finite evaluation results'
+    elem = 8 if args.dtype == 'f64' else 4
+    bytes_per_eval = elem * (nw + ng + nnz + nw + 1)   # read w; write g, J, grad f, f
+    kernel_s = (k_ms / max(calls, 1)) / 1e3
+    achieved = B * bytes_per_eval / kernel_s / 1e9
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            tj = json.load(open(args.traffic_json, encoding='utf-8'))
+            if tj.get('batch') == B and tj.get('dtype') == args.dtype and tj.get('layout') == args.layout:
+                traffic = tj.get('hbm_bytes_per_launch')
+        except (OSError, ValueError):
+            traffic = None
+    evals = {'value': world * B * args.eval_steps / elapsed, 'unit': 'constraint+Jacobian evals/s (g, dg/dw, f, '
+             'grad f per instance, all GPUs)', 'steps': args.eval_steps, 'warmup': args.eval_warmup,
+             'ms_per_step': elapsed / args.eval_steps * 1e3, 'dtype': args.dtype, 'layout': args.layout,
+             'nw': nw, 'ng': ng, 'nnz': nnz}
+    roofline = {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic, 'kernel': 'k_eval',
+                'kernel_avg_us': kernel_s * 1e6, 'reduce_avg_us': r_ms / max(calls, 1) * 1e3,
+                'timed_launches': calls, 'timing_stride': stride,
+                'algorithmic_bytes_per_launch': B * bytes_per_eval,
+                'note': 'the evaluation kernel of every SQP iteration, timed on its own (evals)'}
+    return evals, roofline
+
+
+def cpu_baseline(W, budget_s):
+    '''
+    Rank 0, N = 1, on the GPU box's host cores:
+      * value: the single-instance interior-point solve on the CPU -- the same algorithm
+        (solver/ipm.py) with every evaluation by the C++ CPU twin of the programs
+        (tests/native/hostcheck.cpp, g++ -O3, 1 thread) and the host block LDL^T KKT -- on
+        instance 0 of the same cold starts, capped so it runs about budget_s / 2: SQP it/s;
+      * the C++ twin's evaluation rate (g, dg/dw, f, grad f) on 1 thread and on all threads,
+        and the numpy oracle's (complex-step Jacobian), as sub-keys.
     The reference's CasADi/IPOPT path cannot run anywhere in this pipeline.
     '''
-    from tests.helpers import HostCheck, oracle_nlp
+    from aircraft_trajectory_optimization_amd.solver.ipm import InteriorPointSolver, IPMOptions
     from aircraft_trajectory_optimization_amd.tracks import make_spec
-    hc = HostCheck(make_spec(**spec_kwargs).native_spec())
+    from tests.helpers import HostCheck, HostEvaluator, oracle_nlp
+    spec = make_spec(**SPEC_KW)
+    ev = HostEvaluator(spec)
+    # calibrate the iteration cap on a short solve, then time the capped solve
+    t0 = time.perf_counter()
+    InteriorPointSolver(ev, spec.lbw, spec.ubw, ev.lbg, ev.ubg, IPMOptions(max_iter=3)).solve(W[0])
+    per_it = (time.perf_counter() - t0) / 3
+    cap = int(max(5, min(1000, budget_s / 2 / max(per_it, 1e-3))))
+    t0 = time.perf_counter()
+    r = InteriorPointSolver(ev, spec.lbw, spec.ubw, ev.lbg, ev.ubg, IPMOptions(max_iter=cap)).solve(W[0])
+    t_solve = time.perf_counter() - t0
+    hc = HostCheck(spec.native_spec())
     threads = max(1, int(os.environ.get('OMP_NUM_THREADS', os.cpu_count() or 1)))
 
     def rate(nthreads, budget):
         out = None
-        n, t0 = 0, time.perf_counter()
-        while time.perf_counter() - t0 < budget:
+        n, t0_ = 0, time.perf_counter()
+        while time.perf_counter() - t0_ < budget:
             out = hc.eval_threads(W, nthreads, out)
             n += W.shape[0]
-        return n / (time.perf_counter() - t0), n
+        return n / (time.perf_counter() - t0_), n
 
-    r1, n1 = rate(1, budget_s / 3)
-    rT, nT = rate(threads, budget_s / 3)
-    nlp = oracle_nlp(**spec_kwargs)
-    t0, k = time.perf_counter(), 0
-    while k < 3:
-        w = W[k]
-        nlp.g(w)
-        nlp.jac_dense(w)
-        nlp.f(w)
-        nlp.grad_f(w)
-        k += 1
-    r_np = k / (time.perf_counter() - t0)
-    return {'value': rT, 'unit': 'evals/s', 'cores': threads, 'kind': 'port',
-            'single_thread_value': r1, 'numpy_oracle_value': r_np,
-            'sample': f'C++ twin of ato_eval (g++ -O3 -march=x86-64-v3, OpenMP): {nT} evaluations on '
-                      f'{threads} threads and {n1} on 1 thread of the same {W.shape[0]} seeded 50x4x13 '
-                      f'racetrack instances (g, dg/dw, f, grad f), about {budget_s / 3:.0f} s each; numpy oracle '
-                      f'(complex-step dense J) {k} instances'}
-
-
-def batched_solve(B, max_iter):
-    '''
-    The SQP (interior-point) iteration itself, batched: BASELINE config 3 shape (racetrack 50 x 4
-    drone, B instances on one GPU, fp64). Instance 0 is race.py's use_ws start (point-mass warm
-    start); the others are seeded perturbations of it (raceline/batch_instances.py). Every
-    evaluation, Hessian, KKT factorisation (ato_kkt_factor) and solve runs on the device; the
-    lockstep iteration logic is torch on the device. Instance 0 is also solved by the
-    single-instance host-KKT solver: lap_time_err_instance0_vs_host_s compares the two (the
-    CasADi/IPOPT lap time itself is unpinned: IPOPT is not reachable here).
-    '''
-    from tools.solve_batched import run
-    out = run(B, max_iter, host_ref=True)
-    out['lap_time_vs_casadi'] = 'unpinned (no IPOPT reachable here); vs the single-instance solver: see ' \
-                                'lap_time_err_instance0_vs_host_s'
-    return out
+    r1, n1 = rate(1, budget_s / 4)
+    rT, nT = rate(threads, budget_s / 4)
+    nlp = oracle_nlp(**{k: v for k, v in SPEC_KW.items()})
+    t0 = time.perf_counter()
+    for k in range(2):
+        nlp.g(W[k])
+        nlp.jac_dense(W[k])
+    r_np = 2 / (time.perf_counter() - t0)
+    return {'value': r.iters / t_solve, 'unit': 'SQP iterations/s (one instance)', 'cores': 1, 'kind': 'port',
+            'sample': f'instance 0 of the config-3 cold starts, the interior-point solver (solver/ipm.py) with the '
+                      f'C++ CPU twin of the programs (1 thread) and the host block LDL^T KKT: {r.iters} iterations '
+                      f'(cap {cap}) in {t_solve:.1f} s; twin evaluations: {nT} on {threads} threads, {n1} on 1 '
+                      f'thread; numpy oracle 2 instances',
+            'evals_per_s_1_thread': r1, 'evals_per_s_all_threads': rT, 'eval_threads': threads,
+            'numpy_oracle_evals_per_s': r_np}
 
 
 def main():
     args = parse()
     import torch
     import torch.distributed as dist
-    from aircraft_trajectory_optimization_amd import native
-    from aircraft_trajectory_optimization_amd.raceline.batched import BatchedNLP
+    from aircraft_trajectory_optimization_amd.raceline.batched_solve import gather_solve_records, solve_records, \
+        solve_shard, summarize_records, window_timer, RECORD_BYTES
     from aircraft_trajectory_optimization_amd.raceline.instances import seeded_instances
-    from aircraft_trajectory_optimization_amd.raceline.shard import gather_records, max_over_ranks, shard_seeds
+    from aircraft_trajectory_optimization_amd.raceline.shard import max_over_ranks, shard_seeds
+    from aircraft_trajectory_optimization_amd.solver.ipm import IPMOptions
     from aircraft_trajectory_optimization_amd.tracks import make_spec
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -123,89 +196,98 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
 
-    spec_kwargs = dict(track='race', model='drone', frame='parametric', N=50, K=4, use_quat=True, global_r=True)
-    spec = make_spec(**spec_kwargs)
+    spec = make_spec(**SPEC_KW)
     B = args.batch
-    W, _, _ = seeded_instances(spec, shard_seeds(rank, world, B))
-    dtype = torch.float64 if args.dtype == 'f64' else torch.float32
-    layout = native.ATO_LAYOUT_INTERLEAVED if args.layout == 'interleaved' else native.ATO_LAYOUT_INSTANCE_MAJOR
-    bn = BatchedNLP(spec, B, dtype=dtype, layout=layout, device=dev)
-    bn.set_w(W)
-    nw, ng, nnz = bn.sizes
+    seeds = shard_seeds(rank, world, B)
+    W, _, _ = seeded_instances(spec, seeds)
 
-    for _ in range(args.warmup):
-        bn.evaluate()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    # kernel durations from HIP events on the evaluation stream, recorded on every TIMING_STRIDE-th
-    # step of the timed loop: each recorded step adds three event packets (about 10 us of gaps at
-    # B = 512, tools/diag/step_gaps.py), which would otherwise be part of every measured step
-    bn.problem.timing_stride(TIMING_STRIDE)
-    bn.problem.timing_start((args.steps + TIMING_STRIDE - 1) // TIMING_STRIDE)
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        bn.evaluate()
-    torch.cuda.synchronize(dev)
-    t1 = time.perf_counter()
-    if world > 1:
-        dist.barrier()
-    elapsed = max_over_ranks(t1 - t0, dev)
-    k_ms, r_ms, calls = bn.problem.timing_read()
-    bn.problem.timing_start(0)
-    bn.problem.timing_stride(1)
+    # ---- 1. the evaluation kernel alone (k_eval roofline)
+    evals, roofline = eval_bench(spec, W, args, dev, world)
 
-    # per-instance summary {lap-time guess sum(h), cost f, max equality residual}, all-gathered (RCCL)
-    g, _, f, _ = bn.results()
-    eq = bn.lbg == bn.ubg
-    summary = np.stack([W[:, :spec.N].sum(axis=1), f, np.abs(g[:, eq]).max(axis=1)], axis=1)
-    gathered = gather_records(torch.as_tensor(summary, device=dev))
-    assert bool(torch.isfinite(gathered).all()), 'non-finite evaluation results'
-
+    out = None
+    if not args.no_solve:
+        # ---- 2. the batched SQP solve: lockstep iterations [W, W + K) timed, then to completion
+        sync = lambda: torch.cuda.synchronize(dev)  # noqa: E731
+        hook, win = window_timer(args.warmup, args.steps, sync)
+        sync()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        res, solver, _ = solve_shard(spec, seeds, IPMOptions(max_iter=args.max_iter), on_iteration=hook)
+        sync()
+        t_solve = time.perf_counter() - t0
+        if win['t0'] is None or win['t1'] is None:
+            raise RuntimeError('the solve ended before the timed window began')
+        window_s = max_over_ranks(win['t1'] - win['t0'], dev)
+        counts = torch.tensor([float(win['count']), float(win['timed'])], dtype=torch.float64, device=dev)
+        timed_min = torch.tensor([float(win['timed'])], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(counts, op=dist.ReduceOp.SUM)
+            dist.all_reduce(timed_min, op=dist.ReduceOp.MIN)
+        solve_s = max_over_ranks(t_solve, dev)
+        rec = solve_records(spec, res, solver)
+        allrec = gather_solve_records(rec)            # RCCL all-gather of the 32-byte records
+        lockstep = int(len(solver.history))
+        if rank == 0:
+            summ = summarize_records(allrec)
+            steps_timed = int(timed_min.item())
+            value = float(counts[0].item()) / window_s
+            sqp_full = {'solve_s': solve_s, 'lockstep_iterations': lockstep,
+                        'iterations_per_s': summ['instance_iterations'] / solve_s,
+                        'converged_solves_per_s': summ['converged'] / solve_s, 'max_iter': args.max_iter,
+                        'records_all_gathered': {'bytes_per_instance': RECORD_BYTES, 'instances': len(allrec),
+                                                 'collective': 'all_gather' + (' (RCCL)' if world > 1 else ' (1 rank)')},
+                        **summ, 'solver_stats': {k: v for k, v in res.stats.items() if k not in ('resto_phases',)}}
+            lap_err = None
+            if not args.no_single:
+                # instance 0 re-solved alone (B = 1) from the same start: batched vs single-instance
+                from aircraft_trajectory_optimization_amd.raceline.batched_solve import solve_shard as one
+                r1, s1, _ = one(spec, [seeds[0]], IPMOptions(max_iter=args.max_iter))
+                lap1 = float(r1.x[:spec.N].sum())
+                lap_err = abs(float(allrec[0, 0]) - lap1)
+                sqp_full['instance0'] = {'batched_lap_s': float(allrec[0, 0]), 'single_lap_s': lap1,
+                                         'batched_status': res.status[0], 'single_status': r1.status[0],
+                                         'batched_iters': int(res.iters[0]), 'single_iters': int(r1.iters[0])}
+            out = {
+                'metric': METRIC,
+                'value': value,
+                'unit': 'SQP iterations/s (instance-iterations of the batched interior-point solve, all GPUs)',
+                'n_gpus': world,
+                'steps': steps_timed,
+                'warmup': args.warmup,
+                'ms_per_step': window_s / max(steps_timed, 1) * 1e3,
+                'higher_is_better': True,
+                'scaling': 'weak',
+                'vs_baseline': None,
+                'dtype': 'f64',
+                'data': 'synthetic: seeded cold-start instances (SURVEY 8(d) config 3 generator, raceline/instances.py)',
+                'config': {'workload': 'racetrack_parametric_esp_drone_colloc_N50_K4_cold_start_batched_sqp',
+                           'N': 50, 'K': 4, 'nz': 13, 'nu': 4, 'batch_per_gpu': B, 'global_batch': world * B,
+                           'max_iter': args.max_iter, 'layout': args.layout,
+                           'parallelism': f'instances sharded x{world}, records all-gathered'},
+                'lap_time_err_vs_casadi': None,
+                'lap_time_err_note': 'CasADi/IPOPT cannot run in this pipeline (SURVEY F8): lap-time parity with it '
+                                     'is unpinned; the transcription is pinned to the reference\'s own code '
+                                     '(tests/golden), solutions by oracle KKT + second-order certificates; '
+                                     'lap_time_err_batched_vs_single_s compares instance 0 batched vs alone',
+                'lap_time_err_batched_vs_single_s': lap_err,
+                'roofline': roofline,
+                'cpu_baseline': None,
+                'evals': evals,
+                'sqp_full': sqp_full,
+            }
+            if world == 1 and not args.no_cpu_baseline:
+                out['cpu_baseline'] = cpu_baseline(W, args.cpu_seconds)
+    elif rank == 0:
+        out = {'metric': METRIC, 'value': evals['value'], 'unit': evals['unit'], 'n_gpus': world,
+               'steps': args.eval_steps, 'warmup': args.eval_warmup, 'ms_per_step': evals['ms_per_step'],
+               'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': args.dtype,
+               'data': 'synthetic: seeded cold-start instances (evaluation kernel only, --no-solve)',
+               'config': {'workload': 'racetrack_parametric_esp_drone_colloc_N50_K4_eval', 'batch_per_gpu': B,
+                          'global_batch': world * B, 'layout': args.layout},
+               'roofline': roofline, 'cpu_baseline': None, 'evals': evals}
     if rank == 0:
-        elem = 8 if args.dtype == 'f64' else 4
-        bytes_per_eval = elem * (nw + ng + nnz + nw + 1)   # read w; write g, J, grad f, f
-        kernel_s = (k_ms / max(calls, 1)) / 1e3
-        achieved = B * bytes_per_eval / kernel_s / 1e9
-        traffic = None
-        if os.path.exists(args.traffic_json):
-            try:
-                tj = json.load(open(args.traffic_json, encoding='utf-8'))
-                if tj.get('batch') == B and tj.get('dtype') == args.dtype and tj.get('layout') == args.layout:
-                    traffic = tj.get('hbm_bytes_per_launch')
-            except (OSError, ValueError):
-                traffic = None
-        value = world * B * args.steps / elapsed
-        out = {
-            'metric': METRIC,
-            'value': value,
-            'unit': 'constraint+Jacobian evals/s (g, dg/dw, f, grad f per instance)',
-            'n_gpus': world,
-            'steps': args.steps,
-            'warmup': args.warmup,
-            'ms_per_step': elapsed / args.steps * 1e3,
-            'higher_is_better': True,
-            'scaling': 'weak',
-            'vs_baseline': None,
-            'dtype': args.dtype,
-            'data': 'synthetic: seeded cold-start instances (SURVEY 8(d) config 3 generator)',
-            'config': {'workload': 'racetrack_parametric_esp_drone_colloc_N50_K4', 'N': 50, 'K': 4, 'nz': 13,
-                       'nu': 4, 'batch_per_gpu': B, 'global_batch': world * B, 'layout': args.layout,
-                       'nw': nw, 'ng': ng, 'nnz': nnz, 'parallelism': f'instances sharded x{world}'},
-            'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                         'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
-                         'kernel': 'k_eval', 'kernel_avg_us': kernel_s * 1e6,
-                         'reduce_avg_us': r_ms / max(calls, 1) * 1e3,
-                         'timed_launches': calls, 'timing_stride': TIMING_STRIDE,
-                         'algorithmic_bytes_per_launch': B * bytes_per_eval},
-            'cpu_baseline': None,
-        }
-        if world == 1 and not args.no_cpu_baseline:
-            out['cpu_baseline'] = cpu_baseline(spec_kwargs, W, args.cpu_seconds)
-        if world == 1 and not args.no_solve:
-            out['sqp'] = batched_solve(args.solve_batch, args.solve_max_iter)
-        print(json.dumps(out))
+        print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

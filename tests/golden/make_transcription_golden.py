@@ -353,6 +353,32 @@ def make_cpc():
     print('cpc: done', flush=True)
 
 
+def make_tube(N=12, K=2, collision_r=0.4):
+    ''' the reference's obstacle-free tube search (MeshObstacle.compute_plannning_tube /
+    search_largest_sphere, mesh_obstacle.py:50-76, :110-145) on the arena mesh, over the node s of
+    the obstacles track. trimesh's signed_distance is replaced by the oracle's restatement
+    (oracle/ref_mesh.py; trimesh is not installed); closest_point only feeds the rendered tangent
+    points, which are not recorded. '''
+    from drone3d.obstacles import mesh_obstacle as mo        # the reference's (first on sys.path)
+    sys.path.append(os.path.dirname(os.path.dirname(HERE)))   # the repo LAST: only for oracle/
+    from oracle.ref_mesh import signed_distance as oracle_sd
+    assert mo.__file__.startswith(REFERENCE), mo.__file__
+    mesh = np.load(os.path.join(os.path.dirname(os.path.dirname(HERE)), 'aircraft_trajectory_optimization_amd',
+                                'assets', 'arena_track_obstacles_multistory.npz'))
+    V, F = mesh['vertices'].astype(float), mesh['faces'].astype(np.int64)
+    mo.signed_distance = lambda _mesh, x: -oracle_sd(np.asarray(x, float), V, F)   # trimesh sign: + inside
+    mo.closest_point = lambda _mesh, x: (np.zeros_like(np.asarray(x, float)), None, None)
+    env = mo.MeshObstacle.__new__(mo.MeshObstacle)
+    env.mesh, env.filename, env.color = None, 'arena', [1, 0, 0, 1]
+    line = _ref_line('obstacles', True)
+    s = np.array([line.s_min() + (line.s_max() - line.s_min()) / N * (n + t)
+                  for n in range(N) for t in np.append(0, __import__('casadi').collocation_points(K))])
+    tube = env.compute_plannning_tube(line, s, collision_r)
+    np.savez_compressed(os.path.join(HERE, 'tube.npz'), s=s, collision_r=np.array(collision_r),
+                        ball_center=tube.ball_center, ball_r=tube.ball_r, ball_p=tube.ball_p)
+    print(f'tube: {len(s)} nodes', flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--only', default=None)
@@ -363,6 +389,8 @@ def main():
         make_models()
     if a.only in (None, 'cpc'):
         make_cpc()
+    if a.only in (None, 'tube'):
+        make_tube()
     for i, (name, cfg) in enumerate(CASES.items()):
         if a.only and a.only != name:
             continue

@@ -1,7 +1,11 @@
 '''
 The N > 1 path of bench.py on CPU: two gloo ranks shard seeded instances, each computes a
 per-instance record (here with the oracle, since there is no GPU), the max-over-ranks time
-and the rank-major all-gather must reproduce a single-process run over all seeds.
+and the rank-major all-gather must reproduce a single-process run over all seeds. The sharded
+batched SOLVE (raceline/batched_solve.py) runs the same way on the CPU stand-ins of the device
+pieces (tests/batched_backends.py): each rank solves its cold-start shard, the 32-byte records
+{lap, KKT error, iterations, status} are all-gathered, and they equal one process solving all
+seeds as one batch.
 '''
 import os
 import socket
@@ -64,3 +68,46 @@ def test_two_rank_gather_matches_single_process():
     gathered = res[:-1].reshape(world * PER_RANK, 3)
     np.testing.assert_array_equal(gathered, _records(range(world * PER_RANK)))
     assert slowest == 2.0
+
+
+SOLVE_CFG = dict(track='race', model='point', frame='parametric', N=6, K=2, use_quat=False, global_r=True)
+SOLVE_PER_RANK = 2
+
+
+def _solve_records(seeds):
+    from aircraft_trajectory_optimization_amd.raceline.batched_solve import solve_records, solve_shard
+    from aircraft_trajectory_optimization_amd.solver.ipm import IPMOptions
+    from tests.batched_backends import cpu_solver_factory
+    spec = make_spec(**SOLVE_CFG)
+    res, solver, _ = solve_shard(spec, seeds, IPMOptions(max_iter=150), solver_factory=cpu_solver_factory)
+    return solve_records(spec, res, solver)
+
+
+def _solve_worker(rank, world, port, out):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from aircraft_trajectory_optimization_amd.raceline.batched_solve import gather_solve_records
+        rec = _solve_records(shard_seeds(rank, world, SOLVE_PER_RANK))
+        gathered = gather_solve_records(rec)
+        if rank == 0:
+            np.save(out, gathered.numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_sharded_solve_gathers_single_process_records():
+    from aircraft_trajectory_optimization_amd.raceline.batched_solve import RECORD_BYTES, summarize_records
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, 'records.npy')
+        mp.spawn(_solve_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+        gathered = np.load(out)
+    single = _solve_records(range(world * SOLVE_PER_RANK)).numpy()
+    assert gathered.shape == (world * SOLVE_PER_RANK, 4) and gathered.dtype == np.float64
+    assert gathered.shape[1] * gathered.itemsize == RECORD_BYTES == 32
+    np.testing.assert_array_equal(gathered[:, 2:], single[:, 2:])          # iterations, status
+    np.testing.assert_allclose(gathered[:, :2], single[:, :2], rtol=1e-12, atol=1e-15)
+    s = summarize_records(gathered)
+    assert s['instances'] == 4 and s['converged'] == 4, s

@@ -262,3 +262,27 @@ def test_timing_stride_samples_every_nth_evaluation():
     bn.problem.timing_start(0)
     bn.problem.timing_stride(1)
     assert calls == 3 and k_ms > 0.0 and r_ms >= 0.0
+
+
+@pytest.mark.parametrize('cfg', [c for c in HESS_CASES if c.get('N', 0) < 50], ids=_id)
+def test_hessian_matches_oracle_hvp(cfg):
+    ''' the device Hessian of the Lagrangian against the ORACLE: H v for random directions v equals
+    the central difference of the oracle's exact (complex-step) Lagrangian gradient, whose
+    truncation error is O(eps^2) (tolerance 1e-6 of the scale at eps = 1e-5, as on the CPU) '''
+    from tests.helpers import sym_dense
+    rng = np.random.default_rng(29)
+    spec = product_spec(**cfg)
+    nlp = oracle_nlp(**cfg)
+    B = 2
+    W = np.stack([random_w(nlp, rng) for _ in range(B)])
+    LAM = rng.standard_normal((B, nlp.ng))
+    sig = rng.uniform(0.5, 1.5, B)
+    bn = _batched(spec, B)
+    bn.set_w(W)
+    H = bn.hessian(torch.as_tensor(LAM.T.copy(), device=bn.device), torch.as_tensor(sig, device=bn.device))
+    Hd = H.cpu().numpy().T
+    for b in range(B):
+        V = rng.standard_normal((nlp.nw, 3))
+        Hv = sym_dense(np.asarray(bn.hess_row_ptr), np.asarray(bn.hess_col), Hd[b], nlp.nw) @ V
+        ref = nlp.hvp(W[b], LAM[b], sig[b], V, eps=1e-5)
+        _close(Hv, ref, 1e-6)

@@ -1,0 +1,14 @@
+#!/bin/bash
+# r03 GPU session: all GPU tests, the default bench (batched SQP + eval roofline), rocprof of the eval
+set -u
+cd "${GRAFT_REPO_ROOT}"
+OUT=gpurun_out/r03b
+mkdir -p $OUT
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $OUT/pytest_gpu.log 2>&1 || { echo "tests rc=$?"; tail -30 $OUT/pytest_gpu.log; exit 1; }
+tail -3 $OUT/pytest_gpu.log
+timeout -k 10 600 python -u bench.py > $OUT/bench.log 2> $OUT/bench.err || { echo "bench rc=$?"; tail -20 $OUT/bench.err; exit 1; }
+tail -c 3000 $OUT/bench.log
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python bench.py --no-solve --no-cpu-baseline > $OUT/prof.log 2>&1 || { echo "prof rc=$?"; exit 1; }
+find $OUT -name '*_trace.csv' -delete
+echo done

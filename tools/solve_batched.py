@@ -50,7 +50,7 @@ def run(B, max_iter, N=50, K=4, track='race', host_ref=True, cold=False):
     out = {'workload': f'{track}_parametric_esp_drone_colloc_N{N}_K{K} batched solve (point-mass warm start, '
                        f'instance 0 unperturbed, others seeded perturbations)',
            'batch': B, 'solve_s': t_solve, 'setup_s': t_setup,
-           'instance_iterations': int(res.iters.sum()), 'lockstep_iterations': int(res.iters.max()),
+           'instance_iterations': int(res.iters.sum()), 'lockstep_iterations': int(len(solver.history)),
            'iterations_per_s': float(res.iters.sum() / t_solve),
            'converged': int(ok.sum()), 'statuses': {s: res.status.count(s) for s in set(res.status)},
            'lap_time_instance0_s': float(laps[0]),
