@@ -16,6 +16,7 @@
 #pragma once
 #include <vector>
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include "ato_layout.hpp"
 #include "ato_hessian.hpp"
 
@@ -323,24 +324,27 @@ hipError_t launch_eval(const ProbD& p, int B, int layout, const T* w, T* g, T* J
     // B = 512, and nothing at B = 4096; compile-time K everywhere -- the hoisted loads cut
     // occupancy to one wave per SIMD.)
     const bool paired = layout == ATO_LAYOUT_INTERLEAVED && (B % WAVE) == 0 && wg;
-    if (ev) (void)hipEventRecord(ev[0], st);
+    // timing (ev != nullptr): the evaluation kernel is launched with start / stop events that the
+    // runtime stamps at the kernel's own start and end (hipExtLaunchKernel), i.e. its execution
+    // time as a kernel trace reports it, without the dispatch gaps of separately recorded events
+    hipEvent_t e0 = ev ? ev[0] : nullptr, e1 = ev ? ev[1] : nullptr;
     // Collocation and RK4 problems get separate instantiations so neither pays the other's
     // register allocation (the RK4 dual-number step vs the collocation ODE units).
     auto launch = [&]<int UM>() {
         const dim3 grid(chunks, p.n_units);
         if (paired) {
             if (wj && wg && wf)
-                hipLaunchKernelGGL((k_eval_paired<M, T, 0, true, true, true, true, UM>), grid, block, 0, st, p, B, 0, w, g, J, gf, fpart);
+                hipExtLaunchKernelGGL((k_eval_paired<M, T, 0, true, true, true, true, UM>), grid, block, 0, st, e0, e1, 0, p, B, 0, w, g, J, gf, fpart);
             else if (wj && wg)
-                hipLaunchKernelGGL((k_eval_paired<M, T, 0, true, true, false, true, UM>), grid, block, 0, st, p, B, 0, w, g, J, gf, fpart);
+                hipExtLaunchKernelGGL((k_eval_paired<M, T, 0, true, true, false, true, UM>), grid, block, 0, st, e0, e1, 0, p, B, 0, w, g, J, gf, fpart);
             else if (wg && wf)
-                hipLaunchKernelGGL((k_eval_paired<M, T, 0, false, true, true, true, UM>), grid, block, 0, st, p, B, 0, w, g, J, gf, fpart);
+                hipExtLaunchKernelGGL((k_eval_paired<M, T, 0, false, true, true, true, UM>), grid, block, 0, st, e0, e1, 0, p, B, 0, w, g, J, gf, fpart);
             else
-                hipLaunchKernelGGL((k_eval_paired<M, T, 0, false, true, false, true, UM>), grid, block, 0, st, p, B, 0, w, g, J, gf, fpart);
+                hipExtLaunchKernelGGL((k_eval_paired<M, T, 0, false, true, false, true, UM>), grid, block, 0, st, e0, e1, 0, p, B, 0, w, g, J, gf, fpart);
             return;
         }
         auto go = [&]<bool WJ, bool WG, bool WF>() {
-            hipLaunchKernelGGL((k_eval<M, T, 0, WJ, WG, WF, UM>), grid, block, 0, st, p, B, layout, w, g, J, gf, fpart);
+            hipExtLaunchKernelGGL((k_eval<M, T, 0, WJ, WG, WF, UM>), grid, block, 0, st, e0, e1, 0, p, B, layout, w, g, J, gf, fpart);
         };
         if (wj && wg && wf) go.template operator()<true, true, true>();
         else if (wj && wg) go.template operator()<true, true, false>();
@@ -354,12 +358,13 @@ hipError_t launch_eval(const ProbD& p, int B, int layout, const T* w, T* g, T* J
     else launch.template operator()<UMASK_COLLOC>();
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    if (ev) (void)hipEventRecord(ev[1], st);
     if (wf) {
-        hipLaunchKernelGGL((k_cost_reduce<T>), dim3((B + 255) / 256), dim3(256), 0, st, p.N, B, (const T*)fpart, f);
+        hipExtLaunchKernelGGL((k_cost_reduce<T>), dim3((B + 255) / 256), dim3(256), 0, st, nullptr,
+                              ev ? ev[2] : nullptr, 0, p.N, B, (const T*)fpart, f);
         e = hipGetLastError();
+    } else if (ev) {
+        (void)hipEventRecord(ev[2], st);
     }
-    if (ev) (void)hipEventRecord(ev[2], st);
     return e;
 }
 

@@ -77,24 +77,58 @@ class BatchedDeviceEvaluator:
         self.lbg, self.ubg = self.bn.lbg, self.bn.ubg
         self.var_stage = variable_stages(spec)
         self.counts = {'eval': 0, 'hess': 0}
+        self._events: Optional[list] = None
+
+    # ---- optional evaluation timing (RacelineResults.feval_time of the single-instance API solve):
+    # event pairs on the current stream around every evaluation, summed after the solve
+    def timing_on(self):
+        self._events = []
+
+    def timing_total_s(self) -> float:
+        if not self._events:
+            return 0.0
+        self._events[-1][1].synchronize()
+        return sum(a.elapsed_time(b) for a, b in self._events) / 1e3
+
+    def _tic(self):
+        if self._events is None:
+            return None
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        return e
+
+    def _toc(self, start):
+        if start is not None:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            self._events.append((start, e))
 
     def eval(self, X: torch.Tensor):
+        t = self._tic()
         self.bn.w.copy_(X)
         self.bn.evaluate()
         self.counts['eval'] += 1
-        return self.bn.f.clone(), self.bn.g.clone(), self.bn.grad_f.clone(), self.bn.jac.clone()
+        out = self.bn.f.clone(), self.bn.g.clone(), self.bn.grad_f.clone(), self.bn.jac.clone()
+        self._toc(t)
+        return out
 
     def eval_fg(self, X: torch.Tensor):
         ''' f and g only (no Jacobian written): the line search's trial points '''
+        t = self._tic()
         self.bn.w.copy_(X)
         self.bn.evaluate(jac=False)
         self.counts['eval'] += 1
-        return self.bn.f.clone(), self.bn.g.clone()
+        out = self.bn.f.clone(), self.bn.g.clone()
+        self._toc(t)
+        return out
 
     def hess(self, X: torch.Tensor, lam: torch.Tensor, sigma: torch.Tensor) -> torch.Tensor:
+        t = self._tic()
         self.bn.w.copy_(X)
         self.counts['hess'] += 1
-        return self.bn.hessian(lam.contiguous(), sigma.contiguous()).clone()
+        out = self.bn.hessian(lam.contiguous(), sigma.contiguous()).clone()
+        self._toc(t)
+        return out
 
     def subset(self, count: int) -> '_SubsetDeviceEvaluator':
         ''' an evaluator over `count` <= batch instances (its own [element][count] buffers, the same
