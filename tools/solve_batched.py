@@ -47,8 +47,9 @@ def run(B, max_iter, N=50, K=4, track='race', host_ref=True, cold=False):
     t_solve = time.perf_counter() - t0
     laps = res.x[:spec.N].sum(0).cpu().numpy()
     ok = res.success
-    out = {'workload': f'{track}_parametric_esp_drone_colloc_N{N}_K{K} batched solve (point-mass warm start, '
-                       f'instance 0 unperturbed, others seeded perturbations)',
+    start = ('config-3 seeded cold starts' if cold else
+             'point-mass warm start, instance 0 unperturbed, others seeded perturbations')
+    out = {'workload': f'{track}_parametric_esp_drone_colloc_N{N}_K{K} batched solve ({start})',
            'batch': B, 'solve_s': t_solve, 'setup_s': t_setup,
            'instance_iterations': int(res.iters.sum()), 'lockstep_iterations': int(len(solver.history)),
            'iterations_per_s': float(res.iters.sum() / t_solve),
