@@ -20,6 +20,7 @@
 #include <string>
 #include <vector>
 #include <cstring>
+#include <cstdlib>
 #include <cmath>
 #include "ato_program.hpp"
 
@@ -383,11 +384,20 @@ struct Layout {
         return "";
     }
 
-    // Work units in three classes (each a contiguous range; see ProbD::cls_off / cls_cnt):
+    // Work units in three classes:
     //   0: tail segments (equal-h rows, gates, closure), one unit each
     //   1: the ODE row groups of every collocation node (register-heavy)
     //   2: node units (s-dot, dU, regularity, stage, sphere rows, input gradients) and
     //      interval units (continuity, fixed-s rows, h gradient, cost partial)
+    // The tail units come first; the others are ordered interval by interval (or, with
+    // ATO_UNIT_ORDER=class, class by class: ProbD::cls_off then delimits the classes).
+    // unit order: ATO_UNIT_ORDER=class keeps the class-major order (all ODE units, then the node
+    // and interval units); the default is interval-major
+    static bool interval_order() {
+        const char* e = std::getenv("ATO_UNIT_ORDER");
+        return !(e && std::strcmp(e, "class") == 0);
+    }
+
     void build_units() {
         units.clear();
         auto add = [&](int kind, int n, int k) {
@@ -403,19 +413,36 @@ struct Layout {
             for (int g = 0; g < nu_t; ++g) add(UNIT_TAIL, t, g);
         }
         p.cls_off[1] = (int32_t)(units.size() / 4);
-        for (int n = 0; n < p.N; ++n)
+        auto add_ode = [&](int n) {
             for (int k = 1; k < p.K1; ++k) {
                 const int32_t* sg = &seg[((size_t)(n * p.K1 + k) * NSEG) * 2];
                 if (sg[2 * SEG_ODE_A] >= 0) add(UNIT_ODE_A, n, k);
                 if (sg[2 * SEG_ODE_B] >= 0) add(UNIT_ODE_B, n, k);
             }
-        for (int n = 0; n < p.N; ++n) {
+        };
+        auto add_rk4 = [&](int n) {
             const int32_t* sg = &seg[((size_t)(n * p.K1) * NSEG) * 2];
-            if (sg[2 * SEG_RK4] < 0) continue;
+            if (sg[2 * SEG_RK4] < 0) return;
             int ng_ = 1;
             with_model(p, [&]<class M>() { ng_ = rk4_groups<M>(); });
             for (int g = 0; g < ng_; ++g) add(UNIT_RK4, n, g);
+        };
+        if (interval_order()) {
+            // interval-major: the ODE (RK4), node and interval units of interval n are dispatched
+            // together, so the interval's w (which every one of them reads: the collocation
+            // polynomials span all of its nodes) is still in the XCD's L2 when the next unit
+            // re-reads it, instead of after the whole ODE class has streamed its Jacobian through
+            for (int n = 0; n < p.N; ++n) {
+                add_ode(n);
+                add_rk4(n);
+                add(UNIT_INTERVAL, n, 0);
+                for (int k = 0; k < p.K1; ++k) add(UNIT_NODE, n, k);
+            }
+            p.cls_off[2] = p.cls_off[3] = (int32_t)(units.size() / 4);
+            return;
         }
+        for (int n = 0; n < p.N; ++n) add_ode(n);
+        for (int n = 0; n < p.N; ++n) add_rk4(n);
         p.cls_off[2] = (int32_t)(units.size() / 4);
         for (int n = 0; n < p.N; ++n) {
             add(UNIT_INTERVAL, n, 0);

@@ -525,6 +525,7 @@ class BatchedInteriorPoint:
         dr_used = torch.zeros((m, B), dtype=torch.float64, device=self.dev)
         dw_out = zeros.clone()
         pidx = _idx(pend)
+        npass = 0
         while len(pidx):
             Ds_tot = Ss + delta_w
             dr = (-delta_c).expand(m, B).clone()
@@ -532,8 +533,14 @@ class BatchedInteriorPoint:
             dx = Sx + delta_w
             self.laps.lap('kkt_other')
             inertia = self.kkt.factor(W, Js, dx, dr, pidx)
-            self.laps.lap('kkt_factor')
+            # first pass (delta_w = 0) vs the inertia-correction retries, timed apart
+            self.laps.lap('kkt_factor' if npass == 0 else 'kkt_factor_retry')
             self.stats['factorizations'] += 1
+            fp = self.stats.setdefault('factor_passes', {})   # pass index -> [calls, instances]
+            rec = fp.setdefault(npass, [0, 0])
+            rec[0] += 1
+            rec[1] += len(pidx)
+            npass += 1
             ok = (inertia[:, 0] == n) & (inertia[:, 1] == m) & (inertia[:, 2] == 0)
             sing = inertia[:, 2] > 0
             good = pend & ok & ~sing
@@ -1128,7 +1135,8 @@ class BatchedInteriorPoint:
             return (th <= o.resto_kappa * theta_start) & ~in_f
 
         res = sub.solve(Xr0, mu0=job['mu_r'], stop_check=accept, allow_restoration=False, progress=self._progress)
-        stats = {k2: v for k2, v in sub.stats.items() if k2 not in ('restorations', 'laps', 'resto_phases', 'compactions')}
+        stats = {k2: v for k2, v in sub.stats.items()
+                 if k2 not in ('restorations', 'laps', 'resto_phases', 'compactions', 'factor_passes')}
         stats['evals'] = stats.get('evals', 0) + view.stats['evals']
         stats['resto_phases'] = [[Br, int(len(sub.history))]]
         stopped = torch.as_tensor(np.array([st == 'stopped' for st in res.status]), device=dev)
@@ -1237,7 +1245,8 @@ class BatchedInteriorPoint:
 
         res = sub.solve(Xr0, mu0=mu_r, active=R, stop_check=accept, allow_restoration=False,
                         progress=self._progress)
-        stats = {k2: v for k2, v in sub.stats.items() if k2 not in ('restorations', 'laps', 'resto_phases', 'compactions')}
+        stats = {k2: v for k2, v in sub.stats.items()
+                 if k2 not in ('restorations', 'laps', 'resto_phases', 'compactions', 'factor_passes')}
         stats['resto_phases'] = [[int(R.sum()), int(len(sub.history))]]
         self._resto_merge_stats(stats, dict(sub.laps.t))
         stopped = torch.as_tensor(np.array([st == 'stopped' for st in res.status]), device=dev)

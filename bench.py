@@ -52,6 +52,9 @@ def parse():
     ap.add_argument('--eval-warmup', type=int, default=10)
     ap.add_argument('--dtype', choices=['f64', 'f32'], default='f64', help='evaluation-kernel bench dtype')
     ap.add_argument('--layout', choices=['interleaved', 'instance'], default='interleaved')
+    ap.add_argument('--track', choices=['race', 'fig8'], default='race',
+                    help='fig8: the config-5 evaluation workload (scripts/fig_8.py, N = 50, K = 4), with --dtype f32 '
+                         '--batch 8192 --no-solve')
     ap.add_argument('--cpu-seconds', type=float, default=15.0, help='budget of the CPU baselines')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-solve', action='store_true', help='evaluation kernel only')
@@ -108,7 +111,8 @@ def eval_bench(spec, W, args, dev, world):
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json, encoding='utf-8'))
-            if tj.get('batch') == B and tj.get('dtype') == args.dtype and tj.get('layout') == args.layout:
+            if (tj.get('batch'), tj.get('dtype'), tj.get('layout'), tj.get('track', 'race')) == \
+                    (B, args.dtype, args.layout, args.track):
                 traffic = tj.get('hbm_bytes_per_launch')
         except (OSError, ValueError):
             traffic = None
@@ -125,7 +129,7 @@ def eval_bench(spec, W, args, dev, world):
     return evals, roofline
 
 
-def cpu_baseline(W, budget_s):
+def cpu_baseline(W, budget_s, spec_kw):
     '''
     Rank 0, N = 1, on the GPU box's host cores:
       * value: the single-instance interior-point solve on the CPU -- the same algorithm
@@ -139,7 +143,7 @@ def cpu_baseline(W, budget_s):
     from aircraft_trajectory_optimization_amd.solver.ipm import InteriorPointSolver, IPMOptions
     from aircraft_trajectory_optimization_amd.tracks import make_spec
     from tests.helpers import HostCheck, HostEvaluator, oracle_nlp
-    spec = make_spec(**SPEC_KW)
+    spec = make_spec(**spec_kw)
     ev = HostEvaluator(spec)
     # calibrate the iteration cap on a short solve, then time the capped solve
     t0 = time.perf_counter()
@@ -162,7 +166,7 @@ def cpu_baseline(W, budget_s):
 
     r1, n1 = rate(1, budget_s / 4)
     rT, nT = rate(threads, budget_s / 4)
-    nlp = oracle_nlp(**{k: v for k, v in SPEC_KW.items()})
+    nlp = oracle_nlp(**spec_kw)
     t0 = time.perf_counter()
     for k in range(2):
         nlp.g(W[k])
@@ -196,8 +200,10 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
 
-    spec = make_spec(**SPEC_KW)
+    spec_kw = dict(SPEC_KW, track=args.track)
+    spec = make_spec(**spec_kw)
     B = args.batch
+    track = 'racetrack' if args.track == 'race' else 'fig8'
     seeds = shard_seeds(rank, world, B)
     W, _, _ = seeded_instances(spec, seeds)
 
@@ -261,7 +267,7 @@ def main():
                 'vs_baseline': None,
                 'dtype': 'f64',
                 'data': 'synthetic: seeded cold-start instances (SURVEY 8(d) config 3 generator, raceline/instances.py)',
-                'config': {'workload': 'racetrack_parametric_esp_drone_colloc_N50_K4_cold_start_batched_sqp',
+                'config': {'workload': f'{track}_parametric_esp_drone_colloc_N50_K4_cold_start_batched_sqp',
                            'N': 50, 'K': 4, 'nz': 13, 'nu': 4, 'batch_per_gpu': B, 'global_batch': world * B,
                            'max_iter': args.max_iter, 'layout': args.layout,
                            'parallelism': f'instances sharded x{world}, records all-gathered'},
@@ -277,13 +283,13 @@ def main():
                 'sqp_full': sqp_full,
             }
             if world == 1 and not args.no_cpu_baseline:
-                out['cpu_baseline'] = cpu_baseline(W, args.cpu_seconds)
+                out['cpu_baseline'] = cpu_baseline(W, args.cpu_seconds, spec_kw)
     elif rank == 0:
         out = {'metric': METRIC, 'value': evals['value'], 'unit': evals['unit'], 'n_gpus': world,
                'steps': args.eval_steps, 'warmup': args.eval_warmup, 'ms_per_step': evals['ms_per_step'],
                'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': args.dtype,
                'data': 'synthetic: seeded cold-start instances (evaluation kernel only, --no-solve)',
-               'config': {'workload': 'racetrack_parametric_esp_drone_colloc_N50_K4_eval', 'batch_per_gpu': B,
+               'config': {'workload': f'{track}_parametric_esp_drone_colloc_N50_K4_eval', 'batch_per_gpu': B,
                           'global_batch': world * B, 'layout': args.layout},
                'roofline': roofline, 'cpu_baseline': None, 'evals': evals}
     if rank == 0:

@@ -171,3 +171,4 @@ def test_device_kkt_wide_levels_match_narrow():
     assert all(tuple(i48[b]) == tuple(i1[0]) for b in range(48))
     for b in range(48):
         assert torch.equal(x48[:, b], x1[:, 0]), b
+
