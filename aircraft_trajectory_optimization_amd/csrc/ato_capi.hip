@@ -44,6 +44,7 @@ static void release(ato_handle* h) {
     (void)hipFree(h->d_seg);
     (void)hipFree(h->d_tail);
     (void)hipFree(h->d_units);
+    (void)hipFree(h->d_units_lf);
     (void)hipFree(h->d_fpart);
     for (int32_t* d : {h->d_color, h->d_take_e, h->d_take_r, h->d_csc_ptr, h->d_csc_ent, h->d_csc_row}) (void)hipFree(d);
     (void)hipFree(h->d_dJ);
@@ -83,6 +84,7 @@ int ato_create(const ato_problem_desc* desc, ato_handle** out) {
                 }
             }
         h->L.units = kept;
+        h->L.units_lf = kept;
         h->L.p.cls_off[0] = 0;
         h->L.p.cls_off[1] = cnt[0];
         h->L.p.cls_off[2] = cnt[0] + cnt[1];
@@ -97,7 +99,8 @@ int ato_create(const ato_problem_desc* desc, ato_handle** out) {
     if ((rc = upload(h->L.geom, &h->d_geom)) || (rc = upload(h->L.node_s, &h->d_node_s)) ||
         (rc = upload(h->L.interval_s, &h->d_interval_s)) || (rc = upload(h->L.spheres, &h->d_spheres)) ||
         (rc = upload(h->L.gates, &h->d_gates)) || (rc = upload(h->L.seg, &h->d_seg)) ||
-        (rc = upload(h->L.tail, &h->d_tail)) || (rc = upload(h->L.units, &h->d_units))) {
+        (rc = upload(h->L.tail, &h->d_tail)) || (rc = upload(h->L.units, &h->d_units)) ||
+        (rc = upload(h->L.units_lf, &h->d_units_lf))) {
         release(h);
         delete h;
         return rc;
@@ -111,6 +114,9 @@ int ato_create(const ato_problem_desc* desc, ato_handle** out) {
     h->pd.seg = h->d_seg;
     h->pd.tail = h->d_tail;
     h->pd.units = h->d_units;
+    h->pd_lf = h->pd;
+    h->pd_lf.units = h->d_units_lf;
+    if (const char* e = std::getenv("ATO_LONGFIRST_MAX_B")) h->lf_max_batch = std::atoi(e);
     *out = h;
     return ATO_OK;
 }
@@ -189,7 +195,8 @@ static int eval_impl(ato_handle* h, int32_t batch, int32_t layout, const T* w, T
         int rc = ato_reserve(h, batch);
         if (rc) return rc;
     }
-    const ato::ProbD& p = h->pd;
+    // small batches run the long-first unit order (see Layout::build_units)
+    const ato::ProbD& p = batch <= h->lf_max_batch ? h->pd_lf : h->pd;
     hipError_t e = hipSuccess;
     ato::with_model(p, [&]<class M>() {
         hipEvent_t* ev = nullptr;
@@ -281,8 +288,9 @@ extern "C" int ato_hess_eval(ato_handle* h, int32_t batch, int32_t layout, const
     const ato::HessDev hd{h->d_color, h->d_take_e, h->d_take_r, h->d_csc_ptr, h->d_csc_ent, h->d_csc_row,
                           h->HL.take_off.data(), h->HL.n_colors, h->HL.nnz()};
     hipError_t e = hipSuccess;
-    ato::with_model(h->pd, [&]<class M>() {
-        e = ato::launch_hess<M>(h->pd, hd, batch, layout, w, lam, sigma, hess, h->d_dJ, h->d_dgf,
+    const ato::ProbD& p = batch <= h->lf_max_batch ? h->pd_lf : h->pd;   // unit order as in ato_eval
+    ato::with_model(p, [&]<class M>() {
+        e = ato::launch_hess<M>(p, hd, batch, layout, w, lam, sigma, hess, h->d_dJ, h->d_dgf,
                                 (hipStream_t)stream);
     });
     if (e != hipSuccess) return fail(ATO_ERR_HIP, std::string("hessian launch: ") + hipGetErrorString(e));

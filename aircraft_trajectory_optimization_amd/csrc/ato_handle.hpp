@@ -7,7 +7,9 @@
 struct ato_handle {
     ato::Layout L;
     int device = 0;
-    ato::ProbD pd{};            // device-pointer copy of L.p
+    ato::ProbD pd{};            // device-pointer copy of L.p (interval-major unit table)
+    ato::ProbD pd_lf{};         // the same with the long-first unit table (batches <= lf_max_batch)
+    int32_t lf_max_batch = 2048;
     double* d_geom = nullptr;
     double* d_node_s = nullptr;
     double* d_interval_s = nullptr;
@@ -16,6 +18,7 @@ struct ato_handle {
     int32_t* d_seg = nullptr;
     int32_t* d_tail = nullptr;
     int32_t* d_units = nullptr;
+    int32_t* d_units_lf = nullptr;
     void* d_fpart = nullptr;    // [N][reserved] cost partials (double; reused for float)
     int32_t reserved = 0;
     std::vector<hipEvent_t> events;   // 3 per timed call

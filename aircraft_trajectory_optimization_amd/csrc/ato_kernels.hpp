@@ -15,6 +15,7 @@
 //   sums the partials into f in a fixed order.
 #pragma once
 #include <vector>
+#include <type_traits>
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
 #include "ato_layout.hpp"
@@ -142,6 +143,86 @@ struct DevSinkPaired {
     __device__ __forceinline__ void row_skip() { gr += Bb; }
 };
 
+// fp32 quad writer (interleaved layout, B % 64 == 0). Lane l holds instance 4 (l mod 16) + l / 16
+// of its 64-instance chunk, so the four 16-lane rows of the wave hold four consecutive instances.
+// Four consecutive entries e .. e+3 are transposed across the rows (v_permlane32_swap, then
+// v_permlane16_swap): row m then holds entry e+m of instances 4j .. 4j+3 in lane j + 16 m, and one
+// 16-byte store per lane writes four entries of all 64 instances -- half the store instructions of
+// the paired writer, which in fp32 stores only 8 bytes per lane. Entries left over at a segment end
+// are stored one per instruction.
+// DIAGNOSTIC, rejected (tools/r03h.sh, profiles/r03/eval_ab_r03h/): fig-8 fp32 B = 8192 681 vs 638 us with
+// the paired writer, racetrack fp32 B = 512 39.0 vs 32.7 us -- the two permlane stages cost more than
+// the store instructions they save. Build with -DATO_EVAL_F32_QUAD=1 to select it.
+#ifndef ATO_EVAL_F32_QUAD
+#define ATO_EVAL_F32_QUAD 0
+#endif
+__device__ __forceinline__ void swap_rows16(float& a, float& b) {
+    auto r = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, a), __builtin_bit_cast(unsigned, b),
+                                              false, false);
+    a = __builtin_bit_cast(float, (unsigned)r[0]);
+    b = __builtin_bit_cast(float, (unsigned)r[1]);
+}
+
+__device__ __forceinline__ void st_quad(char* p, float a, float b, float c, float d) {
+    typedef float v4 __attribute__((ext_vector_type(4)));
+    *reinterpret_cast<v4*>(p) = v4{a, b, c, d};
+}
+
+template <bool WJ, bool WG>
+struct DevSinkQuad {
+    const char* Jc;     // (char*) (J + chunk base): uniform
+    const char* gc;     // (char*) (g + chunk base): uniform
+    char* Jr;           // byte address of the next entry's 64-instance row: uniform
+    char* gr;           // byte address of the next row's 64-instance row: uniform
+    long Bb;            // entry stride in bytes (B * 4)
+    long quad_off;      // this lane's byte offset in a quad store: (l / 16) B + 16 (l mod 16) bytes
+    uint32_t self_off;  // this lane's own instance byte offset inside the chunk
+    float p0, p1, p2;   // pending entries (shifted in from p2)
+    int n;              // number pending (wave-uniform)
+    __device__ __forceinline__ void flush() {
+        if (WJ) {
+            if (n >= 1) st_one(Jr - Bb + self_off, p2);
+            if (n >= 2) st_one(Jr - 2 * Bb + self_off, p1);
+            if (n >= 3) st_one(Jr - 3 * Bb + self_off, p0);
+        }
+        n = 0;
+    }
+    __device__ __forceinline__ void begin(int row0, int nnz0) {
+        flush();
+        Jr = const_cast<char*>(Jc) + (long)nnz0 * Bb;
+        gr = const_cast<char*>(gc) + (long)row0 * Bb;
+    }
+    __device__ __forceinline__ void finish() { flush(); }
+    __device__ __forceinline__ void jac(int, float v) {
+        if (WJ) {
+            if (n < 3) {
+                p0 = p1;
+                p1 = p2;
+                p2 = v;
+                ++n;
+            } else {
+                float a = p0, b = p1, c = p2, d = v;     // entries e .. e+3 of this lane's instance
+                swap_halves(a, c);
+                swap_halves(b, d);
+                swap_rows16(a, b);
+                swap_rows16(c, d);
+                st_quad(Jr - 3 * Bb + quad_off, a, b, c, d);
+                n = 0;
+            }
+        }
+        Jr += Bb;
+    }
+    __device__ __forceinline__ void row(float gv, double, double) {
+        if (WG) st_one(gr + self_off, gv);
+        gr += Bb;
+    }
+    __device__ __forceinline__ void skip() {
+        flush();
+        Jr += Bb;
+    }
+    __device__ __forceinline__ void row_skip() { gr += Bb; }
+};
+
 // decision-vector reads for the paired kernel: uniform row base + 32-bit lane byte offset
 template <class T>
 struct DevWPaired {
@@ -191,6 +272,36 @@ __global__ __launch_bounds__(WAVE) void k_eval(ProbD p, int B, int layout, const
     run_unit<M, T, KS, WJ || WG, WF, UMASK>(p, ut[0], ut[1], ut[2], W, s, go);
 }
 
+// One work unit of the paired / quad kernels: the gradient pass (grad f, cost partials) and the row
+// pass (g, J; whole wave). The gradient pass runs FIRST: its loads would otherwise queue behind the
+// row pass's ~100 stores (vmcnt counts loads and stores in order, so waiting for a load waits for
+// every store issued before it): B = 4096 527.5 -> 482 us, B = 512 48.2 -> 47.7 us (tools/r03h.sh;
+// ATO_EVAL_GRAD_FIRST=0 restores rows first). Rejected diagnostic: ATO_EVAL_LIN_KS=K1 (node /
+// interval units with a compile-time node count, so their loads hoist ahead of the stores): 218 us
+// at B = 512, the hoisted loads' registers and code size cost far more.
+#ifndef ATO_EVAL_GRAD_FIRST
+#define ATO_EVAL_GRAD_FIRST 1
+#endif
+#ifndef ATO_EVAL_LIN_KS
+#define ATO_EVAL_LIN_KS 0
+#endif
+template <class M, class T, int KS, bool ROWS, bool GRAD, int UMASK, class W, class S, class GO>
+__device__ __forceinline__ void eval_unit(const ProbD& p, const int32_t* ut, const W& w, S& s, const GO& go) {
+    const int kind = ut[0], n = ut[1], k = ut[2];
+    auto run = [&]<bool R, bool G>() {
+        if constexpr (ATO_EVAL_LIN_KS > 0 && KS == 0) {
+            if (p.K1 == ATO_EVAL_LIN_KS && (kind == UNIT_NODE || kind == UNIT_INTERVAL)) {
+                run_unit<M, T, ATO_EVAL_LIN_KS, R, G, UMASK & UMASK_LIN>(p, kind, n, k, w, s, go);
+                return;
+            }
+        }
+        run_unit<M, T, KS, R, G, UMASK>(p, kind, n, k, w, s, go);
+    };
+    if (ATO_EVAL_GRAD_FIRST && GRAD) run.template operator()<false, true>();
+    if (ROWS) run.template operator()<true, false>();     // whole wave
+    if (!ATO_EVAL_GRAD_FIRST && GRAD) run.template operator()<false, true>();
+}
+
 // Interleaved layout, even B: every lane stays active (permlane swaps need the whole wave);
 // lanes past the end of the batch compute on the last instance and store nothing.
 #ifdef ATO_EVAL_WPE      // DIAGNOSTIC (tools/diag/kkt_variants.py): force an occupancy target
@@ -202,29 +313,45 @@ template <class M, class T, int KS, bool WJ, bool WG, bool WF, bool FULL, int UM
 __global__ __launch_bounds__(WAVE) ATO_EVAL_ATTR void k_eval_paired(ProbD p, int B, int unit0, const T* __restrict__ w,
                                                       T* __restrict__ g, T* __restrict__ J,
                                                       T* __restrict__ gf, T* __restrict__ fpart) {
+    constexpr bool QUAD = FULL && ATO_EVAL_F32_QUAD && std::is_same_v<T, float>;
     const int l = threadIdx.x;
     const int chunk = blockIdx.x * WAVE;
-    const int own = 2 * (l & 31) + (l >> 5);        // instance of this lane inside the chunk
+    // instance of this lane inside the chunk
+    const int own = QUAD ? 4 * (l & 15) + (l >> 4) : 2 * (l & 31) + (l >> 5);
     const int b = chunk + own;
     const int bl = (FULL || b < B) ? b : B - 1;     // clamped instance for loads
     const int32_t* ut = p.units + 4 * (unit0 + blockIdx.y);   // wave-uniform: scalar loads
     const long Bb = (long)B * sizeof(T);
     const DevWPaired<T> W{reinterpret_cast<const char*>(w + chunk), Bb, (uint32_t)((bl - chunk) * sizeof(T))};
-    DevSinkPaired<T, WJ, WG, FULL> s;
-    s.Jc = reinterpret_cast<const char*>(J + chunk);
-    s.gc = reinterpret_cast<const char*>(g + chunk);
-    s.Jr = nullptr;
-    s.gr = nullptr;
-    s.Bb = Bb;
-    s.pair_off = (uint32_t)(((l >= 32 ? (long)B : 0L) + 2 * (l & 31)) * sizeof(T));
-    s.self_off = (uint32_t)(own * sizeof(T));
-    s.pvalid = chunk + 2 * (l & 31) < B;
-    s.svalid = b < B;
-    s.pend = T(0);
-    s.odd = false;
     const GradOut<T> go{WF ? gf + bl : nullptr, (long)B, WF ? fpart + bl : nullptr, B};
-    if (WJ || WG) run_unit<M, T, KS, true, false, UMASK>(p, ut[0], ut[1], ut[2], W, s, go);   // whole wave
-    if (WF && (FULL || b < B)) run_unit<M, T, KS, false, true, UMASK>(p, ut[0], ut[1], ut[2], W, s, go);
+    if constexpr (QUAD) {
+        DevSinkQuad<WJ, WG> s;
+        s.Jc = reinterpret_cast<const char*>(J + chunk);
+        s.gc = reinterpret_cast<const char*>(g + chunk);
+        s.Jr = nullptr;
+        s.gr = nullptr;
+        s.Bb = Bb;
+        s.quad_off = (long)(l >> 4) * Bb + 16 * (l & 15);
+        s.self_off = (uint32_t)(own * sizeof(T));
+        s.p0 = s.p1 = s.p2 = 0.0f;
+        s.n = 0;
+        eval_unit<M, T, KS, WJ || WG, WF, UMASK>(p, ut, W, s, go);
+    } else {
+        DevSinkPaired<T, WJ, WG, FULL> s;
+        s.Jc = reinterpret_cast<const char*>(J + chunk);
+        s.gc = reinterpret_cast<const char*>(g + chunk);
+        s.Jr = nullptr;
+        s.gr = nullptr;
+        s.Bb = Bb;
+        s.pair_off = (uint32_t)(((l >= 32 ? (long)B : 0L) + 2 * (l & 31)) * sizeof(T));
+        s.self_off = (uint32_t)(own * sizeof(T));
+        s.pvalid = chunk + 2 * (l & 31) < B;
+        s.svalid = b < B;
+        s.pend = T(0);
+        s.odd = false;
+        eval_unit<M, T, KS, WJ || WG, WF && FULL, UMASK>(p, ut, W, s, go);
+        if (WF && !FULL && b < B) run_unit<M, T, KS, false, true, UMASK>(p, ut[0], ut[1], ut[2], W, s, go);
+    }
 }
 
 // f[b] = sum_n fpart[n][b]  (fixed order, loads issued in batches)

@@ -256,6 +256,7 @@ struct Layout {
     std::vector<ato_gate> gates;
     std::vector<int32_t> seg, tail;   // segment tables (see ProbD)
     std::vector<int32_t> units;       // work-unit table (see ProbD)
+    std::vector<int32_t> units_lf;    // the same units, long chains first (small batches)
     std::vector<int32_t> row_ptr, col;
     std::vector<double> lbg, ubg;
     int nz = 0, nu = 0;
@@ -389,22 +390,37 @@ struct Layout {
     //   1: the ODE row groups of every collocation node (register-heavy)
     //   2: node units (s-dot, dU, regularity, stage, sphere rows, input gradients) and
     //      interval units (continuity, fixed-s rows, h gradient, cost partial)
-    // The tail units come first; the others are ordered interval by interval (or, with
-    // ATO_UNIT_ORDER=class, class by class: ProbD::cls_off then delimits the classes).
-    // unit order: ATO_UNIT_ORDER=class keeps the class-major order (all ODE units, then the node
-    // and interval units); the default is interval-major
-    static bool interval_order() {
+    // The tail units come first; the two orders of the rest follow.
+    //
+    // Unit orders. Interval-major (the default table): the ODE, interval and node units of interval
+    // n together, so the re-reads of the interval's w hit the XCD's L2. Long-first (units_lf): the
+    // interval units (the longest dependent chains) right after the tail, then interval-major ODE
+    // and node units -- at small batches (few waves per slot) the kernel's end is set by the long
+    // units dispatched last, at large ones by locality (tools/r03g.sh: B = 512 59.5 -> 47.4 us,
+    // B = 4096 507 -> 526 us). ATO_UNIT_ORDER=class|interval|longfirst forces one order for both.
+    static int forced_order() {
         const char* e = std::getenv("ATO_UNIT_ORDER");
-        return !(e && std::strcmp(e, "class") == 0);
+        if (!e) return -1;
+        if (std::strcmp(e, "class") == 0) return 0;
+        if (std::strcmp(e, "longfirst") == 0) return 2;
+        return 1;
     }
 
     void build_units() {
-        units.clear();
+        const int f = forced_order();
+        build_order(f < 0 ? 1 : f, units);
+        build_order(f < 0 ? 2 : f, units_lf);
+    }
+
+    // order 0: class-major (all ODE units, then node and interval units; ProbD::cls_off delimits
+    // the classes), 1: interval-major, 2: long-first
+    void build_order(int order, std::vector<int32_t>& out) {
+        out.clear();
         auto add = [&](int kind, int n, int k) {
-            units.push_back(kind);
-            units.push_back(n);
-            units.push_back(k);
-            units.push_back(0);
+            out.push_back(kind);
+            out.push_back(n);
+            out.push_back(k);
+            out.push_back(0);
         };
         p.cls_off[0] = 0;
         for (int t = 0; t < (int)(tail.size() / 4); ++t) {
@@ -412,7 +428,7 @@ struct Layout {
             with_model(p, [&]<class M>() { nu_t = tail_units<M>(p, tail[4 * t]); });
             for (int g = 0; g < nu_t; ++g) add(UNIT_TAIL, t, g);
         }
-        p.cls_off[1] = (int32_t)(units.size() / 4);
+        p.cls_off[1] = (int32_t)(out.size() / 4);
         auto add_ode = [&](int n) {
             for (int k = 1; k < p.K1; ++k) {
                 const int32_t* sg = &seg[((size_t)(n * p.K1 + k) * NSEG) * 2];
@@ -427,28 +443,32 @@ struct Layout {
             with_model(p, [&]<class M>() { ng_ = rk4_groups<M>(); });
             for (int g = 0; g < ng_; ++g) add(UNIT_RK4, n, g);
         };
-        if (interval_order()) {
-            // interval-major: the ODE (RK4), node and interval units of interval n are dispatched
-            // together, so the interval's w (which every one of them reads: the collocation
-            // polynomials span all of its nodes) is still in the XCD's L2 when the next unit
-            // re-reads it, instead of after the whole ODE class has streamed its Jacobian through
+        if (order == 2) {
+            for (int n = 0; n < p.N; ++n) add(UNIT_INTERVAL, n, 0);
+            for (int n = 0; n < p.N; ++n) {
+                add_ode(n);
+                add_rk4(n);
+                for (int k = 0; k < p.K1; ++k) add(UNIT_NODE, n, k);
+            }
+        } else if (order == 1) {
             for (int n = 0; n < p.N; ++n) {
                 add_ode(n);
                 add_rk4(n);
                 add(UNIT_INTERVAL, n, 0);
                 for (int k = 0; k < p.K1; ++k) add(UNIT_NODE, n, k);
             }
-            p.cls_off[2] = p.cls_off[3] = (int32_t)(units.size() / 4);
+        } else {
+            for (int n = 0; n < p.N; ++n) add_ode(n);
+            for (int n = 0; n < p.N; ++n) add_rk4(n);
+            p.cls_off[2] = (int32_t)(out.size() / 4);
+            for (int n = 0; n < p.N; ++n) {
+                add(UNIT_INTERVAL, n, 0);
+                for (int k = 0; k < p.K1; ++k) add(UNIT_NODE, n, k);
+            }
+            p.cls_off[3] = (int32_t)(out.size() / 4);
             return;
         }
-        for (int n = 0; n < p.N; ++n) add_ode(n);
-        for (int n = 0; n < p.N; ++n) add_rk4(n);
-        p.cls_off[2] = (int32_t)(units.size() / 4);
-        for (int n = 0; n < p.N; ++n) {
-            add(UNIT_INTERVAL, n, 0);
-            for (int k = 0; k < p.K1; ++k) add(UNIT_NODE, n, k);
-        }
-        p.cls_off[3] = (int32_t)(units.size() / 4);
+        p.cls_off[2] = p.cls_off[3] = (int32_t)(out.size() / 4);
     }
 
   private:
