@@ -219,7 +219,11 @@ extern "C" int ato_timing(ato_handle* h, int32_t max_calls) {
     h->timing_seen = 0;
     for (int i = 0; i < 3 * max_calls; ++i) {
         hipEvent_t e;
-        ATO_HIP(hipEventCreate(&e));
+        // timing only: without the system-scope release the stop stamp is not delayed by the
+        // write-back of the L2s the kernel's ~250 MB of stores stream through (hipExtLaunchKernel
+        // stamps with default events read 52.4 us where rocprof's trace of the same launches
+        // averaged 46.7 us, gpurun_out/r03i)
+        ATO_HIP(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
         h->events.push_back(e);
     }
     return ATO_OK;
