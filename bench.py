@@ -186,7 +186,7 @@ def main():
     import torch
     import torch.distributed as dist
     from aircraft_trajectory_optimization_amd.raceline.batched_solve import gather_solve_records, solve_records, \
-        solve_shard, summarize_records, window_timer, RECORD_BYTES
+        solve_shard, summarize_records, time_solution_gathers, window_timer, RECORD_BYTES
     from aircraft_trajectory_optimization_amd.raceline.instances import seeded_instances
     from aircraft_trajectory_optimization_amd.raceline.shard import max_over_ranks, shard_seeds
     from aircraft_trajectory_optimization_amd.solver.ipm import IPMOptions
@@ -233,6 +233,8 @@ def main():
         solve_s = max_over_ranks(t_solve, dev)
         rec = solve_records(spec, res, solver)
         allrec = gather_solve_records(rec)            # RCCL all-gather of the 32-byte records
+        # the optional audit gather of the converged decision vectors, after the window
+        sol_gather = time_solution_gathers(res.x.T.contiguous(), sync, dev) if world > 1 else None
         lockstep = int(len(solver.history))
         if rank == 0:
             summ = summarize_records(allrec)
@@ -244,6 +246,8 @@ def main():
                         'records_all_gathered': {'bytes_per_instance': RECORD_BYTES, 'instances': len(allrec),
                                                  'collective': 'all_gather' + (' (RCCL)' if world > 1 else ' (1 rank)')},
                         **summ, 'solver_stats': {k: v for k, v in res.stats.items() if k not in ('resto_phases',)}}
+            if sol_gather is not None:
+                sqp_full['solutions_all_gathered'] = sol_gather
             lap_err = None
             if not args.no_single:
                 # instance 0 re-solved alone (B = 1) from the same start: batched vs single-instance

@@ -17,7 +17,8 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from aircraft_trajectory_optimization_amd.raceline.instances import seeded_instances
-from aircraft_trajectory_optimization_amd.raceline.shard import gather_records, max_over_ranks, shard_seeds
+from aircraft_trajectory_optimization_amd.raceline.shard import gather_direct, gather_records, max_over_ranks, \
+    shard_seeds
 from aircraft_trajectory_optimization_amd.tracks import make_spec
 
 CFG = dict(track='race', model='drone', frame='parametric', N=6, K=2, use_quat=True, global_r=True)
@@ -111,3 +112,33 @@ def test_two_rank_sharded_solve_gathers_single_process_records():
     np.testing.assert_allclose(gathered[:, :2], single[:, :2], rtol=1e-12, atol=1e-15)
     s = summarize_records(gathered)
     assert s['instances'] == 4 and s['converged'] == 4, s
+
+
+def _direct_worker(rank, world, port, out):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        shard = torch.arange(5 * 7, dtype=torch.float64).reshape(5, 7) + 1000.0 * rank
+        from aircraft_trajectory_optimization_amd.raceline.batched_solve import time_solution_gathers
+        direct = gather_direct(shard)
+        ring = gather_records(shard)
+        timed = time_solution_gathers(shard, lambda: None)      # bench.py's N > 1 audit gather
+        assert timed['identical'] and timed['bytes_total'] == world * timed['bytes_per_rank'] == world * 5 * 7 * 8
+        if rank == world - 1:
+            np.save(out, np.stack([direct.numpy(), ring.numpy()]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_direct_gather_matches_all_gather():
+    ''' the point-to-point audit gather of converged solutions (3 ranks: every peer distance) is
+    rank-major and equals the ring all-gather '''
+    world = 3
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, 'direct.npy')
+        mp.spawn(_direct_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+        direct, ring = np.load(out)
+    expect = np.concatenate([np.arange(35.0).reshape(5, 7) + 1000.0 * r for r in range(world)])
+    np.testing.assert_array_equal(direct, expect)
+    np.testing.assert_array_equal(ring, expect)
