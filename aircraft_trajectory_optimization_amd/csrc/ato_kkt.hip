@@ -45,6 +45,11 @@ struct ato_kkt {
     int32_t *d_ent_src = nullptr, *d_piv_off = nullptr, *d_sc_off = nullptr;
     int32_t *d_kres_ptr = nullptr, *d_kres_col = nullptr, *d_kres_src = nullptr;
     int64_t *d_l_off = nullptr, *d_cb_off = nullptr;
+    int32_t* d_forder = nullptr;     // [F] fronts of every level grouped by kernel class (factor launches)
+    struct Seg { int start, count, cls; };
+    std::vector<std::vector<Seg>> segs;   // per level: contiguous runs of d_forder of one class
+    hipStream_t side = nullptr;      // second stream for the other classes of a level
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     int32_t cap = 0;                 // instances with factor storage
     double* d_L = nullptr;           // [cap][l_size]
     double* d_cb = nullptr;          // [cap][cb_size] contribution blocks
@@ -113,6 +118,7 @@ struct Plan {
     const int* piv_off;
     const long long* cb_off;
     const int* sc_off;
+    const int* forder;            // factor launches: front = forder[f0 + blockIdx.x]
     long long l_size, cb_size;
     int sc_size;
 };
@@ -280,7 +286,11 @@ __device__ __forceinline__ double pick(const double (&v)[NC], int h) {
 }
 
 // column k of the block into c[0 .. 32T): thread (ti, tj) of a workgroup of 32 NTJ threads owns
-// rows 32I+ti and the NC = 32 / NTJ columns 32J + h NTJ + tj (h < NC) of every lower tile (I, J)
+// rows 32I+ti and the NC = 32 / NTJ columns 32J + h NTJ + tj (h < NC) of every lower tile (I, J).
+// Only lower-triangle entries are read: A[i][k] for i >= k, A[k][i] for i < k. The diagonal
+// tiles also carry upper copies, which round differently from the lower entries (l_i c_j
+// against l_j c_i); reading only lower entries makes the factors independent of the tiling, so
+// every kernel variant (32- or 16-wide tiles) produces the same factors bit for bit.
 template <int T, int NC>
 __device__ __forceinline__ void extract_column(const double (&a)[T * (T + 1) / 2][NC], int k, int ti, int tj,
                                                double* __restrict__ c) {
@@ -291,7 +301,8 @@ __device__ __forceinline__ void extract_column(const double (&a)[T * (T + 1) / 2
         if (K == KK) {
             if (tj == kt) {
 #pragma unroll
-                for (int I = KK; I < T; ++I) c[32 * I + ti] = pick<NC>(a[slot(I, KK)], h);
+                for (int I = KK; I < T; ++I)
+                    if (I != KK || ti >= kk) c[32 * I + ti] = pick<NC>(a[slot(I, KK)], h);
             }
             if (ti == kk) {
 #pragma unroll
@@ -299,6 +310,9 @@ __device__ __forceinline__ void extract_column(const double (&a)[T * (T + 1) / 2
 #pragma unroll
                     for (int q = 0; q < NC; ++q) c[32 * J + q * NTJ + tj] = a[slot(KK, J)][q];
                 }
+#pragma unroll
+                for (int q = 0; q < NC; ++q)
+                    if (q * NTJ + tj < kk) c[32 * KK + q * NTJ + tj] = a[slot(KK, KK)][q];
             }
         }
     }
@@ -329,13 +343,16 @@ __global__ __launch_bounds__(FTT) __attribute__((amdgpu_waves_per_eu(W))) void k
     constexpr int SR = NP + 1;                   // strip row stride (odd: conflict-free reads)
     constexpr int NTJ = FTT / 32;                // column owners per tile row
     constexpr int NC = 32 / NTJ;                 // columns per thread and tile
+    static_assert(NP <= FTT, "factor-column stores: one position per thread");
+    constexpr int SRW = FTT == 64 ? 16 : 32;     // assembly strip rows (one wave: half a tile row, so
+                                                 // more fronts share a CU's LDS)
     extern __shared__ double smem[];
-    double* strip = smem;                        // [32][SR]
-    double* colb = strip + 32 * SR;              // [2 parity][2 (k, r)][NP]
+    double* strip = smem;                        // [SRW][SR]
+    double* colb = strip + SRW * SR;             // [2 parity][2 (k, r)][NP]
     int* inv = reinterpret_cast<int*>(colb + 4 * NP);   // [NP] position -> child trailing index
     int* s_spec = inv + NP;                              // [NP] guessed second column per own position
 
-    const int f = f0 + blockIdx.x;
+    const int f = P.forder[f0 + blockIdx.x];
     const int bi = blockIdx.y;
     if (bi >= batch) return;
     const int b = list ? __builtin_amdgcn_readfirstlane(list[bi]) : bi;
@@ -375,35 +392,42 @@ __global__ __launch_bounds__(FTT) __attribute__((amdgpu_waves_per_eu(W))) void k
             }
         }
     }
-    // ---- assemble strip by strip
+    // ---- assemble strip by strip (SRW rows of tile row I at a time)
 #pragma unroll
     for (int I = 0; I < T; ++I) {
         if (32 * I < A) {
-            for (int i = tid; i < 32 * SR; i += FTT) strip[i] = 0.0;
-            __syncthreads();
-            auto put = [&](int ep, double ev) {
-                const int pa = ep >> 16, pb = ep & 0xffff;
-                if (ep >= 0 && (pa >> 5) == I) {
-                    strip[(pa & 31) * SR + pb] = ev;
-                    if ((pb >> 5) == I && pa != pb) strip[(pb & 31) * SR + pa] = ev;
+#pragma unroll
+            for (int hh = 0; hh < 32 / SRW; ++hh) {
+                for (int i = tid; i < SRW * SR; i += FTT) strip[i] = 0.0;
+                __syncthreads();
+                auto in_strip = [&](int p) { return (p >> 5) == I && ((p & 31) / SRW) == hh; };
+                auto put = [&](int ep, double ev) {
+                    const int pa = ep >> 16, pb = ep & 0xffff;
+                    if (ep >= 0 && in_strip(pa)) strip[(pa % SRW) * SR + pb] = ev;
+                    if (ep >= 0 && in_strip(pb) && (pa >> 5) == I && pa != pb) strip[(pb % SRW) * SR + pa] = ev;
+                };
+                if constexpr (FTT == FT) {
+#pragma unroll
+                    for (int q = 0; q < EPT; ++q) put(epos[q], eval[q]);
+                } else {
+                    for (int e = P.ent_ptr[f * MAXT + I] + tid; e < P.ent_ptr[f * MAXT + I + 1]; e += FTT) {
+                        const int ep = P.ent_pos[e];
+                        if (in_strip(ep >> 16) || in_strip(ep & 0xffff)) {
+                            const int2 sc = P.ent_src[e];
+                            put(ep, src_value(V, sc.x, b) + src_value(V, sc.y, b));
+                        }
+                    }
                 }
-            };
-            if constexpr (FTT == FT) {
+                __syncthreads();
+                if (ti / SRW == hh) {
 #pragma unroll
-                for (int q = 0; q < EPT; ++q) put(epos[q], eval[q]);
-            } else {
-                for (int e = P.ent_ptr[f * MAXT + I] + tid; e < P.ent_ptr[f * MAXT + I + 1]; e += FTT) {
-                    const int2 sc = P.ent_src[e];
-                    put(P.ent_pos[e], src_value(V, sc.x, b) + src_value(V, sc.y, b));
+                    for (int J = 0; J <= I; ++J) {
+#pragma unroll
+                        for (int q = 0; q < NC; ++q) a[slot(I, J)][q] = strip[(ti % SRW) * SR + 32 * J + q * NTJ + tj];
+                    }
                 }
+                __syncthreads();
             }
-            __syncthreads();
-#pragma unroll
-            for (int J = 0; J <= I; ++J) {
-#pragma unroll
-                for (int q = 0; q < NC; ++q) a[slot(I, J)][q] = strip[ti * SR + 32 * J + q * NTJ + tj];
-            }
-            __syncthreads();
         } else {
 #pragma unroll
             for (int J = 0; J <= I; ++J) {
@@ -660,6 +684,315 @@ __global__ __launch_bounds__(FTT) __attribute__((amdgpu_waves_per_eu(W))) void k
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// 16-wide tiles for fronts of 161-192 positions (the interval leaves, 161-182 on the racetrack):
+// the same restricted Bunch-Kaufman elimination as k_front_factor_w, with thread (ti, tj) =
+// (tid % 16, tid / 16) of 256 holding A[16 I + ti][16 J + tj] of every lower tile J <= I (one
+// double per tile). Against six 32-wide tiles (192 positions, 21 tiles of 1024 entries) a
+// 161-176-position front keeps 66 tiles of 256 entries: 21 % fewer register entries and Schur
+// FMAs per step, dead tile columns are skipped at 16 positions instead of 32, and the assembly
+// strip is 16 rows, so the LDS (30 KB instead of 57 KB) no longer limits a CU to two fronts.
+// Operations per entry and their order are those of k_front_factor_w, and both read only the
+// lower-triangle entries, so the factors are bit for bit those of k_front_factor_w.
+// ------------------------------------------------------------------------------------------
+template <int TT>
+__device__ __forceinline__ void extract_column16(const double (&a)[TT * (TT + 1) / 2], int k, int ti, int tj,
+                                                 double* __restrict__ c) {
+    const int K = k >> 4, kk = k & 15;
+#pragma unroll
+    for (int KK = 0; KK < TT; ++KK) {
+        if (K == KK) {
+            if (tj == kk) {
+#pragma unroll
+                for (int I = KK; I < TT; ++I)
+                    if (I != KK || ti >= kk) c[16 * I + ti] = a[slot(I, KK)];
+            }
+            if (ti == kk) {
+#pragma unroll
+                for (int J = 0; J <= KK; ++J)
+                    if (J != KK || tj < kk) c[16 * J + tj] = a[slot(KK, J)];
+            }
+        }
+    }
+}
+
+template <int NW>
+__device__ __forceinline__ bool any_in_tile16(const Mask<NW>& m, int J) {   // positions 16J .. 16J+15
+    return ((m.w[J >> 2] >> ((J & 3) * 16)) & 0xffffull) != 0ull;
+}
+
+template <int TT, int W>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void k_front_factor_s(
+    Plan P, Vals V, int f0, int batch, const int* __restrict__ list, double* __restrict__ Lst,
+    int2* __restrict__ piv, double* __restrict__ dinv, int2* __restrict__ sinfo, double* __restrict__ CB,
+    int* __restrict__ inertia) {
+    constexpr int FTT = 256;
+    constexpr int NP = 16 * TT;
+    static_assert(NP <= FTT, "one factor-column position per thread");
+    constexpr int NW = (NP + 63) / 64;
+    constexpr int NQ = NW;
+    constexpr int NS = TT * (TT + 1) / 2;
+    constexpr int SR = NP + 1;                   // strip row stride (odd: conflict-free reads)
+    extern __shared__ double smem[];
+    double* strip = smem;                        // [16][SR]
+    double* colb = strip + 16 * SR;              // [2 parity][2 (k, r)][NP]
+    int* inv = reinterpret_cast<int*>(colb + 4 * NP);   // [NP] position -> child trailing index
+
+    const int f = P.forder[f0 + blockIdx.x];
+    const int bi = blockIdx.y;
+    if (bi >= batch) return;
+    const int b = list ? __builtin_amdgcn_readfirstlane(list[bi]) : bi;
+    const int tid = threadIdx.x;
+    const int ti = tid & 15, tj = tid >> 4;
+    const int lane = tid & 63;
+
+    const int p0 = P.pos_ptr[f];
+    const int A = P.pos_ptr[f + 1] - p0;
+    const int own = P.n_own[f];
+    double a[NS];
+    double* Lb = Lst + (long long)b * P.l_size + P.l_off[f];
+    int2* pv = piv + (long long)b * P.dim + P.piv_off[f];
+    double* dv = dinv + ((long long)b * P.dim + P.piv_off[f]) * 3;
+    int npos = 0, nneg = 0, nzero = 0;
+    long long loff = 0;
+
+    // ---- assemble 16-row strip by strip (entries of the plan's 32-row strip I / 2)
+#pragma unroll
+    for (int I = 0; I < TT; ++I) {
+        if (16 * I < A) {
+            for (int i = tid; i < 16 * SR; i += FTT) strip[i] = 0.0;
+            __syncthreads();
+            for (int e = P.ent_ptr[f * MAXT + (I >> 1)] + tid; e < P.ent_ptr[f * MAXT + (I >> 1) + 1]; e += FTT) {
+                const int ep = P.ent_pos[e];
+                const int pa = ep >> 16, pb = ep & 0xffff;
+                if ((pa >> 4) == I) {
+                    const int2 sc = P.ent_src[e];
+                    const double ev = src_value(V, sc.x, b) + src_value(V, sc.y, b);
+                    strip[(pa & 15) * SR + pb] = ev;
+                    if ((pb >> 4) == I && pa != pb) strip[(pb & 15) * SR + pa] = ev;
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int J = 0; J <= I; ++J) a[slot(I, J)] = strip[ti * SR + 16 * J + tj];
+            __syncthreads();
+        } else {
+#pragma unroll
+            for (int J = 0; J <= I; ++J) a[slot(I, J)] = 0.0;
+        }
+    }
+    // ---- extend-add of the children's contribution blocks (fixed child order: deterministic)
+    for (int ci = P.child_ptr[f]; ci < P.child_ptr[f + 1]; ++ci) {
+        const int c = P.child_list[ci];
+        const int pc = P.pos_ptr[c], oc = P.n_own[c];
+        const int tqc = P.pos_ptr[c + 1] - pc - oc;
+        const int* pm = P.parent_pos + pc + oc;
+        const double* cbc = CB + (long long)b * P.cb_size + P.cb_off[c];
+        for (int i = tid; i < NP; i += FTT) inv[i] = -1;
+        __syncthreads();
+        for (int q = tid; q < tqc; q += FTT) inv[pm[q]] = q;
+        __syncthreads();
+        int qr[TT];
+#pragma unroll
+        for (int I = 0; I < TT; ++I) qr[I] = inv[16 * I + ti];
+#pragma unroll
+        for (int J = 0; J < TT; ++J) {
+            const int qc = inv[16 * J + tj];
+#pragma unroll
+            for (int I = J; I < TT; ++I)
+                if (qr[I] >= 0 && qc >= 0) a[slot(I, J)] += cbc[(long long)qr[I] * tqc + qc];
+        }
+        __syncthreads();
+    }
+    // ---- restricted Bunch-Kaufman elimination of the own positions (all decisions scalar).
+    // Scalar work is kept short: every wave runs it and a SIMD issues one scalar instruction
+    // per four cycles, shared by the waves of up to three fronts. The next candidate comes
+    // from a find-first-set over the live mask; tiles left of the candidate's tile are dead (all
+    // positions below the candidate are eliminated), so the update starts there without
+    // per-tile mask tests; the live count is a counter.
+    Mask<NW> live;
+    live.set_range(0, A);
+    bool lvq[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) lvq[q] = lane + 64 * q < A;
+    bool lvt = tid < A;
+    int cit = tid;
+    int kc = 0, steps = 0, par = 0, nlive = A;
+    while (true) {
+#pragma clang loop unroll(disable)
+        while (kc < own && !live.get(kc)) ++kc;
+        if (kc >= own) break;
+        const int k = kc;
+        double* ck = colb + (par * 2 + 0) * NP;
+        double* cr = colb + (par * 2 + 1) * NP;
+        extract_column16<TT>(a, k, ti, tj, ck);
+        lds_barrier();
+        unsigned key = 0u;
+        double cv[NQ];
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int i = lane + 64 * q;
+            cv[q] = ck[i];
+            if (i < own && i != k && lvq[q]) key = max(key, mag_key(cv[q], i));
+        }
+        key = wave_max_u32(key);
+        const int r = key ? 511 - (int)(key & 0x1FFu) : -1;
+        const double akk = lane_pick<NQ>(cv, k);
+        const double lam = r >= 0 ? fabs(lane_pick<NQ>(cv, r)) : 0.0;
+        int type;            // 0: 1x1 at p, 1: 2x2 (k, r), 2: zero column
+        double arr = 0.0;
+        int p = k;
+        bool use_r = false;
+        if (r < 0 || lam == 0.0) {
+            type = akk == 0.0 ? 2 : 0;
+        } else if (fabs(akk) >= BK_ALPHA * lam) {
+            type = 0;
+        } else {
+            extract_column16<TT>(a, r, ti, tj, cr);
+            lds_barrier();
+            unsigned key2 = 0u;
+            double cw[NQ];
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const int i = lane + 64 * q;
+                cw[q] = cr[i];
+                if (i < own && i != r && lvq[q]) key2 = max(key2, mag_key(cw[q], i));
+            }
+            key2 = wave_max_u32(key2);
+            const int j2 = key2 ? 511 - (int)(key2 & 0x1FFu) : -1;
+            const double sig = j2 >= 0 ? fabs(lane_pick<NQ>(cw, j2)) : 0.0;
+            arr = lane_pick<NQ>(cw, r);
+            if (fabs(akk) * sig >= BK_ALPHA * lam * lam) {
+                type = 0;
+            } else if (fabs(arr) >= BK_ALPHA * sig) {
+                type = 0;
+                p = r;
+                use_r = true;
+            } else {
+                type = 1;
+            }
+        }
+        // ---- pivot record, inertia, factor columns, Schur update
+        double i00 = 0.0, i01 = 0.0, i11 = 0.0;
+        if (type == 2) {
+            live.clear(k);
+            ++nzero;
+        } else if (type == 0) {
+            const double d = use_r ? arr : akk;
+            i00 = rcp_nr(d);
+            live.clear(p);
+            if (d > 0.0) ++npos; else ++nneg;
+        } else {
+            const double A00 = akk, A01 = lane_pick<NQ>(cv, r), A11 = arr;
+            const double det = A00 * A11 - A01 * A01;
+            const double rdet = rcp_nr(det);
+            i00 = A11 * rdet;
+            i01 = -A01 * rdet;
+            i11 = A00 * rdet;
+            live.clear(k);
+            live.clear(r);
+            if (det < 0.0) { ++npos; ++nneg; }
+            else if (A00 + A11 > 0.0) npos += 2;
+            else nneg += 2;
+        }
+        const int ncol = type == 1 ? 2 : 1;
+        nlive -= type == 1 ? 2 : 1;
+        {
+            const int e1p = type == 1 ? k : (type == 2 ? k : p);
+            const int e2p = type == 1 ? r : -1;
+            lvt = lvt && tid != e1p && tid != e2p;
+            cit -= (tid > e1p ? 1 : 0) + (e2p >= 0 && tid > e2p ? 1 : 0);
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const int i = lane + 64 * q;
+                lvq[q] = lvq[q] && i != e1p && i != e2p;
+            }
+        }
+        if (tid == 0) {
+            pv[steps] = make_int2((type == 1 ? k : p) | (type << 16), type == 1 ? r : -1);
+            dv[3 * steps + 0] = i00;
+            dv[3 * steps + 1] = i01;
+            dv[3 * steps + 2] = i11;
+        }
+        const double* c0p = use_r ? cr : ck;     // column p (1x1) or k (2x2)
+        if (lvt) {
+            const int ci = cit;
+            const double x0 = c0p[tid];
+            if (type == 0) {
+                Lb[loff + ci] = x0 * i00;
+            } else if (type == 1) {
+                const double x1 = cr[tid];
+                Lb[loff + 2 * ci] = fma(x0, i00, x1 * i01);
+                Lb[loff + 2 * ci + 1] = fma(x0, i01, x1 * i11);
+            } else {
+                Lb[loff + ci] = 0.0;
+            }
+        }
+        loff += (long long)nlive * ncol;
+        const int npass = type == 0 ? 1 : type == 1 ? 2 : 0;
+        const int J0 = k >> 4;                   // tiles left of k's tile hold only eliminated positions
+#pragma unroll 1
+        for (int pass = 0; pass < npass; ++pass) {
+            const double* cc = pass == 1 ? cr : c0p;
+            const double g0 = pass == 1 ? i01 : i00, g1 = pass == 1 ? i11 : i01;
+            // rows in two groups (fewer row factors live at once: VGPR pressure)
+#pragma unroll
+            for (int G = 0; G < 2; ++G) {
+                constexpr int H = (TT + 1) / 2;
+                const int I0 = G == 0 ? 0 : H, I1 = G == 0 ? H : TT;
+                double li[TT];
+#pragma unroll
+                for (int I = 0; I < TT; ++I) {
+                    if (I >= I0 && I < I1) {
+                        const double x0 = c0p[16 * I + ti];
+                        li[I] = type == 1 ? fma(x0, g0, cr[16 * I + ti] * g1) : x0 * i00;
+                    }
+                }
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int J = 0; J < I1; ++J) {
+                    if (J >= J0) {
+                        const double cj = cc[16 * J + tj];
+#pragma unroll
+                        for (int I = (J > I0 ? J : I0); I < I1; ++I) a[slot(I, J)] = fma(-li[I], cj, a[slot(I, J)]);
+                    }
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        ++steps;
+        par ^= 1;
+    }
+    if (tid == 0) {
+        sinfo[(long long)b * P.F + f] = make_int2(steps, (int)loff);
+        atomicAdd(&inertia[3 * b + 0], npos);
+        atomicAdd(&inertia[3 * b + 1], nneg);
+        atomicAdd(&inertia[3 * b + 2], nzero);
+    }
+    // ---- trailing Schur complement -> contribution block of the parent (HBM)
+    const int tq = A - own;
+    if (tq > 0) {
+        double* cb = CB + (long long)b * P.cb_size + P.cb_off[f];
+#pragma unroll
+        for (int I = 0; I < TT; ++I) {
+#pragma unroll
+            for (int J = 0; J <= I; ++J) {
+                const int i = 16 * I + ti, j = 16 * J + tj;
+                if (i >= own && i < A && j >= own && j < A && (I != J || i >= j)) {
+                    cb[(long long)(i - own) * tq + (j - own)] = a[slot(I, J)];
+                    cb[(long long)(j - own) * tq + (i - own)] = a[slot(I, J)];
+                }
+            }
+        }
+    }
+}
+
+template <int TT>
+size_t factor_s_lds() {
+    constexpr int NP = 16 * TT;
+    return sizeof(double) * (16 * (NP + 1) + 4 * NP) + sizeof(int) * NP;
+}
+
 #if ATO_KKT_X_BLOCKED
 // ------------------------------------------------------------------------------------------
 // blocked factorisation (the interval leaves): the same restricted Bunch-Kaufman elimination as
@@ -711,7 +1044,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     unsigned* xk = reinterpret_cast<unsigned*>(xa + 4);   // [2 parity][2 phase][4 waves] wave max keys
     int* inv = reinterpret_cast<int*>(xk + 16);           // [NP] position -> child trailing index
 
-    const int f = f0 + blockIdx.x;
+    const int f = P.forder[f0 + blockIdx.x];
     const int bi = blockIdx.y;
     if (bi >= batch) return;
     const int b = list ? __builtin_amdgcn_readfirstlane(list[bi]) : bi;
@@ -1356,10 +1689,11 @@ __global__ __launch_bounds__(256) void k_kkt_residual(int dim, int batch, const 
     out[o] = rhs[o] - acc;
 }
 
-template <int T>
+template <int T, int FTT = FT>
 size_t factor_lds() {
     constexpr int NP = 32 * T;
-    return sizeof(double) * (32 * (NP + 1) + 4 * NP) + sizeof(int) * 2 * NP;
+    constexpr int SRW = FTT == 64 ? 16 : 32;
+    return sizeof(double) * (SRW * (NP + 1) + 4 * NP) + sizeof(int) * 2 * NP;
 }
 
 // Six-tile fronts hold 138 VGPRs: one 512-thread workgroup per CU. Allocated for four waves per
@@ -1384,7 +1718,7 @@ int launch_factor_level(const ato_kkt* h, const Plan& P, const Vals& V, int f0, 
     if constexpr (T <= 2) {
         one_wave = (long long)nf * batch >= 4 * CUS;
         if (one_wave)
-            hipLaunchKernelGGL((k_front_factor_w<T, 1, 64>), dim3(nf, batch), dim3(64), factor_lds<T>(), st, P, V,
+            hipLaunchKernelGGL((k_front_factor_w<T, 1, 64>), dim3(nf, batch), dim3(64), (factor_lds<T, 64>()), st, P, V,
                                f0, batch, list, h->d_L, h->d_piv, h->d_dinv, h->d_sinfo, h->d_cb, inertia,
                                h->d_spec);
     }
@@ -1452,11 +1786,41 @@ int launch_bwd_level(const ato_kkt* h, const Plan& P, int f0, int nf, int batch,
     return ATO_OK;
 }
 
-int factor_level(const ato_kkt* h, const Plan& P, const Vals& V, int l, int batch, const int* list, int* inertia,
-                 hipStream_t st) {
-    const int f0 = h->level_ptr[l], nf = h->level_ptr[l + 1] - f0;
+#ifndef ATO_KKT_S16_W
+#define ATO_KKT_S16_W 3
+#endif
+template <int TT>
+int launch_factor_s(const ato_kkt* h, const Plan& P, const Vals& V, int f0, int nf, int batch, const int* list,
+                    int* inertia, hipStream_t st) {
+    hipLaunchKernelGGL((k_front_factor_s<TT, ATO_KKT_S16_W>), dim3(nf, batch), dim3(256), factor_s_lds<TT>(), st, P, V,
+                       f0, batch, list, h->d_L, h->d_piv, h->d_dinv, h->d_sinfo, h->d_cb, inertia);
+    KKT_HIP(hipGetLastError());
+    return ATO_OK;
+}
+
+// Kernel class of a front of A positions: 16-wide tiles (111) for 161-176 positions, otherwise
+// the number of 32-wide tiles. A level's fronts are launched class by class (ato_kkt::segs), so
+// one 65-position separator no longer moves its whole level to three tiles.
+int front_class(int A, bool s16) {
+    if (s16 && A > 160 && A <= 176) return 111;
+    return std::max(1, (A + 31) / 32);
+}
+
+// the 16-wide-tile kernel pays off once three fronts share every CU; below that many workgroups
+// the six-tile kernel's shorter pivot steps set the time (both give the same factors bit for bit)
+int s16_min_workgroups() {
+    static const int v = [] {
+        const char* e = getenv("ATO_KKT_S16_MIN");
+        return e ? atoi(e) : 6 * CUS;
+    }();
+    return v;
+}
+
+int launch_segment(const ato_kkt* h, const Plan& P, const Vals& V, const ato_kkt::Seg& sg, int batch,
+                   const int* list, int* inertia, hipStream_t st) {
+    const int f0 = sg.start, nf = sg.count;
 #define ATO_CALL(T_) launch_factor_level<T_>(h, P, V, f0, nf, batch, list, inertia, st)
-    switch (h->level_tiles[l]) {
+    switch (sg.cls) {
         case 1: return ATO_CALL(1);
         case 2: return ATO_CALL(2);
         case 3: return ATO_CALL(3);
@@ -1465,9 +1829,44 @@ int factor_level(const ato_kkt* h, const Plan& P, const Vals& V, int l, int batc
         case 6: return ATO_CALL(6);
         case 7: return ATO_CALL(7);
         case 8: return ATO_CALL(8);
+        case 111:
+            if ((long long)nf * batch >= s16_min_workgroups())
+                return launch_factor_s<11>(h, P, V, f0, nf, batch, list, inertia, st);
+            return ATO_CALL(6);
         default: return fail(ATO_ERR_UNSUPPORTED, "KKT tiles");
     }
 #undef ATO_CALL
+}
+
+// Fronts of one level are independent: with more than one class the first class runs on the
+// caller's stream and the others on the handle's side stream (fork / join through events), so a
+// class of a few fronts overlaps the large one instead of trailing it.
+int factor_level(ato_kkt* h, const Plan& P, const Vals& V, int l, int batch, const int* list, int* inertia,
+                 hipStream_t st) {
+    const std::vector<ato_kkt::Seg>& sg = h->segs[l];
+    const int nfl = h->level_ptr[l + 1] - h->level_ptr[l];
+    // few workgroups (small batches): one launch at the level's tile count -- the level's time is
+    // one front's latency, which a second launch and the stream fork / join only add to
+    // (the kernel variant never changes the factors)
+    if (sg.size() > 1 && (long long)nfl * batch < 4 * CUS)
+        return launch_segment(h, P, V, ato_kkt::Seg{h->level_ptr[l], nfl, h->level_tiles[l]}, batch, list, inertia, st);
+    if (sg.size() == 1) return launch_segment(h, P, V, sg[0], batch, list, inertia, st);
+    if (!h->side) {
+        KKT_HIP(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
+        KKT_HIP(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
+        KKT_HIP(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
+    }
+    KKT_HIP(hipEventRecord(h->ev_fork, st));
+    KKT_HIP(hipStreamWaitEvent(h->side, h->ev_fork, 0));
+    for (size_t i = 1; i < sg.size(); ++i) {
+        const int rc = launch_segment(h, P, V, sg[i], batch, list, inertia, h->side);
+        if (rc != ATO_OK) return rc;
+    }
+    const int rc = launch_segment(h, P, V, sg[0], batch, list, inertia, st);
+    if (rc != ATO_OK) return rc;
+    KKT_HIP(hipEventRecord(h->ev_join, h->side));
+    KKT_HIP(hipStreamWaitEvent(st, h->ev_join, 0));
+    return ATO_OK;
 }
 
 int solve_level(const ato_kkt* h, const Plan& P, int l, bool fwd, int batch, const int* list, double* x,
@@ -1508,6 +1907,7 @@ Plan make_plan(const ato_kkt* h) {
     P.piv_off = h->d_piv_off;
     P.cb_off = reinterpret_cast<const long long*>(h->d_cb_off);
     P.sc_off = h->d_sc_off;
+    P.forder = h->d_forder;
     P.l_size = h->l_size;
     P.cb_size = h->cb_size;
     P.sc_size = h->sc_size;
@@ -1604,6 +2004,34 @@ int ato_kkt_create(const ato_kkt_plan_desc* d, ato_kkt** out) {
         delete h;
         return fail(ATO_ERR_ARG, "KKT plan: own positions do not cover the KKT dimension");
     }
+    // factor launch order: the fronts of every level grouped by kernel class, larger classes first
+    // (ATO_KKT_SPLIT=0: one launch per level at the level's tile count; ATO_KKT_S16=0: no
+    // 16-wide-tile class), each group in plan order
+    {
+        const char* e_split = getenv("ATO_KKT_SPLIT");
+        const char* e_s16 = getenv("ATO_KKT_S16");
+        const bool split = !(e_split && e_split[0] == '0');
+        const bool s16 = split && !(e_s16 && e_s16[0] == '0');
+        std::vector<int32_t> order;
+        order.reserve(F);
+        h->segs.assign(L, {});
+        for (int l = 0; l < L; ++l) {
+            std::vector<std::pair<int, int>> fc;   // (-class, front)
+            for (int f = d->level_ptr[l]; f < d->level_ptr[l + 1]; ++f)
+                fc.push_back({split ? -front_class(d->pos_ptr[f + 1] - d->pos_ptr[f], s16) : -d->level_tiles[l], f});
+            std::stable_sort(fc.begin(), fc.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+            for (size_t i = 0; i < fc.size(); ++i) {
+                if (i == 0 || fc[i].first != fc[i - 1].first)
+                    h->segs[l].push_back({(int)order.size(), 0, -fc[i].first});
+                ++h->segs[l].back().count;
+                order.push_back(fc[i].second);
+            }
+        }
+        if (int rc = upload(order.data(), order.size(), &h->d_forder)) {
+            ato_kkt_destroy(h);
+            return rc;
+        }
+    }
     if (h->max_ent > EPT * FT) {
         delete h;
         return fail(ATO_ERR_UNSUPPORTED, "KKT plan: more than 4096 entries in one front");
@@ -1627,11 +2055,18 @@ int ato_kkt_create(const ato_kkt_plan_desc* d, ato_kkt** out) {
 
 int ato_kkt_destroy(ato_kkt* h) {
     if (!h) return ATO_OK;
+    if (h->side) {
+        (void)hipStreamSynchronize(h->side);
+        (void)hipStreamDestroy(h->side);
+        (void)hipEventDestroy(h->ev_fork);
+        (void)hipEventDestroy(h->ev_join);
+    }
     free_storage(h);
     for (void* p : {(void*)h->d_pos_ptr, (void*)h->d_n_own, (void*)h->d_pos_index, (void*)h->d_parent_pos,
                     (void*)h->d_child_ptr, (void*)h->d_child_list, (void*)h->d_ent_ptr, (void*)h->d_ent_pos,
                     (void*)h->d_ent_src, (void*)h->d_piv_off, (void*)h->d_l_off, (void*)h->d_cb_off,
-                    (void*)h->d_sc_off, (void*)h->d_kres_ptr, (void*)h->d_kres_col, (void*)h->d_kres_src})
+                    (void*)h->d_sc_off, (void*)h->d_kres_ptr, (void*)h->d_kres_col, (void*)h->d_kres_src,
+                    (void*)h->d_forder})
         (void)hipFree(p);
     delete h;
     return ATO_OK;
