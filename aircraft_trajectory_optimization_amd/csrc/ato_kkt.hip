@@ -30,6 +30,7 @@
 #include <vector>
 #include <cstdint>
 #include <cstdlib>
+#include <type_traits>
 #include "../../include/ato_kkt.h"
 #include "../../include/ato.h"
 
@@ -88,6 +89,9 @@ constexpr int ST = 128;                   // solve threads per (front, instance)
 constexpr int EPT = 8;                    // entries per thread and front (<= 4096 per front)
 #ifndef ATO_KKT_SPEC
 #define ATO_KKT_SPEC 0
+#endif
+#ifndef ATO_KKT_S16_NG
+#define ATO_KKT_S16_NG 3      // row groups of the 16-wide-tile Schur update (B = 512 factor: 2 groups 18.46 ms, 3: 18.22, 4: 18.57)
 #endif
 #ifndef ATO_KKT_X_BLOCKED
 #define ATO_KKT_X_BLOCKED 0   // DIAGNOSTIC: the blocked leaf kernel (k_front_factor_blk, rejected)
@@ -699,20 +703,35 @@ template <int TT>
 __device__ __forceinline__ void extract_column16(const double (&a)[TT * (TT + 1) / 2], int k, int ti, int tj,
                                                  double* __restrict__ c) {
     const int K = k >> 4, kk = k & 15;
+    // one case per tile column (a switch: a branch tree instead of a compare per tile)
+    auto one = [&](auto KC) {
+        constexpr int KK = decltype(KC)::value;
+        if (tj == kk) {
 #pragma unroll
-    for (int KK = 0; KK < TT; ++KK) {
-        if (K == KK) {
-            if (tj == kk) {
-#pragma unroll
-                for (int I = KK; I < TT; ++I)
-                    if (I != KK || ti >= kk) c[16 * I + ti] = a[slot(I, KK)];
-            }
-            if (ti == kk) {
-#pragma unroll
-                for (int J = 0; J <= KK; ++J)
-                    if (J != KK || tj < kk) c[16 * J + tj] = a[slot(KK, J)];
-            }
+            for (int I = KK; I < TT; ++I)
+                if (I != KK || ti >= kk) c[16 * I + ti] = a[slot(I, KK)];
         }
+        if (ti == kk) {
+#pragma unroll
+            for (int J = 0; J <= KK; ++J)
+                if (J != KK || tj < kk) c[16 * J + tj] = a[slot(KK, J)];
+        }
+    };
+    static_assert(TT <= 12, "extract_column16: tile-column cases");
+    switch (K) {
+        case 0: one(std::integral_constant<int, 0>{}); break;
+        case 1: one(std::integral_constant<int, 1>{}); break;
+        case 2: one(std::integral_constant<int, 2>{}); break;
+        case 3: one(std::integral_constant<int, 3>{}); break;
+        case 4: one(std::integral_constant<int, 4>{}); break;
+        case 5: one(std::integral_constant<int, 5>{}); break;
+        case 6: if constexpr (TT > 6) one(std::integral_constant<int, 6>{}); break;
+        case 7: if constexpr (TT > 7) one(std::integral_constant<int, 7>{}); break;
+        case 8: if constexpr (TT > 8) one(std::integral_constant<int, 8>{}); break;
+        case 9: if constexpr (TT > 9) one(std::integral_constant<int, 9>{}); break;
+        case 10: if constexpr (TT > 10) one(std::integral_constant<int, 10>{}); break;
+        case 11: if constexpr (TT > 11) one(std::integral_constant<int, 11>{}); break;
+        default: break;
     }
 }
 
@@ -935,11 +954,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void k
         for (int pass = 0; pass < npass; ++pass) {
             const double* cc = pass == 1 ? cr : c0p;
             const double g0 = pass == 1 ? i01 : i00, g1 = pass == 1 ? i11 : i01;
-            // rows in two groups (fewer row factors live at once: VGPR pressure)
+            // rows in NG groups (fewer row factors live at once: VGPR pressure)
+            constexpr int NG = ATO_KKT_S16_NG;
 #pragma unroll
-            for (int G = 0; G < 2; ++G) {
-                constexpr int H = (TT + 1) / 2;
-                const int I0 = G == 0 ? 0 : H, I1 = G == 0 ? H : TT;
+            for (int G = 0; G < NG; ++G) {
+                const int I0 = (G * TT) / NG, I1 = ((G + 1) * TT) / NG;
+                if (I1 <= J0) continue;              // rows of eliminated tiles only
                 double li[TT];
 #pragma unroll
                 for (int I = 0; I < TT; ++I) {

@@ -98,7 +98,10 @@ def test_batched_device_restoration_follows_single_instance():
     W = np.repeat(spec.w0[None], B, axis=0)
     W[0, :spec.N] *= 1 + 0.1 * rng.uniform(-1, 1, spec.N)
     W[1, :spec.N] *= 1 + 0.1 * rng.uniform(-1, 1, spec.N)
-    opts = IPMOptions(max_iter=300)
+    # IPOPT's own iteration limit in the reference (base_raceline.py:54): with 300 the KKT
+    # rounding of a build can leave one of these instances short of convergence (seed 0 of
+    # tools/diag/resto_seeds.py: 314 iterations)
+    opts = IPMOptions(max_iter=1000)
     solver = device_solver(spec, B, spec.lbw, spec.ubw, opts)
     res = solver.solve(W)
     hist = solver.history                        # [iteration][f, pr, du, mu, E0, restorations][instance]
