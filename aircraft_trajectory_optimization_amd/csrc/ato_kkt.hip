@@ -824,23 +824,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void k
         __syncthreads();
     }
     // ---- restricted Bunch-Kaufman elimination of the own positions (all decisions scalar).
-    // Scalar work is kept short: every wave runs it and a SIMD issues one scalar instruction
-    // per four cycles, shared by the waves of up to three fronts. The next candidate comes
-    // from a find-first-set over the live mask; tiles left of the candidate's tile are dead (all
-    // positions below the candidate are eliminated), so the update starts there without
-    // per-tile mask tests; the live count is a counter.
-    Mask<NW> live;
-    live.set_range(0, A);
+    // Scalar work is kept short: every wave runs it, and the CU's one scalar unit serves the
+    // waves of up to three fronts (SQ counters: ~340 scalar instructions per pivot step and wave
+    // against ~240 vector ones before). The next candidate is a find-first-set over the ballot of
+    // the lanes' live flags, evaluated at the END of the step (with the scan at the loop head the
+    // register allocator copied the whole register block on every iteration); tiles left of the
+    // pivot's tile hold only eliminated positions, so the update starts there; the live count is a
+    // counter.
     bool lvq[NQ];
 #pragma unroll
     for (int q = 0; q < NQ; ++q) lvq[q] = lane + 64 * q < A;
     bool lvt = tid < A;
     int cit = tid;
     int kc = 0, steps = 0, par = 0, nlive = A;
-    while (true) {
-#pragma clang loop unroll(disable)
-        while (kc < own && !live.get(kc)) ++kc;
-        if (kc >= own) break;
+    {   // first live own position >= kc: find-first-set over the ballot of the lanes' live flags
+        int nk = own;
+#pragma unroll
+        for (int q = NQ - 1; q >= 0; --q) {
+            const int lo = kc - 64 * q, hi = own - 64 * q;
+            unsigned long long m = lo <= 0 ? ~0ull : (lo >= 64 ? 0ull : (~0ull << lo));
+            m &= hi >= 64 ? ~0ull : (hi <= 0 ? 0ull : ((1ull << hi) - 1ull));
+            const unsigned long long w = __ballot(lvq[q]) & m;
+            nk = w ? 64 * q + (int)__builtin_ctzll(w) : nk;
+        }
+        kc = nk;
+    }
+    while (kc < own) {
         const int k = kc;
         double* ck = colb + (par * 2 + 0) * NP;
         double* cr = colb + (par * 2 + 1) * NP;
@@ -894,12 +903,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void k
         // ---- pivot record, inertia, factor columns, Schur update
         double i00 = 0.0, i01 = 0.0, i11 = 0.0;
         if (type == 2) {
-            live.clear(k);
             ++nzero;
         } else if (type == 0) {
             const double d = use_r ? arr : akk;
             i00 = rcp_nr(d);
-            live.clear(p);
             if (d > 0.0) ++npos; else ++nneg;
         } else {
             const double A00 = akk, A01 = lane_pick<NQ>(cv, r), A11 = arr;
@@ -908,8 +915,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void k
             i00 = A11 * rdet;
             i01 = -A01 * rdet;
             i11 = A00 * rdet;
-            live.clear(k);
-            live.clear(r);
             if (det < 0.0) { ++npos; ++nneg; }
             else if (A00 + A11 > 0.0) npos += 2;
             else nneg += 2;
@@ -982,6 +987,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void k
         }
         ++steps;
         par ^= 1;
+        {   // first live own position >= kc: find-first-set over the ballot of the lanes' live flags
+            int nk = own;
+#pragma unroll
+            for (int q = NQ - 1; q >= 0; --q) {
+                const int lo = kc - 64 * q, hi = own - 64 * q;
+                unsigned long long m = lo <= 0 ? ~0ull : (lo >= 64 ? 0ull : (~0ull << lo));
+                m &= hi >= 64 ? ~0ull : (hi <= 0 ? 0ull : ((1ull << hi) - 1ull));
+                const unsigned long long w = __ballot(lvq[q]) & m;
+                nk = w ? 64 * q + (int)__builtin_ctzll(w) : nk;
+            }
+            kc = nk;
+        }
     }
     if (tid == 0) {
         sinfo[(long long)b * P.F + f] = make_int2(steps, (int)loff);

@@ -1,0 +1,27 @@
+#!/bin/bash
+# r03u: ballot live scan at the end of the step in the 16-wide-tile leaf kernel against r03r: KKT
+# tests, factor timing, SALU / VALU / branch counts of the leaf kernel; restoration test at IPOPT's max_iter
+set -u
+cd "${GRAFT_REPO_ROOT}"
+OUT=gpurun_out/r03u
+mkdir -p $OUT
+export TMPDIR=/tmp
+step() {
+  local name=$1 secs=$2; shift 2
+  echo "[r03u] $(date +%T) $name"
+  timeout -k 10 "$secs" "$@" > $OUT/$name.log 2>&1
+  local rc=$?
+  echo "[r03u] $name rc=$rc"
+  case $rc in 0) ;; 124|137|134|139|136|135) echo "crash-like exit: stopping"; exit $rc ;; esac
+  find $OUT \( -name '*_trace.csv' -o -name '*.db' \) -delete 2>/dev/null
+}
+step pytest_kkt 300 python -u -m pytest tests/test_gpu_kkt.py tests/test_gpu_batched_ipm.py::test_batched_device_restoration_follows_single_instance -x -v --timeout 200 --timeout-method thread -p no:cacheprovider
+grep -E "passed|failed" $OUT/pytest_kkt.log | tail -2
+for rep in 1 2; do
+  step kkt_cur_$rep 200 python tools/bench_kkt.py --batch 512 --reps 7 --out $OUT/kkt_cur_$rep.json
+  ATO_LIB_PATH=$PWD/tools/diag/_lib/libato_r03r.so step kkt_r03r_$rep 200 python tools/bench_kkt.py --batch 512 --reps 7 --out $OUT/kkt_r03r_$rep.json
+done
+grep -H '"factor_ms"' $OUT/kkt_*.json
+step pmc_cur 90 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_WAVE_CYCLES --output-format csv -d $OUT/pmc_cur -o run -- python tools/bench_kkt.py --batch 512 --reps 2
+ATO_LIB_PATH=$PWD/tools/diag/_lib/libato_r03r.so step pmc_r03r 90 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_WAVE_CYCLES --output-format csv -d $OUT/pmc_r03r -o run -- python tools/bench_kkt.py --batch 512 --reps 2
+echo done
