@@ -87,9 +87,6 @@ int fail(int code, const std::string& m) {
 constexpr int FT = 512;                   // factor threads per (front, instance) (16 x 32 grid)
 constexpr int ST = 128;                   // solve threads per (front, instance): two waves (256: B = 512 solve 3.02 ms, 128: 2.63 ms)
 constexpr int EPT = 8;                    // entries per thread and front (<= 4096 per front)
-#ifndef ATO_KKT_SPEC
-#define ATO_KKT_SPEC 0
-#endif
 #ifndef ATO_KKT_S16_NG
 #define ATO_KKT_S16_NG 3      // row groups of the 16-wide-tile Schur update (B = 512 factor: 2 groups 18.46 ms, 3: 18.22, 4: 18.57)
 #endif
@@ -354,7 +351,6 @@ __global__ __launch_bounds__(FTT) __attribute__((amdgpu_waves_per_eu(W))) void k
     double* strip = smem;                        // [SRW][SR]
     double* colb = strip + SRW * SR;             // [2 parity][2 (k, r)][NP]
     int* inv = reinterpret_cast<int*>(colb + 4 * NP);   // [NP] position -> child trailing index
-    int* s_spec = inv + NP;                              // [NP] guessed second column per own position
 
     const int f = P.forder[f0 + blockIdx.x];
     const int bi = blockIdx.y;
@@ -371,9 +367,6 @@ __global__ __launch_bounds__(FTT) __attribute__((amdgpu_waves_per_eu(W))) void k
     double* Lb = Lst + (long long)b * P.l_size + P.l_off[f];
     int2* pv = piv + (long long)b * P.dim + P.piv_off[f];
     double* dv = dinv + ((long long)b * P.dim + P.piv_off[f]) * 3;
-    int* sp = spec + (long long)b * P.dim + P.piv_off[f];
-    if (ATO_KKT_SPEC)
-        for (int i = tid; i < own; i += FTT) s_spec[i] = sp[i];
     int npos = 0, nneg = 0, nzero = 0;
     long long loff = 0;                          // running offset in the front's column stream
     KST_DECL(f == ATO_KKT_STAMP_FRONT && blockIdx.y == 0)
@@ -466,30 +459,33 @@ __global__ __launch_bounds__(FTT) __attribute__((amdgpu_waves_per_eu(W))) void k
         }
         __syncthreads();
     }
-    // ---- restricted Bunch-Kaufman elimination of the own positions (all decisions scalar)
-    Mask<NW> live;                // scalar copy: candidate scan, tile skipping
-    live.set_range(0, A);
+    // ---- restricted Bunch-Kaufman elimination of the own positions (all decisions scalar; the
+    // next candidate by a find-first-set over the ballot of the lanes' live flags at the end of
+    // the step, as in k_front_factor_s; tiles left of the pivot's tile are skipped in the update)
     bool lvq[NQ];                 // per lane: position lane + 64 q live
 #pragma unroll
     for (int q = 0; q < NQ; ++q) lvq[q] = lane + 64 * q < A;
     bool lvt = tid < A;           // per thread: its factor-column position tid live ...
     int cit = tid;                // ... and its index among the live positions
-    int kc = 0, steps = 0, par = 0;
+    int kc = 0, steps = 0, par = 0, nlive = A;
     KST(0);                      // assembly
-    while (true) {
-        while (kc < own && !live.get(kc)) ++kc;
-        if (kc >= own) break;
+    {   // first live own position >= kc: find-first-set over the ballot of the lanes' live flags
+        int nk = own;
+#pragma unroll
+        for (int q = NQ - 1; q >= 0; --q) {
+            const int lo = kc - 64 * q, hi = own - 64 * q;
+            unsigned long long m = lo <= 0 ? ~0ull : (lo >= 64 ? 0ull : (~0ull << lo));
+            m &= hi >= 64 ? ~0ull : (hi <= 0 ? 0ull : ((1ull << hi) - 1ull));
+            const unsigned long long w = __ballot(lvq[q]) & m;
+            nk = w ? 64 * q + (int)__builtin_ctzll(w) : nk;
+        }
+        kc = nk;
+    }
+    while (kc < own) {
         const int k = kc;
         double* ck = colb + (par * 2 + 0) * NP;
         double* cr = colb + (par * 2 + 1) * NP;
         extract_column<T, NC>(a, k, ti, tj, ck);
-        // speculative second column (ATO_KKT_SPEC): the r Bunch-Kaufman took for k in this storage
-        // slot's previous factorisation, extracted with column k -- a right guess saves the second
-        // barrier and changes nothing else. Measured: B = 512 24.8 -> 25.7 ms, B = 1 0.77 -> 0.81 ms
-        // (the extra extraction on every guessed step costs more than the barriers it saves); off.
-        const int sr = ATO_KKT_SPEC ? __builtin_amdgcn_readfirstlane(s_spec[k]) : -1;
-        const bool spec_ok = ATO_KKT_SPEC && sr >= 0 && sr < own && sr != k && live.get(sr);
-        if (spec_ok) extract_column<T, NC>(a, sr, ti, tj, cr);
         lds_barrier();
         KST(1);                  // extract + barrier (waits for the slowest wave's update)
         // lambda = max_{i eligible, i != k} |A_ik| and its index r
@@ -527,11 +523,8 @@ __global__ __launch_bounds__(FTT) __attribute__((amdgpu_waves_per_eu(W))) void k
             type = 0;
 #endif
         } else {
-            if (!(spec_ok && r == sr)) {
-                extract_column<T, NC>(a, r, ti, tj, cr);
-                lds_barrier();
-            }
-            if (ATO_KKT_SPEC && tid == 0 && r != sr) sp[k] = r;
+            extract_column<T, NC>(a, r, ti, tj, cr);
+            lds_barrier();
             unsigned key2 = 0u;
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
@@ -557,12 +550,10 @@ __global__ __launch_bounds__(FTT) __attribute__((amdgpu_waves_per_eu(W))) void k
         // ---- pivot record, inertia, factor columns, Schur update
         double i00 = 0.0, i01 = 0.0, i11 = 0.0;
         if (type == 2) {
-            live.clear(k);
             ++nzero;
         } else if (type == 0) {
             const double d = use_r ? arr : akk;
             i00 = rcp_nr(d);
-            live.clear(p);
             if (d > 0.0) ++npos; else ++nneg;
         } else {
             const double A00 = akk, A01 = lane_pick<NQ>(cv, r), A11 = arr;
@@ -571,15 +562,13 @@ __global__ __launch_bounds__(FTT) __attribute__((amdgpu_waves_per_eu(W))) void k
             i00 = A11 * rdet;
             i01 = -A01 * rdet;
             i11 = A00 * rdet;
-            live.clear(k);
-            live.clear(r);
             if (det < 0.0) { ++npos; ++nneg; }
             else if (A00 + A11 > 0.0) npos += 2;
             else nneg += 2;
         }
         KST(6);                  // pivot inverse, inertia
-        const int nlive = live.count();
         const int ncol = type == 1 ? 2 : 1;
+        nlive -= ncol;
         {
             const int e1p = type == 1 ? k : (type == 2 ? k : p);
             const int e2p = type == 1 ? r : -1;
@@ -642,7 +631,7 @@ __global__ __launch_bounds__(FTT) __attribute__((amdgpu_waves_per_eu(W))) void k
             }
 #pragma unroll
             for (int J = 0; J < T; ++J) {
-                if (live.any_in_tile(J)) {
+                if (J >= (k >> 5)) {     // tiles left of the pivot's tile hold only eliminated positions
                     double cj[NC];
 #pragma unroll
                     for (int h = 0; h < NC; ++h) cj[h] = cc[32 * J + h * NTJ + tj];
@@ -657,6 +646,18 @@ __global__ __launch_bounds__(FTT) __attribute__((amdgpu_waves_per_eu(W))) void k
         ++steps;
         par ^= 1;
         KST(4);                  // Schur update
+        {   // first live own position >= kc: find-first-set over the ballot of the lanes' live flags
+            int nk = own;
+#pragma unroll
+            for (int q = NQ - 1; q >= 0; --q) {
+                const int lo = kc - 64 * q, hi = own - 64 * q;
+                unsigned long long m = lo <= 0 ? ~0ull : (lo >= 64 ? 0ull : (~0ull << lo));
+                m &= hi >= 64 ? ~0ull : (hi <= 0 ? 0ull : ((1ull << hi) - 1ull));
+                const unsigned long long w = __ballot(lvq[q]) & m;
+                nk = w ? 64 * q + (int)__builtin_ctzll(w) : nk;
+            }
+            kc = nk;
+        }
     }
     KST_DUMP(steps);
     if (tid == 0) {

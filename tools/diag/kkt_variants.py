@@ -3,7 +3,9 @@ DIAGNOSTIC builds of libato.so (not shipped): recompile one translation unit wit
 defines and link it with the library's other objects into tools/diag/_lib/libato_<name>.so,
 which tools/gpu_check.sh (`kktvar`, `evalvar`) times through ATO_LIB_PATH.
 
-    python tools/diag/kkt_variants.py NAME [--unit ato_kkt|ato_inst1|...] [-DFLAG ...]   (CPU)
+    python tools/diag/kkt_variants.py NAME [--unit ato_kkt|ato_inst1|...] [--src FILE] [-DFLAG ...]   (CPU)
+
+--src compiles FILE (e.g. an older ato_kkt.hip) in place of the unit's own source.
 '''
 import argparse
 import glob
@@ -16,7 +18,7 @@ ROOT = os.path.dirname(os.path.dirname(HERE))
 PKG = os.path.join(ROOT, 'aircraft_trajectory_optimization_amd')
 
 
-def build(name, unit, flags):
+def build(name, unit, flags, src_override=None):
     from aircraft_trajectory_optimization_amd import build_native as bn
     bn.build(verbose=False)
     out = os.path.join(HERE, '_lib')
@@ -26,6 +28,8 @@ def build(name, unit, flags):
         src, extra = os.path.join(PKG, 'csrc', 'ato_inst.hip'), [f'-DATO_INST={unit[len("ato_inst"):]}']
     else:
         src, extra = os.path.join(PKG, 'csrc', unit + '.hip'), []
+    if src_override:
+        src = os.path.abspath(src_override)
     subprocess.run(['hipcc', *bn.FLAGS, *extra, *flags, '-c', src, '-o', obj], check=True)
     objs = [o for o in glob.glob(os.path.join(bn.OBJ, '*.o')) if os.path.basename(o) != unit + '.o'] + [obj]
     lib = os.path.join(out, f'libato_{name}.so')
@@ -39,5 +43,6 @@ if __name__ == '__main__':
     ap = argparse.ArgumentParser()
     ap.add_argument('name')
     ap.add_argument('--unit', default='ato_kkt')
+    ap.add_argument('--src', default=None)
     a, rest = ap.parse_known_args()
-    build(a.name, a.unit, rest)
+    build(a.name, a.unit, rest, a.src)
