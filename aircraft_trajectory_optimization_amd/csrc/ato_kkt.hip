@@ -87,8 +87,17 @@ int fail(int code, const std::string& m) {
 constexpr int FT = 512;                   // factor threads per (front, instance) (16 x 32 grid)
 constexpr int ST = 128;                   // solve threads per (front, instance): two waves (256: B = 512 solve 3.02 ms, 128: 2.63 ms)
 constexpr int EPT = 8;                    // entries per thread and front (<= 4096 per front)
+#ifndef ATO_KKT_W_JSKIP
+#define ATO_KKT_W_JSKIP 1
+#endif
+#ifndef ATO_KKT_S16_JSKIP
+#define ATO_KKT_S16_JSKIP 0    // 1: skip the tile columns left of the pivot's tile in the leaf update. Off: the
+                               // per-tile guards cost more scalar issue than the FMAs they save (B = 512
+                               // factor 15.16 -> 13.74 ms with two row groups; profiles/r03/kkt_leaf16/r03z_*)
+#endif
 #ifndef ATO_KKT_S16_NG
-#define ATO_KKT_S16_NG 3      // row groups of the 16-wide-tile Schur update (B = 512 factor: 2 groups 18.46 ms, 3: 18.22, 4: 18.57)
+#define ATO_KKT_S16_NG 2      // row groups of the 16-wide-tile Schur update (with tile guards: 2 groups 18.46 ms,
+                              // 3: 18.22, 4: 18.57; without: 2: 13.74, 3: 14.07)
 #endif
 #ifndef ATO_KKT_X_BLOCKED
 #define ATO_KKT_X_BLOCKED 0   // DIAGNOSTIC: the blocked leaf kernel (k_front_factor_blk, rejected)
@@ -631,7 +640,7 @@ __global__ __launch_bounds__(FTT) __attribute__((amdgpu_waves_per_eu(W))) void k
             }
 #pragma unroll
             for (int J = 0; J < T; ++J) {
-                if (J >= (k >> 5)) {     // tiles left of the pivot's tile hold only eliminated positions
+                if (!ATO_KKT_W_JSKIP || J >= (k >> 5)) {   // tiles left of the pivot's tile: eliminated positions
                     double cj[NC];
 #pragma unroll
                     for (int h = 0; h < NC; ++h) cj[h] = cc[32 * J + h * NTJ + tj];
@@ -977,7 +986,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void k
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int J = 0; J < I1; ++J) {
-                    if (J >= J0) {
+                    if (ATO_KKT_S16_JSKIP == 0 || J >= J0) {
                         const double cj = cc[16 * J + tj];
 #pragma unroll
                         for (int I = (J > I0 ? J : I0); I < I1; ++I) a[slot(I, J)] = fma(-li[I], cj, a[slot(I, J)]);

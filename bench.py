@@ -195,10 +195,10 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
-    if world > 1:
-        dist.init_process_group('nccl')
-    torch.cuda.set_device(local)
+    torch.cuda.set_device(local)                 # before the process group: RCCL binds this rank's device
     dev = torch.device('cuda', local)
+    if world > 1:
+        dist.init_process_group('nccl', device_id=dev)
 
     spec_kw = dict(SPEC_KW, track=args.track)
     spec = make_spec(**spec_kw)
