@@ -760,6 +760,7 @@ class BatchedInteriorPoint:
             laps.lap('check')
             stepping = act.clone()
             resto = torch.zeros(B, dtype=torch.bool, device=dev)
+            kresto = resto
             if progress and it % progress == 0:
                 import sys
                 print(f'[batched ipm{" resto" if stop_check is not None else ""}] iter {it}: '
@@ -802,7 +803,13 @@ class BatchedInteriorPoint:
                 dx, ds, dy, delta_w, ok, ctx = self._kkt_step(W, Js, Sx, Ss, rhs_x, rhs_s, rhs_y, mu, dwl, act)
                 laps.lap('kkt_other')
                 kfail = act & ~ok
-                status = torch.where(kfail, torch.full_like(status, KKT_FAILED), status)
+                if allow_restoration:
+                    # IPOPT's fallback when no search direction can be computed (delta_w beyond its
+                    # maximum): the line search is skipped and the feasibility restoration phase starts
+                    # (IpoptAlgorithm::Optimize -> BacktrackingLineSearch::ActivateFallbackMechanism)
+                    kresto = kfail
+                else:
+                    status = torch.where(kfail, torch.full_like(status, KKT_FAILED), status)
                 act = act & ok
                 dwl = torch.where(act & (delta_w > 0), delta_w, dwl)
                 # ---- bound multiplier steps, fraction to the boundary
@@ -888,6 +895,7 @@ class BatchedInteriorPoint:
                         laps.lap('soc')
                     first = first & False
                     alpha = torch.where(pend, alpha * 0.5, alpha)
+                resto = resto | kresto
                 laps.lap('ls_logic')
                 # ---- accept
                 upd = act & ~resto

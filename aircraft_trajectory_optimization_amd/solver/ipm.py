@@ -17,7 +17,8 @@ IPOPT's default options:
   * filter line search with switching / Armijo conditions and second-order corrections
   * convergence on the scaled optimality error E_0 <= tol (1e-8) plus IPOPT's unscaled
     dual / constraint / complementarity limits; "acceptable" level 1e-6 for 15 iterations
-  * feasibility restoration when the line search fails (IPOPT's min ||c||_1 phase): an
+  * feasibility restoration when the line search fails or no search direction can be computed
+    (IPOPT's fallback mechanism; its min ||c||_1 phase): an
     interior-point solve of  min rho sum(p + n) + zeta/2 |D_R (x - x_r)|^2  s.t.  c(x) - p + n
     within the bounds, p, n >= 0  (rho = 1000, zeta = sqrt(mu), D_R = min(1, 1/|x_r|)), started
     from the closed-form p, n and stopped as soon as the original filter accepts its iterate
@@ -308,8 +309,31 @@ class InteriorPointSolver:
             rhs_y = -r
             step = self._kkt(W, J, Sx, Ss, rhs_x, rhs_s, rhs_y, iin, mu, delta_w_last)
             if step is None:
-                status = 'kkt_failure'
-                break
+                # IPOPT's fallback when no search direction can be computed (delta_w beyond its
+                # maximum): skip the line search, start the feasibility restoration phase
+                # (IpoptAlgorithm::Optimize -> BacktrackingLineSearch::ActivateFallbackMechanism)
+                if in_resto:
+                    status = 'kkt_failure'
+                    break
+                if n_resto >= o.max_resto:
+                    status = 'restoration_failed'
+                    break
+                theta, _ = theta_of(g, s)
+                phi = phi_of(f, x, s, mu)
+                n_resto += 1
+                filt.append(((1 - o.gamma_theta) * theta, phi - o.gamma_phi * theta))
+                xr = self._restore(x, g, mu, theta, filt, theta_of, phi_of, lbg, ubg, xL, xU, dL, dU, iin)
+                if xr is None:
+                    status = 'restoration_failed'
+                    break
+                x = xr
+                f, g, gf, jv = self._eval(x)
+                s = self._push(g[iin], dL, dU)
+                a, b, c, d = slacks(x, s)
+                zl, zu = np.where(hxl, mu / a, 0), np.where(hxu, mu / b, 0)
+                vl, vu = np.where(hsl, mu / c, 0), np.where(hsu, mu / d, 0)
+                y = self._ls_multipliers(self._J(jv), gf, zl, zu, vl, vu, iin)
+                continue
             dx, ds, dy, delta_w, solve = step
             if delta_w > 0:
                 delta_w_last = delta_w

@@ -92,3 +92,47 @@ def test_compaction_follows_full_width_solve():
     for a, b in ((r0.x, r1.x), (r0.lam_g, r1.lam_g), (r0.lam_x, r1.lam_x), (r0.f, r1.f)):
         assert torch.allclose(a, b, rtol=1e-12, atol=1e-12)
     assert h0.shape == h1.shape and np.allclose(h0, h1, rtol=1e-12, atol=1e-12)
+
+
+def test_kkt_failure_falls_back_to_restoration():
+    ''' IPOPT's fallback mechanism: when no search direction can be computed (delta_w beyond its
+    maximum) the instance enters the feasibility restoration phase instead of stopping
+    (IpoptAlgorithm::Optimize -> BacktrackingLineSearch::ActivateFallbackMechanism). The KKT step
+    of instance 1 is made to fail at its third iteration in both solvers: both restore, neither
+    reports 'kkt_failure', and the batched instance follows the single-instance solve. '''
+    spec = product_spec(track='race', model='point', use_quat=False, N=8, K=3)
+    B = 2
+    W = _instances(spec, B)
+    ev = HostBatchEvaluator(spec, B)
+    opts = IPMOptions(max_iter=200)
+    bs = BatchedInteriorPoint(ev, HostBlockKKT(ev), spec.lbw, spec.ubw, opts)
+    calls = {'n': 0}
+    orig_step = bs._kkt_step
+
+    def failing_step(*args, **kw):
+        out = orig_step(*args, **kw)
+        calls['n'] += 1
+        if calls['n'] == 3:
+            ok = out[4].clone()
+            ok[1] = False
+            out = out[:4] + (ok,) + out[5:]
+        return out
+
+    bs._kkt_step = failing_step
+    res = bs.solve(W)
+    hev = HostEvaluator(spec)
+    hs = InteriorPointSolver(hev, spec.lbw, spec.ubw, hev.lbg, hev.ubg, opts)
+    hcalls = {'n': 0}
+    orig_kkt = hs._kkt
+
+    def failing_kkt(*args, **kw):
+        hcalls['n'] += 1
+        return None if hcalls['n'] == 3 else orig_kkt(*args, **kw)
+
+    hs._kkt = failing_kkt
+    ref = hs.solve(W[1])
+    assert ref.stats['restorations'] >= 1 and ref.status != 'kkt_failure'
+    assert res.status[1] == ref.status and res.status[0] != 'kkt_failure'
+    assert res.iters[1] == ref.iters
+    x = res.x.numpy()
+    assert np.abs(x[:, 1] - ref.x).max() <= 1e-6 * max(1.0, np.abs(ref.x).max())
