@@ -74,7 +74,9 @@ int ato_kkt_reserve(ato_kkt* kkt, int32_t max_batch);
 /* Factorise K for `batch` instances: instance list[i] (device int32 array; NULL = 0..batch-1)
  * is factorised into its own storage slot. H may be NULL (W = 0). inertia: device int32
  * [max_batch][3] = (positive, negative, zero) pivots, written for the listed instances.
- * Asynchronous on stream. */
+ * Asynchronous on stream: levels whose fronts fall into several kernel classes also use a
+ * second stream owned by the handle, forked from and joined into `stream` by events, so the
+ * result is ordered on `stream`. One host thread per handle. */
 int ato_kkt_factor(ato_kkt* kkt, int32_t batch, const int32_t* list, int64_t stride_elem,
                    int64_t stride_inst, const double* H, const double* J, const double* diag_x,
                    const double* diag_r, int32_t* inertia, void* stream);
