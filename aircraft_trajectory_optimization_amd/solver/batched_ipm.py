@@ -526,40 +526,11 @@ class BatchedInteriorPoint:
         dw_out = zeros.clone()
         pidx = _idx(pend)
         npass = 0
-        while len(pidx):
-            Ds_tot = Ss + delta_w
-            dr = (-delta_c).expand(m, B).clone()
-            dr[self.iin] -= 1.0 / Ds_tot
-            dx = Sx + delta_w
-            self.laps.lap('kkt_other')
-            inertia = self.kkt.factor(W, Js, dx, dr, pidx)
-            # first pass (delta_w = 0) vs the inertia-correction retries, timed apart
-            self.laps.lap('kkt_factor' if npass == 0 else 'kkt_factor_retry')
-            self.stats['factorizations'] += 1
-            fp = self.stats.setdefault('factor_passes', {})   # pass index -> [calls, instances]
-            rec = fp.setdefault(npass, [0, 0])
-            rec[0] += 1
-            rec[1] += len(pidx)
-            npass += 1
-            ok = (inertia[:, 0] == n) & (inertia[:, 1] == m) & (inertia[:, 2] == 0)
-            sing = inertia[:, 2] > 0
-            good = pend & ok & ~sing
-            gidx = _idx(good)
-            if len(gidx):
-                ry = rhs_y.clone()
-                ry[self.iin] += rhs_s / Ds_tot
-                xs = self._solve(torch.cat([rhs_x, ry]), good, W, Js, dx, dr, idx=gidx)
-                fin = torch.isfinite(xs).all(0) & self.last_solve_ok
-                sing = sing | (good & ~fin)
-                good = good & fin
-                g2 = good[None, :]
-                sol = torch.where(g2, xs, sol)
-                Ds_used = torch.where(g2, Ds_tot, Ds_used)
-                dx_used = torch.where(g2, dx, dx_used)
-                dr_used = torch.where(g2, dr, dr_used)
-                dw_out = torch.where(good, delta_w, dw_out)
-                ok_all = ok_all | good
-            bad = pend & ~good
+        tosolve = torch.zeros(B, dtype=torch.bool, device=self.dev)
+
+        def next_pass(bad, sing):
+            ''' IPOPT's perturbation update for the instances whose attempt failed '''
+            nonlocal delta_c, delta_w, first
             fst = bad & first
             delta_c = torch.where(fst & sing, o.delta_c_base * mu ** o.kappa_c, delta_c)
             dw_first = torch.where(dwl == 0, torch.full_like(dwl, o.delta_w_0),
@@ -569,8 +540,56 @@ class BatchedInteriorPoint:
             delta_w = torch.where(fst, dw_first, torch.where(bad, dw_grow, delta_w))
             first = first & ~bad
             fail = bad & (delta_w > o.delta_w_max)
-            pend = bad & ~fail
+            return bad & ~fail
+
+        # The solves are deferred until the inertia-correction passes are done: an instance whose
+        # inertia is right keeps its factors in its own storage slot while the others refactorise,
+        # so all of them are solved (and refined) in one batched call instead of one per pass. Each
+        # instance still sees factor -> solve -> (on an unrefinable solve) the next pass, exactly
+        # as before; only the order between instances changes.
+        while True:
+            while len(pidx):
+                Ds_tot = Ss + delta_w
+                dr = (-delta_c).expand(m, B).clone()
+                dr[self.iin] -= 1.0 / Ds_tot
+                dx = Sx + delta_w
+                self.laps.lap('kkt_other')
+                inertia = self.kkt.factor(W, Js, dx, dr, pidx)
+                # first pass (delta_w = 0) vs the inertia-correction retries, timed apart
+                self.laps.lap('kkt_factor' if npass == 0 else 'kkt_factor_retry')
+                self.stats['factorizations'] += 1
+                fp = self.stats.setdefault('factor_passes', {})   # pass index -> [calls, instances]
+                rec = fp.setdefault(npass, [0, 0])
+                rec[0] += 1
+                rec[1] += len(pidx)
+                npass += 1
+                ok = (inertia[:, 0] == n) & (inertia[:, 1] == m) & (inertia[:, 2] == 0)
+                sing = inertia[:, 2] > 0
+                good = pend & ok & ~sing
+                g2 = good[None, :]
+                Ds_used = torch.where(g2, Ds_tot, Ds_used)
+                dx_used = torch.where(g2, dx, dx_used)
+                dr_used = torch.where(g2, dr, dr_used)
+                dw_out = torch.where(good, delta_w, dw_out)
+                tosolve = tosolve | good
+                pend = next_pass(pend & ~good, sing)
+                pidx = _idx(pend)
+            sidx = _idx(tosolve)
+            if not len(sidx):
+                break
+            ry = rhs_y.clone()
+            ry[self.iin] += rhs_s / Ds_used
+            xs = self._solve(torch.cat([rhs_x, ry]), tosolve, W, Js, dx_used, dr_used, idx=sidx)
+            fin = torch.isfinite(xs).all(0) & self.last_solve_ok
+            okd = tosolve & fin
+            sol = torch.where(okd[None, :], xs, sol)
+            ok_all = ok_all | okd
+            bad = tosolve & ~fin                 # unrefinable solves count as singular matrices
+            tosolve = torch.zeros_like(tosolve)
+            pend = next_pass(bad, bad)
             pidx = _idx(pend)
+            if not len(pidx):
+                break
         dxs, dy = sol[:n], sol[n:]
         ds = (rhs_s + dy[self.iin]) / Ds_used
         ctx = (W, Js, dx_used, dr_used, Ds_used)
