@@ -148,13 +148,24 @@ def _fronts_nd(n, var_stage, lo, hi, j_row_ptr, j_col, split_pairs=True):
     jc = np.asarray(j_col)
     sel = link[jr] & (var_stage[jc] == hi[jr])
     anchor[jc[sel]] = True
+    # root anchors: the interval-0 variables that border rows touch (a closed line's closure rows
+    # tie node 0 to the last node). They are eliminated in the border front, so the closure rows
+    # no longer couple to leaf 0 -- its block shrinks from 182 to 166 positions on the racetrack,
+    # the size class of the other leaves -- and they reach the root as trailing positions of the
+    # leaf and of the separators on its path.
+    border_row = hi - lo > 1
+    root_anchor = np.zeros(n, bool)
+    rsel = border_row[jr] & (var_stage[jc] == 0)
+    root_anchor[jc[rsel]] = True
+    root_anchor &= ~anchor
     # interior rows whose every entry sits on anchors (e.g. a global-frame gate row on Z[n,0][:3],
     # whose position the continuity rows make anchors) have no variable inside the leaf: in the
     # leaf their own column would hold only the row diagonal (a zero pivot for an equality row,
     # i.e. a spurious singular KKT). They join the separator that owns their anchors instead.
     has_inner = np.zeros(m, bool)
-    has_inner[jr[interior[jr] & ~anchor[jc]]] = True
+    has_inner[jr[interior[jr] & ~anchor[jc] & ~root_anchor[jc]]] = True
     anchor_only = interior & ~has_inner & (lo >= 1)
+    root_only = interior & ~has_inner & (lo == 0) & root_anchor.any()    # rows on root anchors only
     own: List[np.ndarray] = []
     children: List[List[int]] = []
     # isolated pairs: an interior variable whose only Jacobian entry is in an interior row of its
@@ -170,7 +181,7 @@ def _fronts_nd(n, var_stage, lo, hi, j_row_ptr, j_col, split_pairs=True):
         for e in np.nonzero(cnt[jc] == 1)[0]:
             v, r = int(jc[e]), int(jr[e])
             st = int(var_stage[v])
-            if anchor[v] or used[r] or not (interior[r] and lo[r] == st):
+            if anchor[v] or root_anchor[v] or used[r] or root_only[r] or not (interior[r] and lo[r] == st):
                 continue
             used[r] = True
             pairs[st].append((v, r))
@@ -185,8 +196,8 @@ def _fronts_nd(n, var_stage, lo, hi, j_row_ptr, j_col, split_pairs=True):
             children.append([])
     leaf_id = []
     for st in range(S):                          # leaves
-        inner = np.concatenate([np.nonzero((var_stage == st) & ~anchor)[0],
-                                n + np.nonzero(interior & ~anchor_only & (lo == st))[0]])
+        inner = np.concatenate([np.nonzero((var_stage == st) & ~anchor & ~root_anchor)[0],
+                                n + np.nonzero(interior & ~anchor_only & ~root_only & (lo == st))[0]])
         if len(pre[st]):
             inner = inner[~np.isin(inner, pre[st])]
         leaf_id.append(len(own))
@@ -207,7 +218,7 @@ def _fronts_nd(n, var_stage, lo, hi, j_row_ptr, j_col, split_pairs=True):
         return len(own) - 1
 
     top = build(0, S - 1)
-    border = n + np.nonzero(hi - lo > 1)[0]
+    border = np.concatenate([np.nonzero(root_anchor)[0], n + np.nonzero(border_row | root_only)[0]])
     if len(border):
         own.append(border)
         children.append([top])
