@@ -1719,13 +1719,15 @@ __global__ __launch_bounds__(ST) void k_front_bwd(Plan P, int f0, int batch, con
 // per row, lanes = 64 instances (coalesced in the interleaved layout), the row's entries in
 // their fixed CSR order
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_kkt_residual(int dim, int batch, const int* __restrict__ rp,
+__global__ __launch_bounds__(256) void k_kkt_residual(int dim, int batch, const int* __restrict__ list,
+                                                      const int* __restrict__ rp,
                                                       const int* __restrict__ col, const int* __restrict__ src,
                                                       Vals V, const double* __restrict__ x,
                                                       const double* __restrict__ rhs, double* __restrict__ out) {
     const int r = __builtin_amdgcn_readfirstlane(blockIdx.y * 4 + (threadIdx.x >> 6));
-    const int b = blockIdx.x * 64 + (threadIdx.x & 63);
-    if (r >= dim || b >= batch) return;
+    const int bi = blockIdx.x * 64 + (threadIdx.x & 63);
+    if (r >= dim || bi >= batch) return;
+    const int b = list ? list[bi] : bi;
     const int e0 = rp[r], e1 = rp[r + 1];
     double acc = 0.0;
     for (int e = e0; e < e1; ++e) {
@@ -2184,7 +2186,22 @@ int ato_kkt_residual(ato_kkt* h, int32_t batch, int64_t se, int64_t sb, const do
     const Vals V{H, J, dx, dr, se, sb};
     hipStream_t st = static_cast<hipStream_t>(stream);
     hipLaunchKernelGGL(k_kkt_residual, dim3((batch + 63) / 64, (h->dim + 3) / 4), dim3(256), 0, st, h->dim, batch,
-                       h->d_kres_ptr, h->d_kres_col, h->d_kres_src, V, x, rhs, out);
+                       nullptr, h->d_kres_ptr, h->d_kres_col, h->d_kres_src, V, x, rhs, out);
+    KKT_HIP(hipGetLastError());
+    return ATO_OK;
+}
+
+int ato_kkt_residual_list(ato_kkt* h, int32_t count, const int32_t* list, int64_t se, int64_t sb, const double* H,
+                          const double* J, const double* dx, const double* dr, const double* x, const double* rhs,
+                          double* out, void* stream) {
+    if (!list) return ato_kkt_residual(h, count, se, sb, H, J, dx, dr, x, rhs, out, stream);
+    if (!h || !x || !rhs || !out || !J || !dx || !dr || count < 0) return fail(ATO_ERR_ARG, "bad argument");
+    if (count == 0) return ATO_OK;
+    if (h->dim > 4 * 65535) return fail(ATO_ERR_UNSUPPORTED, "KKT residual: dimension above 262140");
+    const Vals V{H, J, dx, dr, se, sb};
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    hipLaunchKernelGGL(k_kkt_residual, dim3((count + 63) / 64, (h->dim + 3) / 4), dim3(256), 0, st, h->dim, count,
+                       list, h->d_kres_ptr, h->d_kres_col, h->d_kres_src, V, x, rhs, out);
     KKT_HIP(hipGetLastError());
     return ATO_OK;
 }

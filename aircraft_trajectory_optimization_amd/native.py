@@ -106,7 +106,7 @@ EXPORTED_SYMBOLS = ('ato_create', 'ato_destroy', 'ato_sizes', 'ato_sparsity', 'a
                     'ato_mesh_create', 'ato_mesh_destroy', 'ato_mesh_signed_distance',
                     'ato_timing', 'ato_timing_read', 'ato_timing_stride', 'ato_last_error', 'ato_version',
                     'ato_kkt_create', 'ato_kkt_destroy', 'ato_kkt_reserve', 'ato_kkt_factor', 'ato_kkt_solve',
-                    'ato_kkt_residual') + IPM_SYMBOLS
+                    'ato_kkt_residual', 'ato_kkt_residual_list') + IPM_SYMBOLS
 
 
 def library_path() -> str:
@@ -145,8 +145,10 @@ def declare(lib: ctypes.CDLL, prefix: str = 'ato') -> ctypes.CDLL:
         lib.ato_kkt_solve.argtypes = [vp, ctypes.c_int32, vp, ctypes.c_int64, ctypes.c_int64, vp, vp]
         lib.ato_kkt_residual.argtypes = [vp, ctypes.c_int32, ctypes.c_int64, ctypes.c_int64, vp, vp, vp, vp, vp, vp,
                                          vp, vp]
+        lib.ato_kkt_residual_list.argtypes = [vp, ctypes.c_int32, vp, ctypes.c_int64, ctypes.c_int64, vp, vp, vp,
+                                              vp, vp, vp, vp, vp]
         for fn in ('ato_kkt_create', 'ato_kkt_destroy', 'ato_kkt_reserve', 'ato_kkt_factor', 'ato_kkt_solve',
-                   'ato_kkt_residual'):
+                   'ato_kkt_residual', 'ato_kkt_residual_list'):
             getattr(lib, fn).restype = ctypes.c_int
         dp, bp, d = ctypes.POINTER(AtoIpmDims), ctypes.POINTER(AtoIpmBounds), ctypes.c_double
         lib.ato_ipm_work_size.argtypes = [dp]

@@ -327,9 +327,13 @@ class BatchedInteriorPoint:
         oy = self._Jx(Js, vx) + dr * vy
         return torch.cat([ox, oy])
 
-    def _residual(self, H, Js, dx, dr, x, rhs):
-        ''' rhs - K x: the KKT backend's fused kernel (ato_kkt_residual) when it has one '''
+    def _residual(self, H, Js, dx, dr, x, rhs, idx=None):
+        ''' rhs - K x: the KKT backend's fused kernel (ato_kkt_residual) when it has one; with idx
+        and a backend that takes instance lists (ato_kkt_residual_list) only those columns are
+        computed (the others are zero), otherwise every column is '''
         if hasattr(self.kkt, 'residual'):
+            if idx is not None and getattr(self.kkt, 'residual_lists', False):
+                return self.kkt.residual(H, Js, dx, dr, x, rhs, instances=idx)
             return self.kkt.residual(H, Js, dx, dr, x, rhs)
         return rhs - self._Kmul(H, Js, dx, dr, x)
 
@@ -471,20 +475,25 @@ class BatchedInteriorPoint:
         self.laps.lap('kkt_solve')
         self.stats['solves'] += 1
         scale = rhs.abs().amax(0) + 1e-300
+        # residuals only for the columns whose x changed since the last one (comp): the others
+        # keep their last rmax, bitwise what a full residual would give them again
+        comp, ridx = mask, idx
+        rmax = torch.zeros_like(scale)
         for _ in range(10):
-            res = self._residual(H, Js, dx, dr, x, rhs)
-            rmax = res.abs().amax(0)
-            need = mask & torch.isfinite(rmax) & (rmax > 1e-10 * scale)
+            res = self._residual(H, Js, dx, dr, x, rhs, ridx)
+            rmax = torch.where(comp, res.abs().amax(0), rmax)
+            need = comp & torch.isfinite(rmax) & (rmax > 1e-10 * scale)
             if not bool(need.any()):
                 break
-            corr = res
+            nidx = _idx(need)
             self.laps.lap('kkt_refine')
-            self.kkt.solve(corr, _idx(need))
+            self.kkt.solve(res, nidx)
             self.laps.lap('kkt_solve')
             self.stats['solves'] += 1
-            x = torch.where(need[None, :], x + corr, x)
+            x = torch.where(need[None, :], x + res, x)
+            comp, ridx = need, nidx
         else:                                        # x changed after the last residual
-            rmax = self._residual(H, Js, dx, dr, x, rhs).abs().amax(0)
+            rmax = torch.where(comp, self._residual(H, Js, dx, dr, x, rhs, ridx).abs().amax(0), rmax)
         # IPOPT (residual_ratio_singular): unrefinable solves count as singular matrices
         self.last_solve_ok = torch.isfinite(rmax) & (rmax <= 1e-5 * scale)
         self.laps.lap('kkt_refine')

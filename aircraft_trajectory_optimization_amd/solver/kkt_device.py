@@ -52,6 +52,7 @@ class AtoKKTPlanDesc(ctypes.Structure):
 
 class DeviceKKT:
     ''' multifrontal Bunch-Kaufman LDL^T of the KKT matrix for a batch of instances on one device '''
+    residual_lists = True                   # residual(..., instances=) computes the listed columns only
 
     def __init__(self, plan: KKTPlan, max_batch: int, device: Optional[torch.device] = None):
         self.lib = native.load()
@@ -148,9 +149,10 @@ class DeviceKKT:
         return x
 
     def residual(self, H: Optional[torch.Tensor], J: torch.Tensor, dx: torch.Tensor, dr: torch.Tensor,
-                 x: torch.Tensor, rhs: torch.Tensor, stream=None) -> torch.Tensor:
-        ''' rhs - K x for every instance (x, rhs [dim][max_batch]); iterative-refinement residual '''
-        return _residual(self, self.cap, H, J, dx, dr, x, rhs, stream)
+                 x: torch.Tensor, rhs: torch.Tensor, stream=None, instances=None) -> torch.Tensor:
+        ''' rhs - K x for every instance, or for the listed ones (the other columns zero) (x, rhs
+        [dim][max_batch]); iterative-refinement residual '''
+        return _residual(self, self.cap, H, J, dx, dr, x, rhs, stream, instances)
 
     def fork(self) -> 'DeviceKKT':
         ''' a second factorisation with its own storage (the asynchronous restoration phase) '''
@@ -174,22 +176,35 @@ class DeviceKKT:
             pass
 
 
-def _residual(kkt, B, H, J, dx, dr, x, rhs, stream):
+def _residual(kkt, B, H, J, dx, dr, x, rhs, stream, instances=None):
     vals = [t.contiguous() for t in (J, dx, dr, x, rhs)] + ([H.contiguous()] if H is not None else [])
     for t in vals:
         if t.dtype != torch.float64 or t.dim() != 2 or t.shape[1] != B or t.device != kkt.device:
             raise ValueError('KKT residual operands must be fp64 [elements][batch] tensors on the KKT device')
     J, dx, dr, x, rhs = vals[:5]
     H = vals[5] if H is not None else None
-    out = torch.empty_like(rhs)
     st = stream if stream is not None else torch.cuda.current_stream(kkt.device)
-    kkt._check(kkt.lib.ato_kkt_residual(kkt.handle, B, B, 1, H.data_ptr() if H is not None else None, J.data_ptr(),
-                                        dx.data_ptr(), dr.data_ptr(), x.data_ptr(), rhs.data_ptr(), out.data_ptr(),
-                                        st.cuda_stream))
+    hp = H.data_ptr() if H is not None else None
+    if instances is None:
+        out = torch.empty_like(rhs)
+        kkt._check(kkt.lib.ato_kkt_residual(kkt.handle, B, B, 1, hp, J.data_ptr(), dx.data_ptr(), dr.data_ptr(),
+                                            x.data_ptr(), rhs.data_ptr(), out.data_ptr(), st.cuda_stream))
+        return out
+    # listed instances only (the refinement of the instances still above the residual ratio);
+    # the other columns are zero
+    lst, nb = kkt._list(instances, B)
+    out = torch.zeros_like(rhs)
+    if nb:
+        kkt._check(kkt.lib.ato_kkt_residual_list(kkt.handle, nb, lst.data_ptr(), B, 1, hp, J.data_ptr(),
+                                                 dx.data_ptr(), dr.data_ptr(), x.data_ptr(), rhs.data_ptr(),
+                                                 out.data_ptr(), st.cuda_stream))
+        kkt._last_res_list = lst              # alive until the asynchronous launch has read it
     return out
 
 
 class _KKTView:
+    residual_lists = True
+
     def __init__(self, base: DeviceKKT, count: int):
         if not 0 < count <= base.cap:
             raise ValueError('KKT view larger than the reserved batch')
@@ -213,8 +228,8 @@ class _KKTView:
         self._last_list = lst
         return b.inertia[:self.cap]
 
-    def residual(self, H, J, dx, dr, x, rhs, stream=None):
-        return _residual(self.base, self.cap, H, J, dx, dr, x, rhs, stream)
+    def residual(self, H, J, dx, dr, x, rhs, stream=None, instances=None):
+        return _residual(self.base, self.cap, H, J, dx, dr, x, rhs, stream, instances)
 
     def view(self, count: int) -> '_KKTView':
         return _KKTView(self.base, count)

@@ -93,6 +93,13 @@ int ato_kkt_residual(ato_kkt* kkt, int32_t batch, int64_t stride_elem, int64_t s
                      const double* H, const double* J, const double* diag_x, const double* diag_r,
                      const double* x, const double* rhs, double* out, void* stream);
 
+/* The same for the listed instances only (device int32 list of `count` instance indices; NULL =
+ * 0..count-1): iterative refinement of the instances whose residual is still above the ratio.
+ * Columns of unlisted instances in `out` are left untouched. */
+int ato_kkt_residual_list(ato_kkt* kkt, int32_t count, const int32_t* list, int64_t stride_elem,
+                          int64_t stride_inst, const double* H, const double* J, const double* diag_x,
+                          const double* diag_r, const double* x, const double* rhs, double* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

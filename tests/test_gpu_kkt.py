@@ -148,6 +148,12 @@ def test_device_kkt_residual_matches_dense(with_h):
                       ev.j_row_ptr, ev.j_col)
         ref = rhs[:, b] - K @ x[:, b]
         assert np.abs(out[:, b] - ref).max() <= 1e-12 * max(1.0, np.abs(ref).max())
+    # ato_kkt_residual_list: the listed columns bitwise as above, the others zero
+    args = (H, _dev([v[2] for v in vals]), _dev([v[3] for v in vals]), _dev([v[4] for v in vals]),
+            torch.as_tensor(x, device='cuda'), torch.as_tensor(rhs, device='cuda'))
+    part = kkt.residual(*args, instances=[2, 0]).cpu().numpy()
+    assert np.array_equal(part[:, [0, 2]], out[:, [0, 2]]) and not part[:, 1].any()
+    assert not kkt.residual(*args, instances=[]).cpu().numpy().any()
 
 
 def test_device_kkt_wide_levels_match_narrow():
