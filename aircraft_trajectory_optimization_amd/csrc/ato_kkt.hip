@@ -1855,12 +1855,14 @@ int front_class(int A, bool s16) {
     return std::max(1, (A + 31) / 32);
 }
 
-// the 16-wide-tile kernel pays off once three fronts share every CU; below that many workgroups
-// the six-tile kernel's shorter pivot steps set the time (both give the same factors bit for bit)
+// the 16-wide-tile kernel pays off once about four fronts share every CU; below that many
+// workgroups the six-tile kernel's shorter pivot steps set the time (both give the same factors
+// bit for bit). Racetrack leaves (50 per instance), factor ms six-tile / 16-wide: B = 8 0.78 / 0.80,
+// B = 16 1.08 / 1.09, B = 24 1.36 / 1.21, B = 30 1.47 / 1.30 (profiles/r03/kkt_leaf16/r03am)
 int s16_min_workgroups() {
     static const int v = [] {
         const char* e = getenv("ATO_KKT_S16_MIN");
-        return e ? atoi(e) : 6 * CUS;
+        return e ? atoi(e) : 4 * CUS;
     }();
     return v;
 }
