@@ -59,7 +59,7 @@ struct ato_kkt {
     double* d_dinv = nullptr;        // [cap][dim][3]
     int2* d_sinfo = nullptr;         // [cap][F] {steps, used stream length of the front}
     int32_t* d_spec = nullptr;       // [cap][dim] second column Bunch-Kaufman took for an own position last time
-    bool blocked = false;            // diagnostic builds (ATO_KKT_X_BLOCKED): ATO_KKT_BLOCKED=1 selects k_front_factor_blk
+    int device = 0;                  // HIP device of the handle (ato_kkt_create's current device)
 };
 
 #ifdef ATO_KKT_STAMPS
@@ -98,9 +98,6 @@ constexpr int EPT = 8;                    // entries per thread and front (<= 40
 #ifndef ATO_KKT_S16_NG
 #define ATO_KKT_S16_NG 2      // row groups of the 16-wide-tile Schur update (with tile guards: 2 groups 18.46 ms,
                               // 3: 18.22, 4: 18.57; without: 2: 13.74, 3: 14.07)
-#endif
-#ifndef ATO_KKT_X_BLOCKED
-#define ATO_KKT_X_BLOCKED 0   // DIAGNOSTIC: the blocked leaf kernel (k_front_factor_blk, rejected)
 #endif
 #ifndef ATO_KKT_CH
 #define ATO_KKT_CH 512      // 8 KB ring: B = 512 solve 3.28 -> 3.01 ms against 16 KB (64 KB: 11.1 ms); B = 1 0.37 -> 0.38 ms
@@ -507,11 +504,7 @@ __global__ __launch_bounds__(FTT) __attribute__((amdgpu_waves_per_eu(W))) void k
             cv[q] = ck[i];
             if (i < own && i != k && lvq[q]) key = max(key, mag_key(cv[q], i));
         }
-#ifdef ATO_KKT_X_NOSEARCH     // DIAGNOSTIC timing only: no pivot search (results wrong)
-        key = 0u;
-#else
         key = wave_max_u32(key);
-#endif
         KST(5);                  // column read, magnitude keys, DPP max
         const int r = key ? 511 - (int)(key & 0x1FFu) : -1;
         const double akk = lane_pick<NQ>(cv, k);
@@ -527,10 +520,6 @@ __global__ __launch_bounds__(FTT) __attribute__((amdgpu_waves_per_eu(W))) void k
             type = akk == 0.0 ? 2 : 0;
         } else if (fabs(akk) >= BK_ALPHA * lam) {
             type = 0;
-#ifdef ATO_KKT_X_NOR            // DIAGNOSTIC timing only: never the second column (results wrong)
-        } else if (true) {
-            type = 0;
-#endif
         } else {
             extract_column<T, NC>(a, r, ti, tj, cr);
             lds_barrier();
@@ -601,11 +590,7 @@ __global__ __launch_bounds__(FTT) __attribute__((amdgpu_waves_per_eu(W))) void k
         // from LDS rather than held in registers across the decision (frees the registers for a
         // second workgroup per CU).
         const double* c0p = use_r ? cr : ck;     // column p (1x1) or k (2x2)
-#ifdef ATO_KKT_X_NOSTORE      // DIAGNOSTIC timing only: no factor-column stores
-        if (false) {
-#else
         if (lvt) {
-#endif
             const int ci = cit;
             const double x0 = c0p[tid];
             if (type == 0) {
@@ -622,11 +607,7 @@ __global__ __launch_bounds__(FTT) __attribute__((amdgpu_waves_per_eu(W))) void k
         KST(3);                  // pivot inverse, record, factor-column stores
         // Schur update: one rank-1 pass (1x1 pivot) or two (2x2 pivot), A -= l c^T with c the
         // pivot column (pass 0: c0, pass 1: cr)
-#ifdef ATO_KKT_X_NOUPDATE     // DIAGNOSTIC timing only: no Schur update (results wrong)
-        const int npass = 0;
-#else
         const int npass = type == 0 ? 1 : type == 1 ? 2 : 0;
-#endif
         for (int pass = 0; pass < npass; ++pass) {
             const double* cc = pass == 1 ? cr : c0p;
             const double f0 = pass == 1 ? i01 : i00, f1 = pass == 1 ? i11 : i01;
@@ -1040,358 +1021,6 @@ size_t factor_s_lds() {
     return sizeof(double) * (16 * (NP + 1) + 4 * NP) + sizeof(int) * NP;
 }
 
-#if ATO_KKT_X_BLOCKED
-// ------------------------------------------------------------------------------------------
-// blocked factorisation (the interval leaves): the same restricted Bunch-Kaufman elimination as
-// k_front_factor_w, with the Schur update deferred over a PANEL of up to NB eliminated columns.
-//
-// Per pivot step of k_front_factor_w every thread applies a rank-1 (rank-2) update to its whole
-// register block and the next pivot column waits at a workgroup barrier for the slowest wave's
-// update: ~8000 shader cycles per step, ~20 % of them FMAs (profiles/r02s3_kkt_phase_b512.log).
-// Here the register block is updated once per panel; a pivot column is extracted stale and
-// corrected with the panel's columns, each thread for the one position it owns (thread t = position
-// t; U s = step s's multipliers, V s = its pivot column, both kept in LDS):
-//     c_i -= U s[max(i, k)] V s[min(i, k)]     for the panel's steps s, in step order,
-// which is exactly the operation sequence the per-step update applies to the stored lower-triangle
-// entry (max(i, k), min(i, k)) -- the factors, pivot records, inertia and contribution blocks are
-// bit for bit those of k_front_factor_w. The pivot search reduces each wave's positions by DPP and
-// the four wave maxima through LDS (one barrier after the column, one more when Bunch-Kaufman
-// looks at a second column). Tile columns without live positions at the panel's end are skipped:
-// their entries are never read again.
-//
-// DIAGNOSTIC, rejected (build with -DATO_KKT_X_BLOCKED=1, then ATO_KKT_BLOCKED=1 selects it):
-// measured on the 50 x 4 racetrack KKT (gpurun_out/r03d, profiles/r03/kkt_blocked_rejected.json)
-// factor B = 512 24.5 ms vs 20.3 ms, B = 64 3.57 vs 3.02 ms, B = 1 0.85 vs 0.76 ms: the per-step
-// barriers and the wave-max exchange stay on the chain, and the column corrections and panel
-// flushes add to it. Its solves also differed from k_front_factor_w by up to 0.17 on an
-// ill-conditioned random KKT (residual and inertia still correct), so the bitwise claim above
-// does not hold as built.
-// ------------------------------------------------------------------------------------------
-template <int T, int NB>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_front_factor_blk(
-    Plan P, Vals V, int f0, int batch, const int* __restrict__ list, double* __restrict__ Lst,
-    int2* __restrict__ piv, double* __restrict__ dinv, int2* __restrict__ sinfo, double* __restrict__ CB,
-    int* __restrict__ inertia) {
-    constexpr int FTT = 256;
-    constexpr int NP = 32 * T;
-    static_assert(NP <= FTT, "one position per thread");
-    constexpr int NW = (NP + 63) / 64;
-    constexpr int NS = T * (T + 1) / 2;
-    constexpr int SR = NP + 1;
-    constexpr int NTJ = FTT / 32;                // 8 column owners per tile row
-    constexpr int NC = 32 / NTJ;                 // 4 columns per thread and tile
-    constexpr int RG = (32 * SR > 2 * NB * NP) ? 32 * SR : 2 * NB * NP;
-    extern __shared__ double smem[];
-    double* strip = smem;                        // [32][SR] while assembling
-    double* Ub = smem;                           // [NB][NP] panel multipliers (after assembly)
-    double* Vb = smem + NB * NP;                 // [NB][NP] panel pivot columns
-    double* colb = smem + RG;                    // [2 parity][2 (k, r)][NP] raw extracted columns
-    double* xv = colb + 4 * NP;                  // [2 parity][2 phase][4 waves] value at the wave's argmax
-    double* xa = xv + 16;                        // [2 parity][2 phase] A_kk / A_rr
-    unsigned* xk = reinterpret_cast<unsigned*>(xa + 4);   // [2 parity][2 phase][4 waves] wave max keys
-    int* inv = reinterpret_cast<int*>(xk + 16);           // [NP] position -> child trailing index
-
-    const int f = P.forder[f0 + blockIdx.x];
-    const int bi = blockIdx.y;
-    if (bi >= batch) return;
-    const int b = list ? __builtin_amdgcn_readfirstlane(list[bi]) : bi;
-    const int tid = threadIdx.x;
-    const int ti = tid & 31, tj = tid >> 5;
-    const int lane = tid & 63, wv = tid >> 6;
-
-    const int p0 = P.pos_ptr[f];
-    const int A = P.pos_ptr[f + 1] - p0;
-    const int own = P.n_own[f];
-    double a[NS][NC];
-    double* Lb = Lst + (long long)b * P.l_size + P.l_off[f];
-    int2* pv = piv + (long long)b * P.dim + P.piv_off[f];
-    double* dv = dinv + ((long long)b * P.dim + P.piv_off[f]) * 3;
-    int npos = 0, nneg = 0, nzero = 0;
-    long long loff = 0;
-
-    // ---- original entries, assembled strip by strip (as the 256-thread k_front_factor_w)
-#pragma unroll
-    for (int I = 0; I < T; ++I) {
-        if (32 * I < A) {
-            for (int i = tid; i < 32 * SR; i += FTT) strip[i] = 0.0;
-            __syncthreads();
-            for (int e = P.ent_ptr[f * MAXT + I] + tid; e < P.ent_ptr[f * MAXT + I + 1]; e += FTT) {
-                const int2 sc = P.ent_src[e];
-                const int ep = P.ent_pos[e];
-                const double ev = src_value(V, sc.x, b) + src_value(V, sc.y, b);
-                const int pa = ep >> 16, pb = ep & 0xffff;
-                if ((pa >> 5) == I) {
-                    strip[(pa & 31) * SR + pb] = ev;
-                    if ((pb >> 5) == I && pa != pb) strip[(pb & 31) * SR + pa] = ev;
-                }
-            }
-            __syncthreads();
-#pragma unroll
-            for (int J = 0; J <= I; ++J) {
-#pragma unroll
-                for (int q = 0; q < NC; ++q) a[slot(I, J)][q] = strip[ti * SR + 32 * J + q * NTJ + tj];
-            }
-            __syncthreads();
-        } else {
-#pragma unroll
-            for (int J = 0; J <= I; ++J) {
-#pragma unroll
-                for (int q = 0; q < NC; ++q) a[slot(I, J)][q] = 0.0;
-            }
-        }
-    }
-    // ---- extend-add of the children's contribution blocks (fixed child order: deterministic)
-    for (int ci = P.child_ptr[f]; ci < P.child_ptr[f + 1]; ++ci) {
-        const int c = P.child_list[ci];
-        const int pc = P.pos_ptr[c], oc = P.n_own[c];
-        const int tqc = P.pos_ptr[c + 1] - pc - oc;
-        const int* pm = P.parent_pos + pc + oc;
-        const double* cbc = CB + (long long)b * P.cb_size + P.cb_off[c];
-        for (int i = tid; i < NP; i += FTT) inv[i] = -1;
-        __syncthreads();
-        for (int q = tid; q < tqc; q += FTT) inv[pm[q]] = q;
-        __syncthreads();
-        int qr[T];
-#pragma unroll
-        for (int I = 0; I < T; ++I) qr[I] = inv[32 * I + ti];
-#pragma unroll
-        for (int J = 0; J < T; ++J) {
-#pragma unroll
-            for (int h = 0; h < NC; ++h) {
-                const int qc = inv[32 * J + h * NTJ + tj];
-#pragma unroll
-                for (int I = J; I < T; ++I)
-                    if (qr[I] >= 0 && qc >= 0) a[slot(I, J)][h] += cbc[(long long)qr[I] * tqc + qc];
-            }
-        }
-        __syncthreads();
-    }
-
-    // column entry of this thread's position i = tid, corrected by the panel's steps (step order)
-    auto correct = [&](double c, int k, int npc) {
-        const bool hi = tid > k;
-        for (int s2 = 0; s2 < npc; ++s2) {
-            const double x = hi ? Ub[s2 * NP + tid] : Vb[s2 * NP + tid];
-            const double y = hi ? Vb[s2 * NP + k] : Ub[s2 * NP + k];
-            c = fma(-(hi ? x : y), hi ? y : x, c);
-        }
-        return c;
-    };
-    // Schur update of the register block by the panel's npc columns (step order per entry)
-    Mask<NW> live;
-    live.set_range(0, A);
-    auto flush = [&](int npc) {
-        for (int s2 = 0; s2 < npc; ++s2) {
-            double uI[T];
-#pragma unroll
-            for (int I = 0; I < T; ++I) uI[I] = Ub[s2 * NP + 32 * I + ti];
-#pragma unroll
-            for (int J = 0; J < T; ++J) {
-                if (live.any_in_tile(J)) {
-                    double vj[NC];
-#pragma unroll
-                    for (int h = 0; h < NC; ++h) vj[h] = Vb[s2 * NP + 32 * J + h * NTJ + tj];
-#pragma unroll
-                    for (int I = J; I < T; ++I) {
-#pragma unroll
-                        for (int h = 0; h < NC; ++h) a[slot(I, J)][h] = fma(-uI[I], vj[h], a[slot(I, J)][h]);
-                    }
-                }
-            }
-        }
-    };
-    // wave max of the keys, the value at the wave's argmax, exchanged through LDS
-    auto wave_exchange = [&](double c, unsigned key, int par, int ph) {
-        const unsigned wkey = wave_max_u32(key);
-        const double wval = wkey ? readlane_f64(c, (511 - (int)(wkey & 0x1FFu)) & 63) : 0.0;
-        if (lane == 0) {
-            xk[(par * 2 + ph) * 4 + wv] = wkey;
-            xv[(par * 2 + ph) * 4 + wv] = wval;
-        }
-    };
-    auto exchange_result = [&](int par, int ph, double& val) {
-        unsigned best = 0u;
-        double bv = 0.0;
-#pragma unroll
-        for (int w2 = 0; w2 < 4; ++w2) {
-            const unsigned kk = xk[(par * 2 + ph) * 4 + w2];
-            const double vv = xv[(par * 2 + ph) * 4 + w2];
-            if (kk > best) {
-                best = kk;
-                bv = vv;
-            }
-        }
-        val = bv;
-        return best;
-    };
-
-    // ---- restricted Bunch-Kaufman elimination of the own positions
-    bool lvt = tid < A;           // this thread's position live ...
-    int cit = tid;                // ... and its index among the live positions
-    int kc = 0, steps = 0, par = 0, npc = 0;
-    while (true) {
-        while (kc < own && !live.get(kc)) ++kc;
-        if (kc >= own) break;
-        const int k = kc;
-        double* ck = colb + (par * 2 + 0) * NP;
-        double* cr = colb + (par * 2 + 1) * NP;
-        extract_column<T, NC>(a, k, ti, tj, ck);
-        lds_barrier();
-        const double cv = tid < NP ? correct(ck[tid < NP ? tid : 0], k, npc) : 0.0;
-        wave_exchange(cv, (tid < own && tid != k && lvt) ? mag_key(cv, tid) : 0u, par, 0);
-        {
-            const double akk_w = readlane_f64(cv, k & 63);      // wave-uniform; the owner wave's is A_kk
-            if (wv == (k >> 6) && lane == 0) xa[par * 2 + 0] = akk_w;
-        }
-        lds_barrier();
-        double ark;
-        const unsigned key = exchange_result(par, 0, ark);
-        const int r = key ? 511 - (int)(key & 0x1FFu) : -1;
-        const double akk = xa[par * 2 + 0];
-        const double lam = r >= 0 ? fabs(ark) : 0.0;
-        int type;                 // 0: 1x1 at p, 1: 2x2 (k, r), 2: zero column
-        double arr = 0.0;
-        double cw = 0.0;          // this thread's entry of column r (when extracted)
-        int p = k;
-        bool use_r = false;
-        if (r < 0 || lam == 0.0) {
-            type = akk == 0.0 ? 2 : 0;
-        } else if (fabs(akk) >= BK_ALPHA * lam) {
-            type = 0;
-        } else {
-            extract_column<T, NC>(a, r, ti, tj, cr);
-            lds_barrier();
-            cw = tid < NP ? correct(cr[tid < NP ? tid : 0], r, npc) : 0.0;
-            wave_exchange(cw, (tid < own && tid != r && lvt) ? mag_key(cw, tid) : 0u, par, 1);
-            {
-                const double arr_w = readlane_f64(cw, r & 63);
-                if (wv == (r >> 6) && lane == 0) xa[par * 2 + 1] = arr_w;
-            }
-            lds_barrier();
-            double sv;
-            const unsigned key2 = exchange_result(par, 1, sv);
-            const double sig = key2 ? fabs(sv) : 0.0;
-            arr = xa[par * 2 + 1];
-            if (fabs(akk) * sig >= BK_ALPHA * lam * lam) {
-                type = 0;
-            } else if (fabs(arr) >= BK_ALPHA * sig) {
-                type = 0;
-                p = r;
-                use_r = true;
-            } else {
-                type = 1;
-            }
-        }
-        // ---- pivot inverse, inertia
-        double i00 = 0.0, i01 = 0.0, i11 = 0.0;
-        if (type == 2) {
-            live.clear(k);
-            ++nzero;
-        } else if (type == 0) {
-            const double d = use_r ? arr : akk;
-            i00 = rcp_nr(d);
-            live.clear(p);
-            if (d > 0.0) ++npos; else ++nneg;
-        } else {
-            const double A00 = akk, A01 = ark, A11 = arr;
-            const double det = A00 * A11 - A01 * A01;
-            const double rdet = rcp_nr(det);
-            i00 = A11 * rdet;
-            i01 = -A01 * rdet;
-            i11 = A00 * rdet;
-            live.clear(k);
-            live.clear(r);
-            if (det < 0.0) { ++npos; ++nneg; }
-            else if (A00 + A11 > 0.0) npos += 2;
-            else nneg += 2;
-        }
-        const int nlive = live.count();
-        const int ncol = type == 1 ? 2 : 1;
-        {
-            const int e1p = type == 1 ? k : (type == 2 ? k : p);
-            const int e2p = type == 1 ? r : -1;
-            lvt = lvt && tid != e1p && tid != e2p;
-            cit -= (tid > e1p ? 1 : 0) + (e2p >= 0 && tid > e2p ? 1 : 0);
-        }
-        if (tid == 0) {
-            pv[steps] = make_int2((type == 1 ? k : p) | (type << 16), type == 1 ? r : -1);
-            dv[3 * steps + 0] = i00;
-            dv[3 * steps + 1] = i01;
-            dv[3 * steps + 2] = i11;
-        }
-        // ---- this step's multipliers / pivot columns into the panel, factor column(s) to HBM
-        const double x0 = use_r ? cw : cv;       // column p (1x1) or k (2x2)
-        if (tid < NP) {
-            if (type == 0) {
-                Ub[npc * NP + tid] = x0 * i00;
-                Vb[npc * NP + tid] = x0;
-            } else if (type == 1) {
-                Ub[npc * NP + tid] = fma(x0, i00, cw * i01);
-                Vb[npc * NP + tid] = x0;
-                Ub[(npc + 1) * NP + tid] = fma(x0, i01, cw * i11);
-                Vb[(npc + 1) * NP + tid] = cw;
-            }
-        }
-        if (lvt) {
-            const int ci = cit;
-            if (type == 0) {
-                Lb[loff + ci] = x0 * i00;
-            } else if (type == 1) {
-                Lb[loff + 2 * ci] = fma(x0, i00, cw * i01);
-                Lb[loff + 2 * ci + 1] = fma(x0, i01, cw * i11);
-            } else {
-                Lb[loff + ci] = 0.0;
-            }
-        }
-        loff += (long long)nlive * ncol;
-        npc += type == 0 ? 1 : type == 1 ? 2 : 0;
-        ++steps;
-        par ^= 1;
-        if (npc > NB - 2) {       // the panel is full (room for a 2x2 kept): update the block
-            lds_barrier();
-            flush(npc);
-            npc = 0;
-        }
-    }
-    if (npc > 0) {
-        lds_barrier();
-        flush(npc);
-    }
-    if (tid == 0) {
-        sinfo[(long long)b * P.F + f] = make_int2(steps, (int)loff);
-        atomicAdd(&inertia[3 * b + 0], npos);
-        atomicAdd(&inertia[3 * b + 1], nneg);
-        atomicAdd(&inertia[3 * b + 2], nzero);
-    }
-    // ---- trailing Schur complement -> contribution block of the parent (HBM)
-    const int tq = A - own;
-    if (tq > 0) {
-        double* cb = CB + (long long)b * P.cb_size + P.cb_off[f];
-#pragma unroll
-        for (int I = 0; I < T; ++I) {
-#pragma unroll
-            for (int J = 0; J <= I; ++J) {
-#pragma unroll
-                for (int h = 0; h < NC; ++h) {
-                    const int i = 32 * I + ti, j = 32 * J + h * NTJ + tj;
-                    if (i >= own && i < A && j >= own && j < A && (I != J || i >= j)) {
-                        cb[(long long)(i - own) * tq + (j - own)] = a[slot(I, J)][h];
-                        cb[(long long)(j - own) * tq + (i - own)] = a[slot(I, J)][h];
-                    }
-                }
-            }
-        }
-    }
-}
-
-template <int T, int NB>
-size_t factor_blk_lds() {
-    constexpr int NP = 32 * T;
-    constexpr int SR = NP + 1;
-    constexpr int RG = (32 * SR > 2 * NB * NP) ? 32 * SR : 2 * NB * NP;
-    return sizeof(double) * (RG + 4 * NP + 16 + 4) + sizeof(unsigned) * 16 + sizeof(int) * NP;
-}
-#endif  // ATO_KKT_X_BLOCKED
 
 // ------------------------------------------------------------------------------------------
 // solve
@@ -1771,16 +1400,6 @@ int launch_factor_level(const ato_kkt* h, const Plan& P, const Vals& V, int f0, 
                                f0, batch, list, h->d_L, h->d_piv, h->d_dinv, h->d_sinfo, h->d_cb, inertia,
                                h->d_spec);
     }
-#if ATO_KKT_X_BLOCKED
-    // Six-tile fronts: the blocked diagnostic kernel (panel of 16 columns)
-    if constexpr (T == 6) {
-        if (!one_wave && h->blocked) {
-            hipLaunchKernelGGL((k_front_factor_blk<T, 16>), dim3(nf, batch), dim3(256), (factor_blk_lds<T, 16>()), st, P,
-                               V, f0, batch, list, h->d_L, h->d_piv, h->d_dinv, h->d_sinfo, h->d_cb, inertia);
-            one_wave = true;
-        }
-    }
-#endif
 #if ATO_KKT_LEAF_FTT == 256
     // Six-tile fronts (the interval leaves): 256 threads, one wave per SIMD, four columns per thread
     // and tile (about 220 VGPRs). Every wave runs the pivot search and decision, so four waves do
@@ -1903,9 +1522,15 @@ int factor_level(ato_kkt* h, const Plan& P, const Vals& V, int l, int batch, con
         return launch_segment(h, P, V, ato_kkt::Seg{h->level_ptr[l], nfl, h->level_tiles[l]}, batch, list, inertia, st);
     if (sg.size() == 1) return launch_segment(h, P, V, sg[0], batch, list, inertia, st);
     if (!h->side) {
-        KKT_HIP(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
-        KKT_HIP(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
-        KKT_HIP(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
+        // created on the handle's device, whatever device is current on the calling thread
+        int cur = 0;
+        KKT_HIP(hipGetDevice(&cur));
+        if (cur != h->device) KKT_HIP(hipSetDevice(h->device));
+        const hipError_t e1 = hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking);
+        const hipError_t e2 = e1 == hipSuccess ? hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming) : e1;
+        const hipError_t e3 = e2 == hipSuccess ? hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming) : e2;
+        if (cur != h->device) KKT_HIP(hipSetDevice(cur));
+        KKT_HIP(e3);
     }
     KKT_HIP(hipEventRecord(h->ev_fork, st));
     KKT_HIP(hipStreamWaitEvent(h->side, h->ev_fork, 0));
@@ -2006,6 +1631,10 @@ int ato_kkt_create(const ato_kkt_plan_desc* d, ato_kkt** out) {
     const int F = d->n_fronts, L = d->n_levels;
     if (d->level_ptr[0] != 0 || d->level_ptr[L] != F) return fail(ATO_ERR_ARG, "KKT plan: levels do not cover the fronts");
     ato_kkt* h = new ato_kkt();
+    if (hipGetDevice(&h->device) != hipSuccess) {
+        delete h;
+        return fail(ATO_ERR_HIP, "hipGetDevice failed");
+    }
     h->n = d->n;
     h->m = d->m;
     h->dim = d->n + d->m;
@@ -2014,10 +1643,6 @@ int ato_kkt_create(const ato_kkt_plan_desc* d, ato_kkt** out) {
     h->l_size = d->l_size;
     h->cb_size = d->cb_size;
     h->sc_size = d->sc_size;
-    if (ATO_KKT_X_BLOCKED) {
-        const char* env = getenv("ATO_KKT_BLOCKED");
-        h->blocked = env && env[0] == '1';
-    }
     h->level_ptr.assign(d->level_ptr, d->level_ptr + L + 1);
     h->level_tiles.assign(d->level_tiles, d->level_tiles + L);
     const int P = d->pos_ptr[F];

@@ -43,8 +43,11 @@ def solve_records(spec: ProblemSpec, res, solver) -> torch.Tensor:
     code = {v: k for k, v in STATUS_NAMES.items()}
     x = res.x
     lap = x[:spec.N].sum(0)
+    fe0 = getattr(solver, 'final_e0', None)
     hist = getattr(solver, 'history', None)
-    if hist is not None and len(hist):
+    if fe0 is not None:
+        e0 = torch.as_tensor(np.asarray(fe0, np.float64), device=x.device)
+    elif hist is not None and len(hist):
         e0 = torch.as_tensor(hist[-1][4], dtype=torch.float64, device=x.device)
     else:
         e0 = torch.full_like(lap, float('nan'))

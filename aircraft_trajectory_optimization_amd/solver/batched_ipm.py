@@ -706,6 +706,7 @@ class BatchedInteriorPoint:
                'iters': torch.zeros(B0, dtype=torch.long, device=dev),
                'n_resto': torch.zeros(B0, dtype=torch.long, device=dev)}
         hist_row = torch.zeros((6, B0), dtype=torch.float64, device=dev)
+        e0_stale = torch.zeros(B0, dtype=torch.bool, device=dev)   # x moved after the last history row
         # ---- asynchronous restoration: a restoration phase runs in a worker thread on its own
         # stream, library handle and KKT storage while the other columns keep iterating; its
         # columns wait (frozen) until it is collected. Waiting does not change an instance's own
@@ -1014,10 +1015,15 @@ class BatchedInteriorPoint:
                     act = act | okr
                 laps.lap('resto_post')
 
+        else:
+            # the lockstep bound ended the loop: the columns that stepped in its last iteration moved
+            # after their last history row
+            e0_stale[cols[stepping]] = True
         if on_iteration is not None:
             on_iteration(it, -1)
         for j in inflight:                           # (the lockstep bound ended the loop first)
             R, xr, okr = self._resto_collect(j, cols, x, B0)
+            e0_stale[cols[R]] = True
             # the phase finished after the last lockstep iteration: restored columns keep their
             # restored point, but none of them iterated again (MAX_ITER); failed ones LS_FAILED
             x = torch.where((R & okr)[None, :], xr, x)
@@ -1038,6 +1044,8 @@ class BatchedInteriorPoint:
         st = out['status'].cpu().numpy()
         # [lockstep iteration][f, inf_pr, inf_du, mu, E0, restorations so far][instance]
         self.history = torch.stack(history).cpu().numpy() if history else np.zeros((0, 6, B0))
+        # E0 of every instance at its returned point (NaN where the point moved after the last row)
+        self.final_e0 = np.where(e0_stale.cpu().numpy(), np.nan, self.history[-1][4] if len(history) else np.nan)
         if laps.on:
             self.stats['laps'] = dict(laps.t)
             if stop_check is None:

@@ -130,6 +130,7 @@ class DeviceKKT:
         self._keep_vals = (H, J, dx, dr)      # alive until the (asynchronous) factorisation has read them
         lst, nb = self._list(instances)
         st = stream if stream is not None else torch.cuda.current_stream(self.device)
+        _on_stream(lst, st)
         self._check(self.lib.ato_kkt_factor(self.handle, nb, lst.data_ptr() if lst is not None else None, B, 1,
                                             H.data_ptr() if H is not None else None, J.data_ptr(), dx.data_ptr(),
                                             dr.data_ptr(), self.inertia.data_ptr(), st.cuda_stream))
@@ -143,6 +144,7 @@ class DeviceKKT:
             raise ValueError('x must be a contiguous fp64 [dim][max_batch] tensor on the KKT device')
         lst, nb = self._list(instances)
         st = stream if stream is not None else torch.cuda.current_stream(self.device)
+        _on_stream(lst, st)
         self._check(self.lib.ato_kkt_solve(self.handle, nb, lst.data_ptr() if lst is not None else None, self.cap, 1,
                                            x.data_ptr(), st.cuda_stream))
         self._last_list = lst
@@ -176,6 +178,13 @@ class DeviceKKT:
             pass
 
 
+def _on_stream(lst, st):
+    ''' an instance list allocated on the current stream but read by a launch on another one: tell
+    the caching allocator, so its memory is not reused before that launch has read it '''
+    if lst is not None and st != torch.cuda.current_stream(lst.device):
+        lst.record_stream(st)
+
+
 def _residual(kkt, B, H, J, dx, dr, x, rhs, stream, instances=None):
     vals = [t.contiguous() for t in (J, dx, dr, x, rhs)] + ([H.contiguous()] if H is not None else [])
     for t in vals:
@@ -195,6 +204,7 @@ def _residual(kkt, B, H, J, dx, dr, x, rhs, stream, instances=None):
     lst, nb = kkt._list(instances, B)
     out = torch.zeros_like(rhs)
     if nb:
+        _on_stream(lst, st)
         kkt._check(kkt.lib.ato_kkt_residual_list(kkt.handle, nb, lst.data_ptr(), B, 1, hp, J.data_ptr(),
                                                  dx.data_ptr(), dr.data_ptr(), x.data_ptr(), rhs.data_ptr(),
                                                  out.data_ptr(), st.cuda_stream))
@@ -222,6 +232,7 @@ class _KKTView:
         if instances is None:
             nb = self.cap
         st = stream if stream is not None else torch.cuda.current_stream(self.device)
+        _on_stream(lst, st)
         b._check(b.lib.ato_kkt_factor(b.handle, nb, lst.data_ptr() if lst is not None else None, self.cap, 1,
                                       H.data_ptr() if H is not None else None, J.data_ptr(), dx.data_ptr(),
                                       dr.data_ptr(), b.inertia.data_ptr(), st.cuda_stream))
@@ -243,6 +254,7 @@ class _KKTView:
         if instances is None:
             nb = self.cap
         st = stream if stream is not None else torch.cuda.current_stream(self.device)
+        _on_stream(lst, st)
         b._check(b.lib.ato_kkt_solve(b.handle, nb, lst.data_ptr() if lst is not None else None, self.cap, 1,
                                      x.data_ptr(), st.cuda_stream))
         self._last_list = lst

@@ -86,6 +86,11 @@ for s in $STEPS; do
                    ATO_LIB_PATH=$lp run solve_$v 600 python tools/solve_batched.py --batch 512 --max-iter 200 --no-host --out "$OUT/solve_$v.json"
                    cp "$OUT/solve_$v.json" "$OUT/solve_${v}_$(date +%s).json"
                done ;;
+        s16ab) i=0
+               for v in 1536 1024 1536 1024; do
+                   i=$((i+1))
+                   ATO_KKT_S16_MIN=$v run solve_s16min${v}_$i 600 python tools/solve_batched.py --batch 512 --max-iter 200 --cold --no-host --out "$OUT/solve_s16min${v}_$i.json"
+               done ;;
         listpmc) run listpmc 120 rocprofv3 -L ;;
         mb)    run mb_store 120 ./tools/mb_store ;;
         mbpmc) run mb_fetch 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/mb_fetch" -o run -- ./tools/mb_store
