@@ -18,7 +18,7 @@ CSRC = os.path.join(PKG, 'csrc')
 OUT = os.path.join(PKG, '_lib')
 OBJ = os.path.join(PKG, '_lib', 'obj')
 LIB = os.path.join(OUT, 'libato.so')
-N_INST = 9
+N_INST = 12
 ARCH = os.environ.get('ATO_OFFLOAD_ARCH', 'gfx950')
 FLAGS = ['-std=c++20', '-O3', f'--offload-arch={ARCH}', '-fPIC', '-I', os.path.join(REPO, 'include')]
 

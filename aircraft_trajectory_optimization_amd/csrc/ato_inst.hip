@@ -1,5 +1,5 @@
 // ato_inst.hip -- explicit instantiation of the evaluation launchers for ONE model variant.
-// Compiled once per variant with -DATO_INST=<0..8> (see build_native.py).
+// Compiled once per variant with -DATO_INST=<0..11> (see build_native.py).
 #define ATO_DEFINE_LAUNCHERS
 #include "ato_kernels.hpp"
 
@@ -26,6 +26,12 @@ using Model = PointModel<GLOBAL>;
 using Model = PointModel<PARAM_GR>;
 #elif ATO_INST == 8
 using Model = PointModel<PARAM_REL>;
+#elif ATO_INST == 9
+using Model = DroneModel<DCM, GLOBAL>;
+#elif ATO_INST == 10
+using Model = DroneModel<DCM, PARAM_GR>;
+#elif ATO_INST == 11
+using Model = DroneModel<DCM, PARAM_REL>;
 #endif
 template hipError_t launch_eval<Model, double>(const ProbD&, int, int, const double*, double*, double*, double*,
                                               double*, double*, hipStream_t, hipEvent_t*);

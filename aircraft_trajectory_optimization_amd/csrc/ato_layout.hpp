@@ -73,6 +73,10 @@ bool with_model(const ProbD& p, F&& f) {
             if (p.frame == GLOBAL) { f.template operator()<DroneModel<YPR, GLOBAL>>(); return true; }
             if (p.frame == PARAM_GR) { f.template operator()<DroneModel<YPR, PARAM_GR>>(); return true; }
             if (p.frame == PARAM_REL) { f.template operator()<DroneModel<YPR, PARAM_REL>>(); return true; }
+        } else if (p.att == ATO_ATT_DCM) {
+            if (p.frame == GLOBAL) { f.template operator()<DroneModel<DCM, GLOBAL>>(); return true; }
+            if (p.frame == PARAM_GR) { f.template operator()<DroneModel<DCM, PARAM_GR>>(); return true; }
+            if (p.frame == PARAM_REL) { f.template operator()<DroneModel<DCM, PARAM_REL>>(); return true; }
         }
     } else if (p.model == ATO_MODEL_POINT) {
         if (p.frame == GLOBAL) { f.template operator()<PointModel<GLOBAL>>(); return true; }
@@ -299,7 +303,7 @@ struct Layout {
         p.K1 = d.K + 1;
         p.P = d.N * (d.K + 1);
         if (d.model == ATO_MODEL_DRONE) {
-            nz = d.attitude == ATO_ATT_ESP ? 13 : 12;
+            nz = d.attitude == ATO_ATT_ESP ? 13 : (d.attitude == ATO_ATT_DCM ? 18 : 12);
             nu = 4;
         } else if (d.model == ATO_MODEL_POINT) {
             nz = 6;
@@ -307,7 +311,8 @@ struct Layout {
         } else {
             return "unknown model";
         }
-        if (d.model == ATO_MODEL_DRONE && d.attitude != ATO_ATT_ESP && d.attitude != ATO_ATT_YPR)
+        if (d.model == ATO_MODEL_DRONE && d.attitude != ATO_ATT_ESP && d.attitude != ATO_ATT_YPR &&
+            d.attitude != ATO_ATT_DCM)
             return "unknown attitude parameterisation";
         p.NZ = nz;
         p.NU = nu;

@@ -25,7 +25,7 @@
 
 namespace ato {
 
-enum Att { ESP = 0, YPR = 1 };
+enum Att { ESP = 0, YPR = 1, DCM = 2 };
 enum Frame { GLOBAL = 0, PARAM_GR = 1, PARAM_REL = 2 };
 
 template <class T>
@@ -174,12 +174,58 @@ struct AttYPR {
     }
 };
 
+// Direction-cosine matrix (config 5's "Non-Euclidean DCM / SO(3) pose"; not in the reference, whose
+// rotations.py:19-24 offers ESP and YPR only): the attitude state IS R, row-major (r_{3i+j} = R_ij),
+// with the kinematics R' = R [w]x. R(r) is the identity map, so every force / pose term the ESP
+// model builds from R(q) is reused unchanged. Orthonormality is carried by the continuity operator
+// (ato_program.hpp AttOp: the analogue of the reference's quaternion normalisation).
+struct AttDCM {
+    static constexpr int NR = 9;
+
+    template <class T>
+    ATO_HD static void R(const T* r, T* Rm) {
+        for (int i = 0; i < 9; ++i) Rm[i] = r[i];
+    }
+
+    template <class T>
+    ATO_HD static void dR(const T*, const T*, int m, T* out) {
+        for (int i = 0; i < 9; ++i) out[i] = T(i == m ? 1 : 0);
+    }
+
+    // (R [w]x)_i0 = R_i1 w2 - R_i2 w1, _i1 = R_i2 w0 - R_i0 w2, _i2 = R_i0 w1 - R_i1 w0
+    template <class T>
+    ATO_HD static void kin(const T* r, const T* w, T* rdot, T drq[9][9], T Mm[9][3]) {
+        for (int a = 0; a < 9; ++a) {
+            for (int m = 0; m < 9; ++m) drq[a][m] = T(0);
+            for (int c = 0; c < 3; ++c) Mm[a][c] = T(0);
+        }
+        for (int i = 0; i < 3; ++i) {
+            const T r0 = r[3 * i], r1 = r[3 * i + 1], r2 = r[3 * i + 2];
+            rdot[3 * i + 0] = r1 * w[2] - r2 * w[1];
+            rdot[3 * i + 1] = r2 * w[0] - r0 * w[2];
+            rdot[3 * i + 2] = r0 * w[1] - r1 * w[0];
+            drq[3 * i + 0][3 * i + 1] = w[2];  drq[3 * i + 0][3 * i + 2] = -w[1];
+            drq[3 * i + 1][3 * i + 2] = w[0];  drq[3 * i + 1][3 * i + 0] = -w[2];
+            drq[3 * i + 2][3 * i + 0] = w[1];  drq[3 * i + 2][3 * i + 1] = -w[0];
+            Mm[3 * i + 0][2] = r1;  Mm[3 * i + 0][1] = -r2;
+            Mm[3 * i + 1][0] = r2;  Mm[3 * i + 1][2] = -r0;
+            Mm[3 * i + 2][1] = r0;  Mm[3 * i + 2][0] = -r1;
+        }
+    }
+
+    static constexpr bool kin_r(int i, int m) { return m / 3 == i / 3 && m != i; }
+    static constexpr bool kin_w(int i, int c) { return c != i % 3; }
+    static constexpr bool R_dep(int row, int col, int m) { return m == row * 3 + col; }
+};
+
 template <int A>
 struct AttSel;
 template <>
 struct AttSel<ESP> { using type = AttESP; };
 template <>
 struct AttSel<YPR> { using type = AttYPR; };
+template <>
+struct AttSel<DCM> { using type = AttDCM; };
 
 // --------------------------------------------------------------------- drone
 // z = [p(3), r(NR), v_b(3), w_b(3)], u = 4 rotor thrusts.
@@ -192,6 +238,7 @@ struct DroneModel {
     static constexpr bool PARAM = FRAME != GLOBAL;
     static constexpr bool IS_DRONE = true;
     static constexpr bool HAS_QUAT = ATT == ESP;
+    static constexpr bool HAS_DCM = ATT == DCM;
 
     // d(row of global R used for gravity, i.e. R_g[2][c]) / d r_m
     static constexpr bool grav_dep(int c, int m) {
@@ -478,6 +525,7 @@ struct PointModel {
     static constexpr bool PARAM = FRAME != GLOBAL;
     static constexpr bool IS_DRONE = false;
     static constexpr bool HAS_QUAT = false;
+    static constexpr bool HAS_DCM = false;
 
     static constexpr bool zmask(int i, int m) {
         if (i < 3) return PARAM ? (m == 1 || m == 2 || m >= 3) : (m == 3 + i);

@@ -238,6 +238,65 @@ ATO_HD void qnormalize(const T* q, T* qh, T& inv_norm) {
     for (int i = 0; i < 4; ++i) qh[i] = q[i] / nq;
 }
 
+// The continuity operator on the attitude components (applied to the extrapolated interval end
+// state in continuity rows, closures and open-line terminal rows):
+//   ESP (NO = 4): q / |q|                               drone_raceline.py:42-45
+//   DCM (NO = 9): one Newton-Schulz step towards SO(3),  P(R) = R (3 I - R^T R) / 2
+//                 (build-side: the reference has no DCM pose). P is the identity on SO(3) and
+//                 contracts the orthonormality error quadratically, so the Gauss-Legendre
+//                 collocation, which conserves R^T R inside an interval, keeps every interval on
+//                 SO(3) -- the analogue of the quaternion's normalisation, with no extra rows.
+//   others (NO = 0): the identity.
+// v[a] = op(r)_a, jac(a, m) = d op(r)_a / d r_m (every (a, m) is structural).
+template <class M, class T, int KIND = M::HAS_QUAT ? 1 : (M::HAS_DCM ? 2 : 0)>
+struct AttOp {
+    static constexpr int NO = 0;
+    T v[1];
+    ATO_HD void apply(const T*) {}
+    ATO_HD T jac(int, int) const { return T(0); }
+};
+
+template <class M, class T>
+struct AttOp<M, T, 1> {
+    static constexpr int NO = 4;
+    T v[4], iq;
+    ATO_HD void apply(const T* q) { qnormalize(q, v, iq); }
+    ATO_HD T jac(int a, int m) const { return ((a == m ? T(1) : T(0)) - v[a] * v[m]) * iq; }
+};
+
+template <class M, class T>
+struct AttOp<M, T, 2> {
+    static constexpr int NO = 9;
+    T v[9], R[9], S[9], RR[9];     // S = R^T R, RR = R R^T
+    ATO_HD void apply(const T* r) {
+#pragma unroll
+        for (int i = 0; i < 9; ++i) R[i] = r[i];
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                S[i * 3 + j] = R[i] * R[j] + R[3 + i] * R[3 + j] + R[6 + i] * R[6 + j];
+                RR[i * 3 + j] = R[3 * i] * R[3 * j] + R[3 * i + 1] * R[3 * j + 1] + R[3 * i + 2] * R[3 * j + 2];
+            }
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j)
+                v[i * 3 + j] = T(1.5) * R[i * 3 + j] -
+                               T(0.5) * (R[i * 3] * S[j] + R[i * 3 + 1] * S[3 + j] + R[i * 3 + 2] * S[6 + j]);
+    }
+    // d P_ij / d R_ab = 3/2 d_ia d_jb - 1/2 (d_ia S_bj + R_ib R_aj + RR_ia d_jb)
+    ATO_HD T jac(int ij, int ab) const {
+        const int i = ij / 3, j = ij % 3, a = ab / 3, b = ab % 3;
+        T acc = R[i * 3 + b] * R[a * 3 + j];
+        if (i == a) acc += S[b * 3 + j];
+        if (j == b) acc += RR[i * 3 + a];
+        T out = T(-0.5) * acc;
+        if (i == a && j == b) out += T(1.5);
+        return out;
+    }
+};
+
 // continuity into interval n >= 1 (base_raceline.py:474-490, parametric :1149-1163)
 template <class M, class T, int KS, class W, class S>
 ATO_HD void seg_cont(const ProbD& p, int n, const W& w, S& s) {
@@ -257,22 +316,23 @@ ATO_HD void seg_cont(const ProbD& p, int n, const W& w, S& s) {
 #pragma unroll
         for (int i = 0; i < NU; ++i) ub[i] += w(c.u(n - 1, k, i)) * dk;
     }
-    T qh[4] = {T(0), T(0), T(0), T(0)}, iq = T(0);
-    if (M::HAS_QUAT) qnormalize(zb + IR, qh, iq);
+    using Op = AttOp<M, T>;
+    constexpr int NO = Op::NO;
+    Op op;
+    if constexpr (NO > 0) op.apply(zb + IR);
 #pragma unroll
     for (int i = (M::PARAM ? 1 : 0); i < NZ; ++i) {
-        const bool isq = M::HAS_QUAT && i >= IR && i < IR + 4;
+        const bool isq = NO > 0 && i >= IR && i < IR + NO;
         if (isq) {
             const int a = i - IR;
 #pragma unroll
             for (int k = 0; k < K1; ++k) {
                 const T dk = T(p.D[k]);
 #pragma unroll
-                for (int m = 0; m < 4; ++m)
-                    s.jac(c.z(n - 1, k, IR + m), -dk * ((a == m ? T(1) : T(0)) - qh[a] * qh[m]) * iq);
+                for (int m = 0; m < NO; ++m) s.jac(c.z(n - 1, k, IR + m), -dk * op.jac(a, m));
             }
             s.jac(c.z(n, 0, i), T(1));
-            s.row(w(c.z(n, 0, i)) - qh[a], 0.0, 0.0);
+            s.row(w(c.z(n, 0, i)) - op.v[a], 0.0, 0.0);
         } else {
             for (int k = 0; k < K1; ++k) s.jac(c.z(n - 1, k, i), -T(p.D[k]));
             s.jac(c.z(n, 0, i), T(1));
@@ -419,8 +479,10 @@ ATO_HD void seg_drone_closure(const ProbD& p, const W& w, S& s) {
 #pragma unroll
         for (int i = 0; i < NU; ++i) ub[i] += w(c.u(nl, k, i)) * dk;
     }
-    T qh[4] = {T(0), T(0), T(0), T(0)}, iq = T(0);
-    if (M::HAS_QUAT) qnormalize(zb + IR, qh, iq);
+    using Op = AttOp<M, T>;
+    constexpr int NO = Op::NO;
+    Op op;
+    if constexpr (NO > 0) op.apply(zb + IR);
     // uF - u0
 #pragma unroll
     for (int i = 0; i < NU; ++i) {
@@ -435,22 +497,23 @@ ATO_HD void seg_drone_closure(const ProbD& p, const W& w, S& s) {
     };
     plain(1, T(0));
     plain(2, T(0));
-    // z_delta[7:] (ESP) or z_delta[4:] (YPR): everything after the first attitude slot(s)
-    const int first_after = M::HAS_QUAT ? IR + 4 : IR + 1;
+    // z_delta[7:] (ESP), z_delta[12:] (DCM) or z_delta[4:] (YPR): everything after the first
+    // attitude slot(s)
+    const int first_after = NO > 0 ? IR + NO : IR + 1;
     for (int i = first_after; i < NZ; ++i) plain(i, T(0));
-    if (M::HAS_QUAT) {
-        const T sgn = p.quat_flip ? T(1) : T(-1);
+    if constexpr (NO > 0) {
+        // ESP: op(q_F) -/+ q_0 (the sign of the warm start's branch); DCM: op(R_F) - R_0
+        const T sgn = (M::HAS_QUAT && p.quat_flip) ? T(1) : T(-1);
 #pragma unroll
-        for (int a = 0; a < 4; ++a) {
+        for (int a = 0; a < NO; ++a) {
             s.jac(c.z(0, 0, IR + a), sgn);
 #pragma unroll
             for (int k = 0; k < K1; ++k) {
                 const T dk = T(p.D[k]);
 #pragma unroll
-                for (int m = 0; m < 4; ++m)
-                    s.jac(c.z(nl, k, IR + m), dk * ((a == m ? T(1) : T(0)) - qh[a] * qh[m]) * iq);
+                for (int m = 0; m < NO; ++m) s.jac(c.z(nl, k, IR + m), dk * op.jac(a, m));
             }
-            s.row(qh[a] + sgn * w(c.z(0, 0, IR + a)), 0.0, 0.0);
+            s.row(op.v[a] + sgn * w(c.z(0, 0, IR + a)), 0.0, 0.0);
         }
     } else {
         const double two_pi = 6.283185307179586;
@@ -491,13 +554,15 @@ ATO_HD void seg_boundary(const ProbD& p, int end, const W& w, S& s) {
     T z[NZ];
 #pragma unroll
     for (int i = 0; i < NZ; ++i) z[i] = zb[i];
-    T qh[4] = {T(0), T(0), T(0), T(0)}, iq = T(0);
-    const bool opq = M::IS_DRONE && M::HAS_QUAT && end;
-    if constexpr (M::IS_DRONE && M::HAS_QUAT) {
+    using Op = AttOp<M, T>;
+    constexpr int NO = Op::NO;
+    Op op;
+    const bool opq = M::IS_DRONE && NO > 0 && end;
+    if constexpr (M::IS_DRONE && NO > 0) {
         if (opq) {
-            qnormalize(zb + IR, qh, iq);
+            op.apply(zb + IR);
 #pragma unroll
-            for (int a = 0; a < 4; ++a) z[IR + a] = qh[a];
+            for (int a = 0; a < NO; ++a) z[IR + a] = op.v[a];
         }
     }
     // one row: derivatives dz (after the operator, mask zm) and du (mask um), chained through
@@ -510,14 +575,16 @@ ATO_HD void seg_boundary(const ProbD& p, int end, const W& w, S& s) {
             dzb[m] = dz[m];
             zmb[m] = zm[m];
         }
-        if constexpr (M::IS_DRONE && M::HAS_QUAT) {
+        if constexpr (M::IS_DRONE && NO > 0) {
             if (opq) {
-                const bool anyq = zm[IR] || zm[IR + 1] || zm[IR + 2] || zm[IR + 3];
+                bool anyq = false;
 #pragma unroll
-                for (int m = 0; m < 4; ++m) {
+                for (int a = 0; a < NO; ++a) anyq = anyq || zm[IR + a];
+#pragma unroll
+                for (int m = 0; m < NO; ++m) {
                     T acc = T(0);
 #pragma unroll
-                    for (int a = 0; a < 4; ++a) acc += dz[IR + a] * ((a == m ? T(1) : T(0)) - qh[a] * qh[m]) * iq;
+                    for (int a = 0; a < NO; ++a) acc += dz[IR + a] * op.jac(a, m);
                     dzb[IR + m] = acc;
                     zmb[IR + m] = anyq;
                 }
@@ -703,10 +770,11 @@ struct RK4Dep {
             for (int i = 0; i < NZ; ++i) kd[i] = kn[i];
         }
         for (int i = 0; i < NZ; ++i) dep[i] = dop[i] = (1u << i) | acc[i];
-        if (M::HAS_QUAT) {
+        constexpr int NO = M::HAS_QUAT ? 4 : (M::HAS_DCM ? 9 : 0);
+        if (NO > 0) {
             uint32_t q = 0;
-            for (int a = 0; a < 4; ++a) q |= dep[M::IR + a];
-            for (int a = 0; a < 4; ++a) dop[M::IR + a] = q;
+            for (int a = 0; a < NO; ++a) q |= dep[M::IR + a];
+            for (int a = 0; a < NO; ++a) dop[M::IR + a] = q;
         }
     }
 };
@@ -752,11 +820,11 @@ ATO_HD void rk4_phi(const ProbD& p, int n, int grp, const W& w, Dual<T, RK4_CG>*
     const D h6 = h / 6.0;
 #pragma unroll
     for (int i = 0; i < NZ; ++i) phi[i] = z[i] + h6 * acc[i];
-    if (OP && M::HAS_QUAT) {
-        D qh[4], iq;
-        qnormalize(phi + M::IR, qh, iq);
+    if constexpr (OP && AttOp<M, D>::NO > 0) {
+        AttOp<M, D> op;
+        op.apply(phi + M::IR);
 #pragma unroll
-        for (int a = 0; a < 4; ++a) phi[M::IR + a] = qh[a];
+        for (int a = 0; a < AttOp<M, D>::NO; ++a) phi[M::IR + a] = op.v[a];
     }
 }
 
@@ -882,12 +950,13 @@ ATO_HD void seg_drone_closure_rk4(const ProbD& p, int grp, const W& w, S& s) {
     };
     plain(1, T(0));
     plain(2, T(0));
-    const int first_after = M::HAS_QUAT ? IR + 4 : IR + 1;
+    constexpr int NO = AttOp<M, T>::NO;
+    const int first_after = NO > 0 ? IR + NO : IR + 1;
     for (int i = first_after; i < NZ; ++i) plain(i, T(0));
-    if (M::HAS_QUAT) {
-        const T sgn = p.quat_flip ? T(1) : T(-1);
+    if constexpr (NO > 0) {
+        const T sgn = (M::HAS_QUAT && p.quat_flip) ? T(1) : T(-1);
 #pragma unroll
-        for (int a = 0; a < 4; ++a) {
+        for (int a = 0; a < NO; ++a) {
             r.dh(phi[IR + a], T(1));
             r.lin(c.z(0, 0, IR + a), sgn);
             r.dzu(phi[IR + a], dp.dop[IR + a], T(1));

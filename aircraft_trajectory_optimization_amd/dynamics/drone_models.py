@@ -27,9 +27,10 @@ class DroneModel(DynamicsModel):
     def __init__(self, config: DroneConfig):
         self.config = config
         self.rot = Rotation(Reference.GLOBAL if config.global_r else Reference.PARAMETRIC,
+                            Parameterization.DCM if getattr(config, 'use_dcm', False) else
                             Parameterization.ESP if config.use_quat else Parameterization.YPR)
         self.nr = self.rot.nr
-        self.nz, self.nu = 6 + self.nr, 4
+        self.nz, self.nu = 9 + self.nr, 4     # p (3), r (nr), v_b (3), w_b (3)
 
     def _split(self, z):
         nr = self.nr
@@ -39,7 +40,7 @@ class DroneModel(DynamicsModel):
         ''' (p_dot, r_dot, R global, R relative to the frame the thrust is reported in) '''
         _, r, vb, wb = self._split(z)
         R = self.rot.R(r)
-        return R @ vb, self.rot.M(r) @ wb, R, R
+        return R @ vb, self.rot.rate(r, wb), R, R
 
     def _evaluate(self, z, u, geo):
         ''' drone_models.py:47-123 '''
@@ -81,13 +82,20 @@ class DroneModel(DynamicsModel):
         self.u2state(state, u)
         _, r, vb, wb = self._split(z)
         state.x.from_vec(z[:3])
-        state.r.from_vec(r)
+        self._set_r(state, r)
         state.v.from_vec(vb)
         state.w.from_vec(wb)
-        if self.config.use_quat:
+        if self.config.use_quat and self.rot.param == Parameterization.ESP:
             state.q.from_vec(r)
         else:
             self._set_q(state, z, u)
+
+    def _set_r(self, state, r):
+        if self.rot.param == Parameterization.DCM:     # the quaternion of R (orthonormalised)
+            U, _, Vt = np.linalg.svd(self.rot.R(r))
+            state.r.from_mat(U @ Vt)
+        else:
+            state.r.from_vec(r)
 
     def _zu_base(self):
         c = self.config
@@ -120,7 +128,7 @@ class ParametricDroneModel(ParametricDynamicsModel, DroneModel):
         p_dot, wp = self._parametric_rates(R_rel @ vb, z, geo)
         w_eff = wb if self.config.global_r else wb - Rr.T @ wp
         R = Rr if self.config.global_r else Rp @ Rr
-        return p_dot, self.rot.M(r) @ w_eff, R, R_rel
+        return p_dot, self.rot.rate(r, w_eff), R, R_rel
 
     def state2zu(self, state: DroneState):
         z = [*state.p.to_vec(), *state.r.to_vec(), *state.v.to_vec(), *state.w.to_vec()]
@@ -132,7 +140,7 @@ class ParametricDroneModel(ParametricDynamicsModel, DroneModel):
         self.u2state(state, u)
         _, r, vb, wb = self._split(z)
         state.p.from_vec(z[:3])
-        state.r.from_vec(r)
+        self._set_r(state, r)
         state.v.from_vec(vb)
         state.w.from_vec(wb)
         state.x.from_vec(self.line.p2x(*z[:3]))

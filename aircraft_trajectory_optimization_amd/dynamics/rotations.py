@@ -3,6 +3,7 @@ Attitude parameterisations on the host (numpy): drone3d/dynamics/rotations.py.
 
     ESP (quaternion, scalar last: qi, qj, qk, qr)   R(q) = standard DCM / |q|^2,  r_dot = M(q) w
     YPR (a, b, c)                                    R = Rz(a) Ry(b) Rx(c),        r_dot = M(r) w
+    DCM (R row-major; build-side, config 5)          R = r,                        r_dot = R [w]x
 
 The same expressions as the device models (csrc/ato_models.hpp) and the reference's SX
 graphs (rotations.py:44-102); bounds as rotations.py:130-161.
@@ -25,6 +26,7 @@ class Parameterization(Enum):
     ''' rotation parameterisation '''
     ESP = 0
     YPR = 1
+    DCM = 2      # build-side (config 5): not in the reference's rotations.py:19-24
 
 
 def esp_R(q) -> np.ndarray:
@@ -63,16 +65,30 @@ class Rotation:
 
     @property
     def nr(self) -> int:
-        return 4 if self.param == Parameterization.ESP else 3
+        return {Parameterization.ESP: 4, Parameterization.YPR: 3, Parameterization.DCM: 9}[self.param]
 
     def R(self, r) -> np.ndarray:
+        if self.param == Parameterization.DCM:
+            return np.asarray(r, float).reshape(3, 3)
         return esp_R(r) if self.param == Parameterization.ESP else ypr_R(r)
 
     def M(self, r) -> np.ndarray:
+        if self.param == Parameterization.DCM:
+            raise ValueError('the DCM rate is R [w]x, not M(r) w: use rate()')
         return esp_M(r) if self.param == Parameterization.ESP else ypr_M(r)
+
+    def rate(self, r, w) -> np.ndarray:
+        ''' r_dot for the body rate w '''
+        if self.param == Parameterization.DCM:
+            w = np.asarray(w, float)
+            W = np.array([[0, -w[2], w[1]], [w[2], 0, -w[0]], [-w[1], w[0], 0]])
+            return (self.R(r) @ W).reshape(-1)
+        return self.M(r) @ w
 
     def ubr(self):
         ''' rotations.py:130-145 '''
+        if self.param == Parameterization.DCM:
+            return [np.inf] * 9
         if self.param == Parameterization.ESP:
             return [np.inf] * 4
         if self.ref == Reference.GLOBAL:
@@ -81,6 +97,8 @@ class Rotation:
 
     def lbr(self):
         ''' rotations.py:147-161 '''
+        if self.param == Parameterization.DCM:
+            return [-np.inf] * 9
         if self.param == Parameterization.ESP:
             return [-np.inf] * 4
         if self.ref == Reference.GLOBAL:
@@ -88,7 +106,9 @@ class Rotation:
         return [-np.pi / 2, -np.pi / 2.1, -np.pi / 2.1]
 
     def get_empty_state(self):
-        ''' rotations.py:163-183 '''
+        ''' rotations.py:163-183 (DCM: the state's attitude field holds the quaternion of R) '''
+        if self.param == Parameterization.DCM:
+            return GlobalQuaternion() if self.ref == Reference.GLOBAL else RelativeQuaternion()
         if self.ref == Reference.GLOBAL:
             return GlobalQuaternion() if self.param == Parameterization.ESP else GlobalEulerAngles()
         return RelativeQuaternion() if self.param == Parameterization.ESP else RelativeEulerAngles()

@@ -14,7 +14,7 @@ KMAX = 9
 GEOM_WIDTH = 16
 
 ATO_MODEL_DRONE, ATO_MODEL_POINT = 0, 1
-ATO_ATT_ESP, ATO_ATT_YPR = 0, 1
+ATO_ATT_ESP, ATO_ATT_YPR, ATO_ATT_DCM = 0, 1, 2
 ATO_FRAME_GLOBAL, ATO_FRAME_PARAMETRIC = 0, 1
 ATO_TRANS_COLLOCATION, ATO_TRANS_RK4 = 0, 1
 ATO_GATE_CIRCLE, ATO_GATE_SQUARE = 0, 1

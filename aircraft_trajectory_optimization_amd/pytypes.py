@@ -317,6 +317,9 @@ class DroneConfig(RacerConfig):
     w_max: float = field(default=10)
     w_min: float = field(default=-10)
     use_quat: bool = field(default=False)
+    # build-side (config 5, not in the reference): direction-cosine-matrix attitude, the state
+    # carries R row-major (nz = 18); takes precedence over use_quat
+    use_dcm: bool = field(default=False)
 
 
 @dataclass

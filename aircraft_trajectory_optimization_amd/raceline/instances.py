@@ -23,7 +23,7 @@ def seeded_instances(spec: ProblemSpec, seeds: Iterable[int]) -> Tuple[np.ndarra
     nw, N, P, nv = spec.nw, spec.N, spec.P, spec.nv
     node = N + np.arange(P) * nv
     # velocity slots of the guess (scaled by v0): drone z[IV:IV+3], point z[3:6]
-    iv = (7 if spec.nz == 13 else 6) if spec.is_drone else 3
+    iv = spec.nz - 6 if spec.is_drone else 3
     W = np.repeat(spec.w0[None], B, axis=0)
     LBW = np.repeat(spec.lbw[None], B, axis=0)
     UBW = np.repeat(spec.ubw[None], B, axis=0)

@@ -33,6 +33,8 @@ def _rot_bounds(vehicle: RacerConfig):
     ''' attitude bounds (rotations.py:130-161) '''
     if not isinstance(vehicle, DroneConfig):
         return [], []
+    if getattr(vehicle, 'use_dcm', False):
+        return [INF] * 9, [-INF] * 9
     if vehicle.use_quat:
         return [INF] * 4, [-INF] * 4
     if vehicle.global_r:
@@ -60,8 +62,9 @@ class ProblemSpec:
         if not self.is_drone and not isinstance(vehicle, PointConfig):
             raise TypeError('vehicle must be DroneConfig or PointConfig')
         self.param = frame == 'parametric'
+        self.use_dcm = self.is_drone and bool(getattr(vehicle, 'use_dcm', False))
         if self.is_drone:
-            self.nz = 13 if vehicle.use_quat else 12
+            self.nz = 18 if self.use_dcm else 13 if vehicle.use_quat else 12
             self.nu = 4
         else:
             self.nz, self.nu = 6, 3
@@ -240,7 +243,10 @@ class ProblemSpec:
             z[0], z[1], z[2] = xg
             z[3], z[4], z[5] = vg
         if self.is_drone:
-            att = [1, 0, 0, 0] if self.vehicle.use_quat else [0, 0, 0]
+            if self.use_dcm:       # build-side DCM pose: R of the quaternion cold start (1, 0, 0, 0)
+                att = [1, 0, 0, 0, -1, 0, 0, 0, -1]
+            else:
+                att = [1, 0, 0, 0] if self.vehicle.use_quat else [0, 0, 0]
             z = [*z[:3], *att, *z[3:6], 0, 0, 0]
             if self.param:
                 z[0] = self.get_s(n, k)
@@ -288,7 +294,8 @@ class ProblemSpec:
             veh.update({'I': [v.I1, v.I2, v.I3], 'bw': [v.bw1, v.bw2, v.bw3], 'l': v.l, 'k': v.k})
         return {
             'model': native.ATO_MODEL_DRONE if self.is_drone else native.ATO_MODEL_POINT,
-            'attitude': native.ATO_ATT_ESP if (self.is_drone and v.use_quat) else native.ATO_ATT_YPR,
+            'attitude': (native.ATO_ATT_DCM if self.is_drone and self.use_dcm else
+                         native.ATO_ATT_ESP if (self.is_drone and v.use_quat) else native.ATO_ATT_YPR),
             'frame': native.ATO_FRAME_PARAMETRIC if self.param else native.ATO_FRAME_GLOBAL,
             'global_r': int(bool(v.global_r)),
             'transcription': native.ATO_TRANS_RK4 if self.rk4 else native.ATO_TRANS_COLLOCATION,

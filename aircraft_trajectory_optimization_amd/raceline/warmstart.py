@@ -71,7 +71,9 @@ def drone_guess(drone: ProblemSpec, point: ProblemSpec, x_point: np.ndarray) \
                 R = np.eye(3) + hat + hat @ hat * (1 - c) / s ** 2
             if not veh.global_r:
                 R = drone.line.p2Rp(drone.get_s(n, k)).T @ R
-            if veh.use_quat:
+            if getattr(veh, 'use_dcm', False):               # build-side DCM pose: R itself
+                r = R.reshape(-1)
+            elif veh.use_quat:
                 r = Rotation.from_matrix(R).as_quat()          # (x, y, z, w) = (qi, qj, qk, qr)
                 if last_r is not None and np.linalg.norm(r - last_r) >= 1:
                     r = -r
@@ -94,6 +96,7 @@ def drone_guess(drone: ProblemSpec, point: ProblemSpec, x_point: np.ndarray) \
             w0[di:di + drone.nz] = np.concatenate([zp[:3], r, vb, wb])
             w0[di + drone.nz:di + drone.nz + 4] = np.linalg.norm(T) / 4
             w0[di + drone.nz + 4:di + drone.nz + 8] = 0.0
-    quat_flip = bool(veh.use_quat and closed and np.linalg.norm(first_r - last_r) > 1)
-    wraps = float(np.round((last_r - first_r)[0] / 2 / np.pi)) if (closed and not veh.use_quat) else 0.0
+    dcm = bool(getattr(veh, 'use_dcm', False))
+    quat_flip = bool(veh.use_quat and not dcm and closed and np.linalg.norm(first_r - last_r) > 1)
+    wraps = float(np.round((last_r - first_r)[0] / 2 / np.pi)) if (closed and not veh.use_quat and not dcm) else 0.0
     return w0, lbw, ubw, quat_flip, wraps

@@ -38,7 +38,7 @@ def make_line(track: str, closed: bool = True) -> SplineCenterline:
 
 def make_spec(track='race', model='drone', frame='parametric', N=50, K=4, use_quat=True, global_r=True,
               fix_gate_center=False, quat_flip=False, spheres=None, v0=1.0, h0=1, rk4=False,
-              euler_wraps=0.0, closed=True) -> ProblemSpec:
+              euler_wraps=0.0, closed=True, use_dcm=False) -> ProblemSpec:
     ''' ProblemSpec of a scenario the way solve_util configures it (utils/solve_util.py:29-75) '''
     line = make_line(track, closed)
     if frame == 'parametric':
@@ -51,7 +51,7 @@ def make_spec(track='race', model='drone', frame='parametric', N=50, K=4, use_qu
         cfg.gate_xi, cfg.gate_xj, cfg.gate_xk = line.config.x
     cfg.fix_gate_center = fix_gate_center
     if model == 'drone':
-        veh = DroneConfig(global_r=True if frame == 'global' else global_r, use_quat=use_quat)
+        veh = DroneConfig(global_r=True if frame == 'global' else global_r, use_quat=use_quat, use_dcm=use_dcm)
     else:
         veh = PointConfig(global_r=global_r)
     return ProblemSpec(line, cfg, veh, frame, quat_flip=quat_flip, euler_wraps=euler_wraps, sphere_table=spheres)
@@ -61,7 +61,7 @@ def make_warm_spec(x_point, **kw) -> ProblemSpec:
     ''' drone ProblemSpec warm-started from a point-mass solution x_point of the same scenario
     (the point problem is make_spec(model='point', ...) with the same track / frame / N / K) '''
     from aircraft_trajectory_optimization_amd.raceline.warmstart import drone_guess
-    point = make_spec(**{**kw, 'model': 'point', 'use_quat': False})
+    point = make_spec(**{**kw, 'model': 'point', 'use_quat': False, 'use_dcm': False})
     drone0 = make_spec(**{**kw, 'model': 'drone'})
     w0, lbw, ubw, flip, wraps = drone_guess(drone0, point, np.asarray(x_point, float))
     drone = make_spec(**{**kw, 'model': 'drone', 'quat_flip': flip, 'euler_wraps': wraps})

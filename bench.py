@@ -55,6 +55,9 @@ def parse():
     ap.add_argument('--track', choices=['race', 'fig8'], default='race',
                     help='fig8: the config-5 evaluation workload (scripts/fig_8.py, N = 50, K = 4), with --dtype f32 '
                          '--batch 8192 --no-solve')
+    ap.add_argument('--pose', choices=['esp', 'dcm'], default='esp',
+                    help='attitude: esp (quaternion, the reference\'s) or dcm (config 5\'s direction-cosine-matrix '
+                         'pose, build-side): --track fig8 --pose dcm --dtype f32 --batch 8192 --no-solve')
     ap.add_argument('--cpu-seconds', type=float, default=15.0, help='budget of the CPU baselines')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-solve', action='store_true', help='evaluation kernel only')
@@ -111,8 +114,8 @@ def eval_bench(spec, W, args, dev, world):
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json, encoding='utf-8'))
-            if (tj.get('batch'), tj.get('dtype'), tj.get('layout'), tj.get('track', 'race')) == \
-                    (B, args.dtype, args.layout, args.track):
+            if (tj.get('batch'), tj.get('dtype'), tj.get('layout'), tj.get('track', 'race'), tj.get('pose', 'esp')) == \
+                    (B, args.dtype, args.layout, args.track, args.pose):
                 traffic = tj.get('hbm_bytes_per_launch')
         except (OSError, ValueError):
             traffic = None
@@ -200,7 +203,7 @@ def main():
     if world > 1:
         dist.init_process_group('nccl', device_id=dev)
 
-    spec_kw = dict(SPEC_KW, track=args.track)
+    spec_kw = dict(SPEC_KW, track=args.track, use_dcm=args.pose == 'dcm')
     spec = make_spec(**spec_kw)
     B = args.batch
     track = 'racetrack' if args.track == 'race' else 'fig8'
@@ -271,8 +274,8 @@ def main():
                 'vs_baseline': None,
                 'dtype': 'f64',
                 'data': 'synthetic: seeded cold-start instances (SURVEY 8(d) config 3 generator, raceline/instances.py)',
-                'config': {'workload': f'{track}_parametric_esp_drone_colloc_N50_K4_cold_start_batched_sqp',
-                           'N': 50, 'K': 4, 'nz': 13, 'nu': 4, 'batch_per_gpu': B, 'global_batch': world * B,
+                'config': {'workload': f'{track}_parametric_{args.pose}_drone_colloc_N50_K4_cold_start_batched_sqp',
+                           'N': 50, 'K': 4, 'nz': spec.nz, 'nu': 4, 'batch_per_gpu': B, 'global_batch': world * B,
                            'max_iter': args.max_iter, 'layout': args.layout,
                            'parallelism': f'instances sharded x{world}, records all-gathered'},
                 'lap_time_err_vs_casadi': None,
@@ -293,7 +296,8 @@ def main():
                'steps': args.eval_steps, 'warmup': args.eval_warmup, 'ms_per_step': evals['ms_per_step'],
                'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': args.dtype,
                'data': 'synthetic: seeded cold-start instances (evaluation kernel only, --no-solve)',
-               'config': {'workload': f'{track}_parametric_esp_drone_colloc_N50_K4_eval', 'batch_per_gpu': B,
+               'config': {'workload': f'{track}_parametric_{args.pose}_drone_colloc_N50_K4_eval', 'batch_per_gpu': B,
+                          'nz': spec.nz,
                           'global_batch': world * B, 'layout': args.layout},
                'roofline': roofline, 'cpu_baseline': None, 'evals': evals}
     if rank == 0:

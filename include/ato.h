@@ -43,7 +43,8 @@ enum { ATO_OK = 0, ATO_ERR_ARG = -1, ATO_ERR_UNSUPPORTED = -2, ATO_ERR_HIP = -3,
        ATO_ERR_STATE = -4 };
 
 enum { ATO_MODEL_DRONE = 0, ATO_MODEL_POINT = 1 };
-enum { ATO_ATT_ESP = 0, ATO_ATT_YPR = 1 };          /* quaternion / yaw-pitch-roll */
+enum { ATO_ATT_ESP = 0, ATO_ATT_YPR = 1, ATO_ATT_DCM = 2 };  /* quaternion / yaw-pitch-roll / direction-cosine
+                                                              matrix (build-side, config 5) */
 enum { ATO_FRAME_GLOBAL = 0, ATO_FRAME_PARAMETRIC = 1 };
 enum { ATO_TRANS_COLLOCATION = 0, ATO_TRANS_RK4 = 1 };
 enum { ATO_GATE_CIRCLE = 0, ATO_GATE_SQUARE = 1 };

@@ -6,6 +6,10 @@ Arrays carry a trailing batch axis and may be complex (complex-step differentiat
   drone pose / forces / state          drone3d/dynamics/drone_models.py:47-123
   parametric drone pose                drone3d/dynamics/drone_models.py:249-292
   point mass (global / parametric)     drone3d/dynamics/point_model.py:28-75, :149-213
+  DCM attitude (config 5)              NOT in the reference (rotations.py:19-24 has ESP and YPR only):
+                                       r = R row-major, R' = R [w]x -- parity unpinned by
+                                       construction; pinned by equivalence with the ESP model
+                                       (tests/test_dcm_cpu.py)
 '''
 import numpy as np
 
@@ -42,6 +46,18 @@ def ypr_M(r):
                      [o, np.sin(c) * np.tan(b), np.cos(c) * np.tan(b)]])
 
 
+def dcm_R(r):
+    ''' the DCM attitude state is R itself (row-major 9-vector) '''
+    return np.array([[r[0], r[1], r[2]], [r[3], r[4], r[5]], [r[6], r[7], r[8]]])
+
+
+def dcm_rdot(r, w):
+    ''' R' = R [w]x, row-major '''
+    R = dcm_R(r)
+    Rd = np.einsum('ijb,jkb->ikb', R, hat(w))
+    return Rd.reshape(9, *Rd.shape[2:])
+
+
 def mv(A, x):
     ''' (3,3,B) or (3,3) times (3,B) '''
     if A.ndim == 2:
@@ -54,19 +70,28 @@ def hat(v):
     return np.array([[z, -v[2], v[1]], [v[2], z, -v[0]], [-v[1], v[0], z]])
 
 
+def _att(use_quat):
+    ''' attitude parameterisation: True / 'esp' quaternion, False / 'ypr' Euler, 'dcm' matrix '''
+    if use_quat == 'dcm':
+        return 'dcm', 9
+    return ('esp', 4) if use_quat in (True, 'esp') else ('ypr', 3)
+
+
 def drone_zdot(z, u, veh, use_quat, frame, global_r, geo=None):
     '''
     z: (nz, B), u: (4, B). veh: dict of DroneConfig fields. frame: 'global' | 'parametric'.
     geo: dict with Rp (3,3), ks, ky, kn, mag for the parametric frame (fixed node geometry).
+    use_quat: True (ESP), False (YPR) or 'dcm'.
     '''
-    nr = 4 if use_quat else 3
+    att, nr = _att(use_quat)
     p, r, vb, wb = z[:3], z[3:3 + nr], z[3 + nr:6 + nr], z[6 + nr:9 + nr]
-    Rr = esp_R(r) if use_quat else ypr_R(r)
-    M = esp_M(r) if use_quat else ypr_M(r)
+    Rr = esp_R(r) if att == 'esp' else ypr_R(r) if att == 'ypr' else dcm_R(r)
+    kin = (lambda w: mv(esp_M(r), w)) if att == 'esp' else (lambda w: mv(ypr_M(r), w)) if att == 'ypr' \
+        else (lambda w: dcm_rdot(r, w))
     if frame == 'global':
         R = Rr
         p_dot = mv(R, vb)
-        r_dot = mv(M, wb)
+        r_dot = kin(wb)
     else:
         Rp = geo['Rp']
         R_rel = np.einsum('ai,ajb->ijb', Rp, Rr) if global_r else Rr
@@ -79,7 +104,7 @@ def drone_zdot(z, u, veh, use_quat, frame, global_r, geo=None):
         k = np.array([geo['ks'], geo['ky'], geo['kn']])
         wp = k[:, None] * s_dot * geo['mag']
         w_eff = wb if global_r else wb - np.einsum('jib,jb->ib', Rr, wp)
-        r_dot = mv(M, w_eff)
+        r_dot = kin(w_eff)
         R = Rr if global_r else np.einsum('ij,jkb->ikb', Rp, Rr)
     Fgb = -veh['m'] * veh['g'] * np.array([R[2, 0], R[2, 1], R[2, 2]])
     Fdb = -np.array([veh['b1'], veh['b2'], veh['b3']])[:, None] * vb
@@ -99,9 +124,9 @@ def drone_zdot(z, u, veh, use_quat, frame, global_r, geo=None):
 
 def drone_vg_R(z, use_quat, frame, global_r, geo=None):
     ''' global velocity and global rotation (f_vg, f_R helpers) '''
-    nr = 4 if use_quat else 3
+    att, nr = _att(use_quat)
     r, vb = z[3:3 + nr], z[3 + nr:6 + nr]
-    Rr = esp_R(r) if use_quat else ypr_R(r)
+    Rr = esp_R(r) if att == 'esp' else ypr_R(r) if att == 'ypr' else dcm_R(r)
     if frame == 'global' or global_r:
         R = Rr
     else:

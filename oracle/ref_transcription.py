@@ -52,10 +52,15 @@ class RefNLP:
         base.update(veh or {})
         self.veh = base
         self.use_quat = bool(base.get('use_quat', False)) if model == 'drone' else False
+        # build-side DCM pose (config 5; not in the reference): attitude state R, row-major
+        self.use_dcm = bool(base.get('use_dcm', False)) if model == 'drone' else False
+        if self.use_dcm:
+            self.use_quat = False
+        self.att = 'dcm' if self.use_dcm else self.use_quat
         self.global_r = bool(base.get('global_r', False))
         if model == 'drone' and frame == 'global':
             self.global_r = True     # GlobalDroneRaceline._get_model (drone_raceline.py:314-316)
-        self.nz = (13 if self.use_quat else 12) if model == 'drone' else 6
+        self.nz = (18 if self.use_dcm else 13 if self.use_quat else 12) if model == 'drone' else 6
         self.nu = 4 if model == 'drone' else 3
         self.nv = self.nz + 2 * self.nu
         self.closed, self.fix_gate_center = closed, fix_gate_center
@@ -106,7 +111,7 @@ class RefNLP:
 
     def f_ode(self, z, u, s):
         if self.model == 'drone':
-            return ref_models.drone_zdot(z, u, self.veh, self.use_quat, self.frame, self.global_r,
+            return ref_models.drone_zdot(z, u, self.veh, self.att, self.frame, self.global_r,
                                          self.geo(s) if self.frame == 'parametric' else None)
         return ref_models.point_zdot(z, u, self.veh, self.frame, self.global_r,
                                      self.geo(s) if self.frame == 'parametric' else None)
@@ -126,6 +131,13 @@ class RefNLP:
             z = z.copy()
             q = z[3:7]
             z[3:7] = q / np.sqrt(q[0] ** 2 + q[1] ** 2 + q[2] ** 2 + q[3] ** 2)
+        if self.model == 'drone' and self.use_dcm:
+            # build-side: one Newton-Schulz step towards SO(3), R (3 I - R^T R) / 2
+            z = z.copy()
+            R = ref_models.dcm_R(z[3:12])
+            S = np.einsum('kib,kjb->ijb', R, R)
+            P = 1.5 * R - 0.5 * np.einsum('ikb,kjb->ijb', R, S)
+            z[3:12] = P.reshape(9, *P.shape[2:])
         return z
 
     # -------------------------------------------------------------- guesses and bounds
@@ -154,7 +166,9 @@ class RefNLP:
             z[0], z[1], z[2] = xg
             z[3], z[4], z[5] = vg
         if self.model == 'drone':
-            if self.use_quat:
+            if self.use_dcm:      # R of the ESP cold-start quaternion (1, 0, 0, 0)
+                z = [*z[:3], 1, 0, 0, 0, -1, 0, 0, 0, -1, *z[3:6], 0, 0, 0]
+            elif self.use_quat:
                 z = [*z[:3], 1, 0, 0, 0, *z[3:6], 0, 0, 0]
             else:
                 z = [*z[:3], 0, 0, 0, *z[3:6], 0, 0, 0]
@@ -166,7 +180,9 @@ class RefNLP:
         v = self.veh
         inf = np.inf
         if self.model == 'drone':
-            if self.use_quat:
+            if self.use_dcm:
+                ru, rl = [inf] * 9, [-inf] * 9
+            elif self.use_quat:
                 ru, rl = [inf] * 4, [-inf] * 4
             elif self.global_r:
                 ru, rl = [inf, np.pi / 2.1, np.pi / 2.1], [-inf, -np.pi / 2.1, -np.pi / 2.1]
@@ -377,7 +393,11 @@ class RefNLP:
             zf, uf = zF(), uF()
             zd = zf - z0
             add(uf - u0, 0., 0.)
-            if self.use_quat:
+            if self.use_dcm:
+                add(zd[1:3], 0., 0.)
+                add(zd[12:], 0., 0.)
+                add(zf[3:12] - z0[3:12], 0., 0.)
+            elif self.use_quat:
                 add(zd[1:3], 0., 0.)
                 add(zd[7:], 0., 0.)
                 if self.quat_flip:
@@ -400,7 +420,7 @@ class RefNLP:
         if self.model == 'drone':
             if not (self.frame == 'global' or self.global_r):
                 raise NotImplementedError('oracle: open lines with the relative attitude')
-            return ref_models.drone_vg_R(z, self.use_quat, self.frame, self.global_r)
+            return ref_models.drone_vg_R(z, self.att, self.frame, self.global_r)
         if self.frame == 'parametric' and not self.global_r:
             raise NotImplementedError('oracle: open lines with the relative attitude')
         R = np.eye(3)

@@ -23,10 +23,11 @@ def oracle_line(track, closed=True):
 
 def oracle_nlp(track='race', model='drone', frame='parametric', N=50, K=4, use_quat=True, global_r=True,
                fix_gate_center=False, quat_flip=False, spheres=None, v0=1.0, h0=1, rk4=False, closed=True,
-               euler_wraps=0.0):
+               euler_wraps=0.0, use_dcm=False):
     from oracle.ref_transcription import RefNLP
     line = oracle_line(track, closed)
-    veh = {'use_quat': use_quat, 'global_r': global_r} if model == 'drone' else {'global_r': global_r}
+    veh = {'use_quat': use_quat, 'global_r': global_r, 'use_dcm': use_dcm} if model == 'drone' else \
+        {'global_r': global_r}
     fixed = (line.s[:-1] if closed else line.s) if frame == 'parametric' else None
     return RefNLP(line, model, frame, N, K, veh=veh, fix_gate_center=fix_gate_center, fixed_gates=fixed,
                   quat_flip=quat_flip, spheres=spheres, v0=v0, h0=h0, rk4=rk4, closed=closed,

@@ -34,6 +34,13 @@ for _model, _frame, _quat in [('drone', 'parametric', True), ('drone', 'parametr
                               ('point', 'parametric', False), ('point', 'global', False)]:
     VARIANTS.append(dict(track='race', model=_model, frame=_frame, use_quat=_quat, closed=False,
                          N=6 if _frame == 'global' else 4, K=3))
+# build-side DCM pose (config 5): restated in the oracle, pinned by equivalence (tests/test_dcm_cpu.py)
+for _frame, _gr, _extra in [('parametric', True, {}), ('parametric', False, {}), ('global', True, {}),
+                            ('parametric', True, {'closed': False}), ('global', True, {'closed': False}),
+                            ('parametric', True, {'rk4': True}), ('global', True, {'rk4': True})]:
+    VARIANTS.append(dict(track='race', model='drone', frame=_frame, use_dcm=True, global_r=_gr,
+                         N=7 if (_frame == 'global' or _extra.get('rk4')) else 4, K=2 if _extra.get('rk4') else 3,
+                         **_extra))
 
 
 def _id(c):

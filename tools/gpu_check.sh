@@ -86,6 +86,12 @@ for s in $STEPS; do
                    ATO_LIB_PATH=$lp run solve_$v 600 python tools/solve_batched.py --batch 512 --max-iter 200 --no-host --out "$OUT/solve_$v.json"
                    cp "$OUT/solve_$v.json" "$OUT/solve_${v}_$(date +%s).json"
                done ;;
+        config5) run pytest_config5 600 python -u -m pytest tests/test_gpu_config5.py -x -v -s --timeout 400 --timeout-method thread -p no:cacheprovider ;;
+        bench5) run bench5_dcm_f32 300 python bench.py --track fig8 --pose dcm --dtype f32 --batch 8192 --no-solve --no-cpu-baseline --eval-steps 50
+               run bench5_dcm_f64 300 python bench.py --track fig8 --pose dcm --dtype f64 --batch 8192 --no-solve --no-cpu-baseline --eval-steps 50
+               run bench5_esp_f32 300 python bench.py --track fig8 --pose esp --dtype f32 --batch 8192 --no-solve --no-cpu-baseline --eval-steps 50 ;;
+        prof5) run prof5 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof5" -o run -- \
+                   python bench.py --track fig8 --pose dcm --dtype f32 --batch 8192 --no-solve --no-cpu-baseline --eval-steps 30 ;;
         s16ab) i=0
                for v in 1536 1024 1536 1024; do
                    i=$((i+1))
