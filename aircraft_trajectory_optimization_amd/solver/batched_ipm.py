@@ -17,6 +17,9 @@ single-instance solver would make:
   * filter line search with switching / Armijo conditions and second-order corrections; every
     trial point of every instance is evaluated in one batched ato_eval
 
+  * IPOPT's watchdog and tiny-step handling (as solver/ipm.py), per instance: the watchdog point
+    and direction are stored column by column, watchdog trials are tested against them, and a
+    column whose watchdog fails returns to its point and backtracks along its direction
   * feasibility restoration (IPOPT's min ||c||_1 phase, as solver/ipm.py): the instances whose
     line search fails run a nested batched solve of the restoration NLP over (x, p, n); the
     elastic variables p, n are eliminated from its KKT system (_RestorationKKT), so it is
@@ -39,10 +42,13 @@ import torch
 
 from aircraft_trajectory_optimization_amd.solver.ipm import INF, IPMOptions
 
-RUNNING, OPTIMAL, ACCEPTABLE, MAX_ITER, LS_FAILED, KKT_FAILED, STOPPED, INACTIVE = range(8)
+RUNNING, OPTIMAL, ACCEPTABLE, MAX_ITER, LS_FAILED, KKT_FAILED, STOPPED, INACTIVE, TINY_STEP = range(9)
 STATUS_NAMES = {RUNNING: 'running', OPTIMAL: 'optimal', ACCEPTABLE: 'acceptable', MAX_ITER: 'max_iter',
                 LS_FAILED: 'restoration_failed', KKT_FAILED: 'kkt_failure', STOPPED: 'stopped',
-                INACTIVE: 'inactive'}
+                INACTIVE: 'inactive', TINY_STEP: 'tiny_step'}
+# watchdog point and direction of every column (stored while the column's watchdog is active)
+WD_VECS = ('x', 's', 'y', 'zl', 'zu', 'vl', 'vu', 'dx', 'ds', 'dy', 'dzl', 'dzu', 'dvl', 'dvu')
+WD_SCAL = ('alpha_max', 'alpha_z', 'theta', 'phi', 'gphi_d')
 FILTER_MAX = 256
 
 
@@ -676,6 +682,15 @@ class BatchedInteriorPoint:
         status = torch.where(act, torch.full((B,), RUNNING, dtype=torch.long, device=dev),
                              torch.full((B,), INACTIVE, dtype=torch.long, device=dev))
         n_resto = torch.zeros(B, dtype=torch.long, device=dev)
+        # watchdog / tiny steps (solver/ipm.py): shortened-step counter, watchdog flag and trial count,
+        # the tiny-step flag that forces a barrier decrease; wd: the stored watchdog points
+        ws_short = torch.zeros(B, dtype=torch.long, device=dev)
+        in_wd = torch.zeros(B, dtype=torch.bool, device=dev)
+        wd_trial = torch.zeros(B, dtype=torch.long, device=dev)
+        tiny_flag = torch.zeros(B, dtype=torch.bool, device=dev)
+        wd = {}
+        wd_on = o.watchdog_shortened_iter_trigger > 0
+        wdst = torch.zeros(4, dtype=torch.long, device=dev)         # started, succeeded, reverted, tiny steps
         own = torch.zeros(B, dtype=torch.long, device=dev)          # iterations done per instance
         waiting = torch.zeros(B, dtype=torch.bool, device=dev)      # frozen until the next restoration batch
         iters = torch.zeros(B, dtype=torch.long, device=dev)
@@ -744,8 +759,10 @@ class BatchedInteriorPoint:
                     save(cols, x, y, zl, zu, status, iters, n_resto)
                     sel = torch.nonzero(live).reshape(-1)
                     (x, s, f, g, gf, jv, y, zl, zu, vl, vu, mu, tau, nf, dwl, n_acc, status, n_resto, own, waiting,
-                     iters, act, infl) = self._compact(sel, (x, s, f, g, gf, jv, y, zl, zu, vl, vu, mu, tau, nf, dwl,
-                                                            n_acc, status, n_resto, own, waiting, iters, act, infl))
+                     iters, act, infl, ws_short, in_wd, wd_trial, tiny_flag) = self._compact(
+                        sel, (x, s, f, g, gf, jv, y, zl, zu, vl, vu, mu, tau, nf, dwl, n_acc, status, n_resto, own,
+                              waiting, iters, act, infl, ws_short, in_wd, wd_trial, tiny_flag))
+                    wd = dict(zip(wd.keys(), self._compact(sel, tuple(wd.values()))))
                     F = F.index_select(0, sel).contiguous()
                     cols = cols.index_select(0, sel)
                     self.ev = keep['ev'].subset(n_live)
@@ -795,14 +812,22 @@ class BatchedInteriorPoint:
                 print(f'[batched ipm{" resto" if stop_check is not None else ""}] iter {it}: '
                       f'{int(act.sum())} active, {int((status == OPTIMAL).sum())} optimal', file=sys.stderr, flush=True)
             if any_act:
-                # ---- barrier update (monotone), per instance
+                # ---- barrier update (monotone), per instance; a tiny step forces one decrease, and with
+                # mu already at its minimum ends the instance (IPOPT: TINY_STEP_DETECTED)
+                force = tiny_flag & act
+                tiny_flag = tiny_flag & False
                 for _ in range(100):
                     if self.vk is not None:
                         Emu = self.vk.errors(self._bd(), x, s, g, self.c_rhs, sg, y, zl, zu, vl, vu, dual_x, mu,
                                              self.n_bounds, o.s_max)[0]
                     else:
                         Emu = self._errors(dual_x, g, x, s, y, zl, zu, vl, vu, mu)[0]
-                    upd = act & (Emu <= o.kappa_eps * mu) & (mu > o.tol / 10)
+                    want = act & ((Emu <= o.kappa_eps * mu) | force)
+                    tstop = want & force & (mu <= o.tol / 10)
+                    status = torch.where(tstop, torch.full_like(status, TINY_STEP), status)
+                    act = act & ~tstop
+                    upd = want & (mu > o.tol / 10)
+                    force = force & False
                     if not bool(upd.any()):
                         break
                     mu_new = torch.clamp(torch.minimum(o.kappa_mu * mu, mu ** o.theta_mu), min=o.tol / 10)
@@ -832,6 +857,9 @@ class BatchedInteriorPoint:
                 dx, ds, dy, delta_w, ok, ctx = self._kkt_step(W, Js, Sx, Ss, rhs_x, rhs_s, rhs_y, mu, dwl, act)
                 laps.lap('kkt_other')
                 kfail = act & ~ok
+                # IPOPT: no direction inside the watchdog -> back to the watchdog point (below)
+                kwd = kfail & in_wd
+                kfail = kfail & ~in_wd
                 if allow_restoration:
                     # IPOPT's fallback when no search direction can be computed (delta_w beyond its
                     # maximum): the line search is skipped and the feasibility restoration phase starts
@@ -841,6 +869,7 @@ class BatchedInteriorPoint:
                     status = torch.where(kfail, torch.full_like(status, KKT_FAILED), status)
                 act = act & ok
                 dwl = torch.where(act & (delta_w > 0), delta_w, dwl)
+                act = act | kwd
                 # ---- bound multiplier steps, fraction to the boundary
                 if self.vk is not None:
                     dzl, dzu, dvl, dvu, alpha_max, alpha_z, gphi_d = self.vk.direction(
@@ -859,15 +888,75 @@ class BatchedInteriorPoint:
                     gphi_d = (gx * dx).sum(0) + (gs * ds).sum(0)
                 # ---- filter line search, all instances in lockstep
                 theta, phi = self._measures(x, s, g, f, mu)
-                neg = gphi_d < 0
-                mgd = torch.clamp(-gphi_d, min=1e-300)
-                t1 = o.gamma_phi * theta / mgd
-                t2 = o.delta * theta ** o.s_theta / mgd ** o.s_phi
-                amin = torch.where(neg & (theta <= self.theta_min),
-                                   torch.clamp(torch.minimum(t1, t2), max=o.gamma_theta),
-                                   torch.where(neg, torch.clamp(t1, max=o.gamma_theta), torch.full_like(t1, o.gamma_theta)))
-                alpha_min = o.alpha_min_frac * amin
-                alpha = alpha_max.clone()
+                # ---- tiny steps (IPOPT DetectTinyStep): taken in full, no line search
+                tiny = torch.zeros_like(act)
+                if o.tiny_step_tol > 0:
+                    rel_x = (dx.abs() / (1.0 + x.abs())).amax(0) if n else torch.zeros_like(mu)
+                    rel_s = (ds.abs() / (1.0 + s.abs())).amax(0) if ds.shape[0] else torch.zeros_like(mu)
+                    dymax = dy.abs().amax(0) if m else torch.zeros_like(mu)
+                    rmax_ = r.abs().amax(0) if m else torch.zeros_like(mu)
+                    tiny = act & ~in_wd & ~kwd & (rel_x <= o.tiny_step_tol) & (rel_s <= o.tiny_step_tol) & \
+                        (dymax <= o.tiny_step_y_tol) & (rmax_ <= 1e-4)
+                    tiny_flag = tiny_flag | tiny
+                # ---- watchdog: columns whose last trigger steps were all shortened store this point
+                # and direction; their trial below is the full step against these references
+                dirs = {'dx': dx, 'ds': ds, 'dy': dy, 'dzl': dzl, 'dzu': dzu, 'dvl': dvl, 'dvu': dvu}
+                nosoc = torch.zeros_like(act)
+                wdm = torch.zeros_like(act)
+                if wd_on:
+                    start = act & ~tiny & ~in_wd & ~kwd & (ws_short >= o.watchdog_shortened_iter_trigger)
+                    cur = {'x': x, 's': s, 'y': y, 'zl': zl, 'zu': zu, 'vl': vl, 'vu': vu, **dirs,
+                           'alpha_max': alpha_max, 'alpha_z': alpha_z, 'theta': theta, 'phi': phi, 'gphi_d': gphi_d}
+                    if not wd:
+                        wd = {k: torch.zeros_like(cur[k]) for k in WD_VECS + WD_SCAL}
+                    wd = {k: torch.where(start[None, :] if v.dim() == 2 else start, cur[k], v) for k, v in wd.items()}
+                    in_wd = in_wd | start
+                    wd_trial = torch.where(start, torch.zeros_like(wd_trial), wd_trial)
+                    wdst[0] += start.sum()
+                    wdm = act & in_wd
+
+                def revert(msk):
+                    # stop the watchdog of the masked columns: their iterate and direction go back to the
+                    # watchdog point's, the line search backtracks from half its full step (the full step
+                    # was tried there) without second-order corrections (the factors are gone)
+                    nonlocal x, s, y, zl, zu, vl, vu, alpha_max, alpha_z, theta, phi, gphi_d, in_wd, nosoc, \
+                        f, g, gf, jv
+                    m2 = msk[None, :]
+                    x, s, y = (torch.where(m2, wd[k], v) for k, v in (('x', x), ('s', s), ('y', y)))
+                    zl, zu, vl, vu = (torch.where(m2, wd[k], v) for k, v in (('zl', zl), ('zu', zu), ('vl', vl),
+                                                                           ('vu', vu)))
+                    for k in dirs:
+                        dirs[k] = torch.where(m2, wd[k], dirs[k])
+                    alpha_max, alpha_z, theta, phi, gphi_d = (
+                        torch.where(msk, wd[k], v) for k, v in (('alpha_max', alpha_max), ('alpha_z', alpha_z),
+                                                                ('theta', theta), ('phi', phi), ('gphi_d', gphi_d)))
+                    in_wd = in_wd & ~msk
+                    nosoc = nosoc | msk
+                    fe_, ge_, gfe_, jve_ = self._eval(x)
+                    f, g = torch.where(msk, fe_, f), torch.where(m2, ge_, g)
+                    gf, jv = torch.where(m2, gfe_, gf), torch.where(m2, jve_, jv)
+                    wdst[2] += msk.sum()
+
+                def alpha_min_of(theta_, gphi_):
+                    neg = gphi_ < 0
+                    mgd = torch.clamp(-gphi_, min=1e-300)
+                    t1 = o.gamma_phi * theta_ / mgd
+                    t2 = o.delta * theta_ ** o.s_theta / mgd ** o.s_phi
+                    amin = torch.where(neg & (theta_ <= self.theta_min),
+                                       torch.clamp(torch.minimum(t1, t2), max=o.gamma_theta),
+                                       torch.where(neg, torch.clamp(t1, max=o.gamma_theta),
+                                                   torch.full_like(t1, o.gamma_theta)))
+                    return o.alpha_min_frac * amin
+
+                any_kwd = wd_on and bool(kwd.any())
+                if any_kwd:
+                    revert(kwd)
+                dx, ds, dy, dzl, dzu, dvl, dvu = (dirs[k] for k in ('dx', 'ds', 'dy', 'dzl', 'dzu', 'dvl', 'dvu'))
+                alpha_min = alpha_min_of(theta, gphi_d)
+                alpha = torch.where(kwd, alpha_max * 0.5, alpha_max) if any_kwd else alpha_max.clone()
+                any_wd = wd_on and bool(wdm.any())
+                wd_succ = torch.zeros_like(act)
+                wd_cols = wdm.clone()
                 pend = act.clone()
                 resto = torch.zeros(B, dtype=torch.bool, device=dev)
                 first = torch.ones(B, dtype=torch.bool, device=dev)
@@ -905,15 +994,43 @@ class BatchedInteriorPoint:
                     ft, gt = self._eval_fg(xt)
                     laps.lap('ls_eval')
                     tht, pht = self._measures(xt, st, gt, ft, mu)
+                    if _ls == 0 and any_wd:          # watchdog trials: tested against the watchdog point
+                        th_r, ph_r = torch.where(wdm, wd['theta'], theta), torch.where(wdm, wd['phi'], phi)
+                        gd_r, al_r = torch.where(wdm, wd['gphi_d'], gphi_d), torch.where(wdm, wd['alpha_max'], alpha)
+                    else:
+                        th_r, ph_r, gd_r, al_r = theta, phi, gphi_d, alpha
                     if self.vk is not None:          # one launch: the filter test and the SOC candidates
-                        okt, armt, soc = self.vk.filter_accept(theta, phi, gphi_d, alpha, tht, pht, F, nf,
+                        okt, armt, soc = self.vk.filter_accept(th_r, ph_r, gd_r, al_r, tht, pht, F, nf,
                                                                self.theta_max, self.theta_min, pend, first, o)
                     else:
-                        okt, armt = self._accept(theta, phi, gphi_d, alpha, tht, pht, F, nf)
+                        okt, armt = self._accept(th_r, ph_r, gd_r, al_r, tht, pht, F, nf)
                         okt = okt & pend
-                        soc = pend & ~okt & first & (tht >= theta)
+                        soc = pend & ~okt & first & (tht >= th_r)
+                    soc = soc & ~nosoc & ~wdm & ~tiny
                     take(okt, alpha, xt, st, armt, dy)
                     pend = pend & ~okt
+                    if _ls == 0:
+                        # tiny steps: taken untested (no filter entry)
+                        take(tiny, alpha, xt, st, torch.ones_like(tiny), dy)
+                        pend = pend & ~tiny
+                        if any_wd:
+                            wd_succ = wdm & okt
+                            in_wd = in_wd & ~wd_succ
+                            failw = wdm & ~okt
+                            wd_trial = torch.where(failw, wd_trial + 1, wd_trial)
+                            blind = failw & (wd_trial <= o.watchdog_trial_iter_max)
+                            take(blind, alpha, xt, st, torch.ones_like(blind), dy)   # accepted untested
+                            rev = failw & ~blind
+                            pend = pend & ~wdm
+                            if bool(rev.any()):
+                                revert(rev)
+                                dx, ds, dy, dzl, dzu, dvl, dvu = (dirs[k] for k in ('dx', 'ds', 'dy', 'dzl',
+                                                                                    'dzu', 'dvl', 'dvu'))
+                                alpha_min = torch.where(rev, alpha_min_of(theta, gphi_d), alpha_min)
+                                alpha = torch.where(rev, alpha_max, alpha)   # halved below: skips the full step
+                                pend = pend | rev
+                                wd_cols = wd_cols & ~rev
+                            wdst[1] += wd_succ.sum()
                     if _ls == 0 and bool(soc.any()):     # corrections only after the first trial step
                         laps.lap('ls_logic')
                         if slk is None:
@@ -928,7 +1045,16 @@ class BatchedInteriorPoint:
                 laps.lap('ls_logic')
                 # ---- accept
                 upd = act & ~resto
+                if any_wd:                           # a successful watchdog trial: the watchdog references
+                    theta = torch.where(wd_succ, wd['theta'], theta)
+                    phi = torch.where(wd_succ, wd['phi'], phi)
                 add_filter(upd & ~armn, theta, phi)
+                if wd_on:
+                    # watchdog trigger: consecutive accepted steps shorter than the fraction-to-the-boundary step
+                    normal = upd & ~tiny & ~wd_cols
+                    ws_short = torch.where(normal, torch.where(an < alpha_max, ws_short + 1, torch.zeros_like(ws_short)),
+                                           torch.where(upd, torch.zeros_like(ws_short), ws_short))
+                wdst[3] += tiny.sum()
                 m2 = upd[None, :]
                 x = torch.where(m2, xn, x)
                 s = torch.where(m2, sn, s)
@@ -1035,6 +1161,10 @@ class BatchedInteriorPoint:
             self._async_pool = None
         save(cols, x, y, zl, zu, status, iters, n_resto)
         self.stats['restorations'] = self.stats.get('restorations', 0) + int(out['n_resto'].sum())
+        wv = wdst.tolist()
+        prev = self.stats.get('watchdog', {})
+        self.stats['watchdog'] = {k: prev.get(k, 0) + v for k, v in
+                                  zip(('started', 'succeeded', 'reverted', 'tiny_steps'), wv)}
         for k_, v_ in keep.items():                 # back to the full batch
             setattr(self, k_, v_)
         x = out['x']
@@ -1251,7 +1381,11 @@ class BatchedInteriorPoint:
         for k2, v in stats.items():
             if k2 == 'resto_phases':
                 self.stats.setdefault('resto_phases', []).extend(v)
-            else:
+            elif k2 == 'watchdog':
+                cur = self.stats.setdefault('resto_watchdog', {})
+                for k3, v3 in v.items():
+                    cur[k3] = cur.get(k3, 0) + v3
+            elif isinstance(v, (int, float)):
                 self.stats[k2] = self.stats.get(k2, 0) + v
         for k2, v in laps.items():                # diagnostic split of the nested solve
             self.laps.t['resto:' + k2] = self.laps.t.get('resto:' + k2, 0.0) + v

@@ -17,6 +17,14 @@ IPOPT's default options:
   * filter line search with switching / Armijo conditions and second-order corrections
   * convergence on the scaled optimality error E_0 <= tol (1e-8) plus IPOPT's unscaled
     dual / constraint / complementarity limits; "acceptable" level 1e-6 for 15 iterations
+  * the watchdog (non-monotone) procedure: after 10 consecutive shortened steps the full step is
+    tried against the watchdog point's filter references for up to 3 iterations (accepted
+    untested while it fails); if none passes, the iterate returns to the watchdog point and the
+    line search backtracks along its stored direction
+  * tiny-step detection: a step below 10 eps relative to every x and s (and below 1e-2 in y, with
+    the constraint violation below 1e-4) is taken in full without a line search and forces a
+    barrier decrease; with the barrier already at its minimum the solve stops ('tiny_step', IPOPT's
+    "search direction becomes too small")
   * feasibility restoration when the line search fails or no search direction can be computed
     (IPOPT's fallback mechanism; its min ||c||_1 phase): an
     interior-point solve of  min rho sum(p + n) + zeta/2 |D_R (x - x_r)|^2  s.t.  c(x) - p + n
@@ -88,6 +96,12 @@ class IPMOptions:
     resto_penalty: float = 1000.0
     resto_kappa: float = 0.9
     max_resto: int = 50
+    # watchdog (IPOPT: watchdog_shortened_iter_trigger, watchdog_trial_iter_max)
+    watchdog_shortened_iter_trigger: int = 10
+    watchdog_trial_iter_max: int = 3
+    # tiny steps (IPOPT: tiny_step_tol = 10 eps, tiny_step_y_tol)
+    tiny_step_tol: float = 10 * 2.220446049250313e-16
+    tiny_step_y_tol: float = 1e-2
     verbose: bool = False
 
 
@@ -266,6 +280,10 @@ class InteriorPointSolver:
         history = []
         status = 'max_iter'
         it = 0
+        ws_short = 0              # consecutive accepted steps shorter than alpha_max (watchdog trigger)
+        wd = None                 # watchdog point and direction while the watchdog is active
+        tiny_flag = False         # the last step was tiny: force a barrier decrease
+        self.wd_stats = {'started': 0, 'succeeded': 0, 'reverted': 0, 'tiny_steps': 0}
         for it in range(o.max_iter + 1):
             J = self._J(jv)
             E0, du, pr, co = errors(gf, J, g, x, s, y, zl, zu, vl, vu, 0.0)
@@ -288,14 +306,23 @@ class InteriorPointSolver:
                 break
             if it == o.max_iter:
                 break
-            # ---- barrier update (monotone)
+            # ---- barrier update (monotone); a tiny step forces one decrease, and with mu already at
+            # its minimum ends the solve (IPOPT: MonotoneMuUpdate, TINY_STEP_DETECTED)
+            force, tiny_flag = tiny_flag, False
             while True:
                 Emu = errors(gf, J, g, x, s, y, zl, zu, vl, vu, mu)[0]
-                if Emu > o.kappa_eps * mu or mu <= o.tol / 10:
+                if Emu > o.kappa_eps * mu and not force:
+                    break
+                if mu <= o.tol / 10:
+                    if force:
+                        status = 'tiny_step'
                     break
                 mu = max(o.tol / 10, min(o.kappa_mu * mu, mu ** o.theta_mu))
                 tau = max(o.tau_min, 1.0 - mu)
                 filt = []
+                force = False
+            if status == 'tiny_step':
+                break
             # ---- Newton step
             W = _lower_to_full(n, self.ev.h_row_ptr, self.ev.h_col, self.ev.hess(x, y * self.sg, self.sf))
             self.evals['hess'] += 1
@@ -308,6 +335,10 @@ class InteriorPointSolver:
             rhs_s = -(gs - y[iin])
             rhs_y = -r
             step = self._kkt(W, J, Sx, Ss, rhs_x, rhs_s, rhs_y, iin, mu, delta_w_last)
+            if step is None and wd is not None:
+                # IPOPT: no direction inside the watchdog -> back to the watchdog point, and the line
+                # search continues along its stored direction
+                step = 'revert'
             if step is None:
                 # IPOPT's fallback when no search direction can be computed (delta_w beyond its
                 # maximum): skip the line search, start the feasibility restoration phase
@@ -334,22 +365,77 @@ class InteriorPointSolver:
                 vl, vu = np.where(hsl, mu / c, 0), np.where(hsu, mu / d, 0)
                 y = self._ls_multipliers(self._J(jv), gf, zl, zu, vl, vu, iin)
                 continue
-            dx, ds, dy, delta_w, solve = step
-            if delta_w > 0:
-                delta_w_last = delta_w
-            # ---- bound multiplier steps
-            dzl = np.where(hxl, mu / a - zl - zl / a * dx, 0)
-            dzu = np.where(hxu, mu / b - zu + zu / b * dx, 0)
-            dvl = np.where(hsl, mu / c - vl - vl / c * ds, 0)
-            dvu = np.where(hsu, mu / d - vu + vu / d * ds, 0)
-            alpha_max = min(self._ftb(a, dx, hxl, tau), self._ftb(b, -dx, hxu, tau),
-                            self._ftb(c, ds, hsl, tau), self._ftb(d, -ds, hsu, tau))
-            alpha_z = min(self._ftb(zl, dzl, hxl, tau), self._ftb(zu, dzu, hxu, tau),
-                          self._ftb(vl, dvl, hsl, tau), self._ftb(vu, dvu, hsu, tau))
+            if step != 'revert':
+                dx, ds, dy, delta_w, solve = step
+                if delta_w > 0:
+                    delta_w_last = delta_w
+                # ---- bound multiplier steps
+                dzl = np.where(hxl, mu / a - zl - zl / a * dx, 0)
+                dzu = np.where(hxu, mu / b - zu + zu / b * dx, 0)
+                dvl = np.where(hsl, mu / c - vl - vl / c * ds, 0)
+                dvu = np.where(hsu, mu / d - vu + vu / d * ds, 0)
+                alpha_max = min(self._ftb(a, dx, hxl, tau), self._ftb(b, -dx, hxu, tau),
+                                self._ftb(c, ds, hsl, tau), self._ftb(d, -ds, hsu, tau))
+                alpha_z = min(self._ftb(zl, dzl, hxl, tau), self._ftb(zu, dzu, hxu, tau),
+                              self._ftb(vl, dvl, hsl, tau), self._ftb(vu, dvu, hsu, tau))
+                theta, _ = theta_of(g, s)
+                phi = phi_of(f, x, s, mu)
+                gphi_d = gx @ dx + gs @ ds
+            accepted = None
+            skip_first = False
+            tiny = False
+            if step != 'revert':
+                # ---- tiny step (IPOPT DetectTinyStep): taken in full, no line search
+                tiny = (wd is None and o.tiny_step_tol > 0 and
+                        np.max(np.abs(dx) / (1.0 + np.abs(x)), initial=0) <= o.tiny_step_tol and
+                        np.max(np.abs(ds) / (1.0 + np.abs(s)), initial=0) <= o.tiny_step_tol and
+                        np.max(np.abs(dy), initial=0) <= o.tiny_step_y_tol and np.abs(r).max(initial=0) <= 1e-4)
+                if tiny:
+                    self.wd_stats['tiny_steps'] += 1
+                    tiny_flag = True
+                    xt, st = x + alpha_max * dx, s + alpha_max * ds
+                    ft, gt, gft, jvt = self._eval(xt)
+                    accepted = (alpha_max, xt, st, ft, gt, gft, jvt, True, dy)
+                elif wd is None and o.watchdog_shortened_iter_trigger > 0 and \
+                        ws_short >= o.watchdog_shortened_iter_trigger:
+                    # ---- start the watchdog at this iterate and direction
+                    self.wd_stats['started'] += 1
+                    wd = dict(x=x, s=s, y=y, zl=zl, zu=zu, vl=vl, vu=vu, f=f, g=g, gf=gf, jv=jv, dx=dx, ds=ds,
+                              dy=dy, dzl=dzl, dzu=dzu, dvl=dvl, dvu=dvu, alpha_max=alpha_max, alpha_z=alpha_z,
+                              theta=theta, phi=phi, gphi_d=gphi_d, trial=0)
+                if wd is not None and not tiny:
+                    # ---- watchdog trial: the full step, tested against the watchdog point's references
+                    xt, st = x + alpha_max * dx, s + alpha_max * ds
+                    ft, gt, gft, jvt = self._eval(xt)
+                    tht, _ = theta_of(gt, st)
+                    pht = phi_of(ft, xt, st, mu)
+                    ok, arm = self._accept(wd['theta'], wd['phi'], wd['gphi_d'], wd['alpha_max'], tht, pht, filt,
+                                           theta_max, theta_min)
+                    if ok:
+                        self.wd_stats['succeeded'] += 1
+                        theta, phi = wd['theta'], wd['phi']     # filter references of the accepted step
+                        accepted = (alpha_max, xt, st, ft, gt, gft, jvt, arm, dy)
+                        wd = None
+                    else:
+                        wd['trial'] += 1
+                        if wd['trial'] <= o.watchdog_trial_iter_max:
+                            accepted = (alpha_max, xt, st, ft, gt, gft, jvt, True, dy)   # untested
+                        else:
+                            step = 'revert'
+            if step == 'revert':
+                # ---- stop the watchdog: back to its point; backtrack along its direction, skipping
+                # the full step already tried there (no second-order correction: the factors are gone)
+                self.wd_stats['reverted'] += 1
+                x, s, y, zl, zu, vl, vu = (wd[k] for k in ('x', 's', 'y', 'zl', 'zu', 'vl', 'vu'))
+                f, g, gf, jv = wd['f'], wd['g'], wd['gf'], wd['jv']
+                dx, ds, dy, dzl, dzu, dvl, dvu = (wd[k] for k in ('dx', 'ds', 'dy', 'dzl', 'dzu', 'dvl', 'dvu'))
+                alpha_max, alpha_z = wd['alpha_max'], wd['alpha_z']
+                theta, phi, gphi_d = wd['theta'], wd['phi'], wd['gphi_d']
+                a, b, c, d = slacks(x, s)
+                wd = None
+                skip_first = True
+                solve = None
             # ---- filter line search
-            theta, _ = theta_of(g, s)
-            phi = phi_of(f, x, s, mu)
-            gphi_d = gx @ dx + gs @ ds
             if gphi_d < 0 and theta <= theta_min:
                 amin = min(o.gamma_theta, o.gamma_phi * theta / -gphi_d,
                            o.delta * theta ** o.s_theta / (-gphi_d) ** o.s_phi)
@@ -358,10 +444,9 @@ class InteriorPointSolver:
             else:
                 amin = o.gamma_theta
             alpha_min = o.alpha_min_frac * amin
-            alpha = alpha_max
-            accepted = None
-            first = True
-            while alpha >= alpha_min:
+            alpha = alpha_max * (0.5 if skip_first else 1.0)
+            first = not skip_first
+            while accepted is None and alpha >= alpha_min:
                 xt, st = x + alpha * dx, s + alpha * ds
                 ft, gt, gft, jvt = self._eval(xt)
                 tht, rt = theta_of(gt, st)
@@ -370,7 +455,7 @@ class InteriorPointSolver:
                 if ok:
                     accepted = (alpha, xt, st, ft, gt, gft, jvt, armijo_step, dy)
                     break
-                if first and tht >= theta:
+                if first and tht >= theta and solve is not None:
                     # second-order corrections (IPOPT A-5.7 ... A-5.10)
                     soc = self._soc(solve, rhs_x, rhs_s, x, s, alpha, r, rt, theta, phi, gphi_d, filt, theta_max,
                                     theta_min, theta_of, phi_of, tau, a, b, c, d, hxl, hxu, hsl, hsu, mu)
@@ -400,6 +485,11 @@ class InteriorPointSolver:
             alpha, xt, st, ft, gt, gft, jvt, armijo_step, dyacc = accepted
             if not armijo_step:
                 filt.append(((1 - o.gamma_theta) * theta, phi - o.gamma_phi * theta))
+            if wd is None and not tiny:
+                # watchdog trigger: consecutive steps shorter than the fraction-to-the-boundary step
+                ws_short = ws_short + 1 if alpha < alpha_max else 0
+            else:
+                ws_short = 0
             x, s, f, g, gf, jv = xt, st, ft, gt, gft, jvt
             y = y + alpha * dyacc
             zl, zu = zl + alpha_z * dzl, zu + alpha_z * dzu
@@ -420,6 +510,7 @@ class InteriorPointSolver:
         success = status in ('optimal', 'acceptable')
         stats = dict(self.evals)
         stats['restorations'] = n_resto
+        stats['watchdog'] = dict(self.wd_stats)
         return IPMResult(x=x, f=float(fu), g=gu, lam_g=lam_g, lam_x=lam_x, status=status, success=success,
                          iters=it, stats=stats, history=history)
 

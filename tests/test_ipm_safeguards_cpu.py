@@ -1,0 +1,93 @@
+'''
+IPOPT's watchdog procedure and tiny-step handling (IPOPT defaults the reference runs with, since
+base_raceline.py:752-799 sets neither watchdog_shortened_iter_trigger = 10 nor tiny_step_tol =
+10 eps): in the single-instance solver (solver/ipm.py) and in the lockstep batched solver
+(solver/batched_ipm.py), which must make the same decisions instance by instance.
+
+  * watchdog: a drone cold start whose line search shortens 10 steps in a row starts it; both a
+    successful watchdog and one that returns to its point and backtracks occur on this instance;
+    the solve converges to a KKT point, and the batched solver follows the single one;
+  * tiny steps: on a small problem that cannot meet the (here unreachable) constraint-violation
+    tolerance, the converged steps fall below 10 eps; each forces a barrier decrease and, with the
+    barrier at its minimum, the solve stops with 'tiny_step' (IPOPT: "search direction becomes too
+    small"), in both solvers at the same iteration.
+'''
+import numpy as np
+import torch
+
+from aircraft_trajectory_optimization_amd.raceline.instances import seeded_instances
+from aircraft_trajectory_optimization_amd.solver.batched_ipm import BatchedInteriorPoint
+from aircraft_trajectory_optimization_amd.solver.ipm import InteriorPointSolver, IPMOptions
+from tests.batched_backends import HostBatchEvaluator, HostBlockKKT
+from tests.helpers import HostEvaluator, product_spec
+
+
+def test_watchdog_starts_succeeds_reverts_and_converges():
+    spec = product_spec(track='fig8', N=6, K=2)
+    ev = HostEvaluator(spec)
+    W, L, U = seeded_instances(spec, [4])
+    o = IPMOptions(max_iter=600)
+    r = InteriorPointSolver(ev, L[0], U[0], ev.lbg, ev.ubg, o).solve(W[0])
+    wd = r.stats['watchdog']
+    assert r.status == 'optimal', r.status
+    assert wd['started'] >= 2 and wd['succeeded'] >= 1 and wd['reverted'] >= 1, wd
+    # without the watchdog the same start takes another path
+    r0 = InteriorPointSolver(ev, L[0], U[0], ev.lbg, ev.ubg,
+                             IPMOptions(max_iter=600, watchdog_shortened_iter_trigger=0)).solve(W[0])
+    assert r0.stats['watchdog']['started'] == 0 and r0.iters != r.iters
+    # the batched solver makes the same decisions (CPU stand-ins of its device pieces) over the first
+    # 40 iterations, which hold a successful and a reverted watchdog
+    o40 = IPMOptions(max_iter=40)
+    r40 = InteriorPointSolver(ev, L[0], U[0], ev.lbg, ev.ubg, o40).solve(W[0])
+    assert r40.stats['watchdog']['succeeded'] >= 1 and r40.stats['watchdog']['reverted'] >= 1
+    bev = HostBatchEvaluator(spec, 1)
+    rb = BatchedInteriorPoint(bev, HostBlockKKT(bev), L, U, o40).solve(W)
+    assert rb.status[0] == r40.status and int(rb.iters[0]) == r40.iters
+    assert rb.stats['watchdog'] == r40.stats['watchdog']
+    assert np.abs(rb.x[:, 0].numpy() - r40.x).max() <= 1e-8 * max(1.0, np.abs(r40.x).max())
+
+
+class _Toy:
+    ''' min (x0 - 0.3)^2 + (x1 - 0.3)^2  s.t.  x0 + x1 = 1,  0 <= x <= 1  (solution 0.5, 0.5), as the
+    single-instance evaluator and as a batched CPU evaluator of `batch` identical instances '''
+    nw, ng = 2, 1
+    n, m = 2, 1
+    j_row_ptr, j_col = np.array([0, 2]), np.array([0, 1])
+    h_row_ptr, h_col = np.array([0, 1, 2]), np.array([0, 1])
+    lbg, ubg = np.array([1.0]), np.array([1.0])
+    var_stage = np.zeros(2, int)
+    device = torch.device('cpu')
+
+    def __init__(self, batch=1):
+        self.batch = batch
+
+    def eval(self, x):
+        if torch.is_tensor(x):
+            B = x.shape[1]
+            f = ((x - 0.3) ** 2).sum(0)
+            return f, x.sum(0, keepdim=True), 2 * (x - 0.3), torch.ones((2, B), dtype=torch.float64)
+        return float(((x - 0.3) ** 2).sum()), np.array([x.sum()]), 2 * (x - 0.3), np.ones(2)
+
+    def hess(self, x, lam, sigma):
+        if torch.is_tensor(x):
+            return 2 * sigma[None, :].expand(2, -1).clone()
+        return np.full(2, 2.0 * sigma)
+
+    def subset(self, count):
+        return _Toy(count)
+
+
+def test_tiny_steps_force_the_barrier_down_and_end_the_solve():
+    o = IPMOptions(max_iter=200, constr_viol_tol=-1.0)        # convergence unreachable on purpose
+    lb, ub = np.zeros(2), np.ones(2)
+    x0 = np.array([0.9, 0.2])
+    r = InteriorPointSolver(_Toy(), lb, ub, _Toy.lbg, _Toy.ubg, o).solve(x0)
+    assert r.status == 'tiny_step', r.status
+    assert r.stats['watchdog']['tiny_steps'] >= 1
+    assert r.history[-1]['mu'] <= o.tol / 10 * (1 + 1e-12)
+    np.testing.assert_allclose(r.x, [0.5, 0.5], atol=1e-8)
+    ev = _Toy(2)
+    rb = BatchedInteriorPoint(ev, HostBlockKKT(ev), lb, ub, o).solve(np.stack([x0, x0]))
+    assert rb.status == ['tiny_step', 'tiny_step']
+    assert list(rb.iters) == [r.iters, r.iters]
+    assert rb.stats['watchdog']['tiny_steps'] == 2 * r.stats['watchdog']['tiny_steps']
