@@ -143,6 +143,23 @@ int ato_sparsity(const ato_handle* h, const int32_t** row_ptr, const int32_t** c
     return ATO_OK;
 }
 
+int ato_set_instance_spheres(ato_handle* h, const double* centres, int64_t stride) {
+    if (!h) return fail(ATO_ERR_ARG, "null handle");
+    if (centres && !h->L.p.has_spheres) return fail(ATO_ERR_ARG, "per-instance spheres need a problem with sphere rows");
+    if (centres && stride < 1) return fail(ATO_ERR_ARG, "bad sphere table stride");
+    for (ato::ProbD* p : {&h->pd, &h->pd_lf}) {
+        p->isph = centres;
+        p->isph_stride = centres ? stride : 0;
+    }
+    return ATO_OK;
+}
+
+int ato_sphere_rows(const ato_handle* h, int32_t* rows) {
+    if (!h || !rows) return fail(ATO_ERR_ARG, "null argument");
+    for (int q = 0; q < h->L.p.P; ++q) rows[q] = h->L.seg[((size_t)q * ato::NSEG + ato::SEG_SPHERE) * 2];
+    return ATO_OK;
+}
+
 int ato_bounds(const ato_handle* h, double* lbg, double* ubg) {
     if (!h) return fail(ATO_ERR_ARG, "null handle");
     for (size_t i = 0; i < h->L.lbg.size(); ++i) {

@@ -77,6 +77,7 @@ inline Dep tcos(Dep a) { return a; }
 
 struct DepW {
     Dep operator()(int col) const { return Dep::var(col); }
+    double par(long) const { return 0.0; }     // per-instance constants depend on nothing
 };
 
 // records (column of the entry, variable its value depends on) pairs
@@ -262,6 +263,7 @@ struct ColorW {
     const int32_t* color;
     int c;
     ATO_HD Dual<T, 1> operator()(int col) const { return Dual<T, 1>::seed(base(col), color[col] == c ? 0 : -1); }
+    ATO_HD double par(long i) const { return base.par(i); }
 };
 
 // gradient output of the seeded pass: only the tangent (grad^2 f v_c) is kept

@@ -229,16 +229,22 @@ struct DevWPaired {
     const char* w0;     // (char*) (w + chunk base)
     long Bb;
     uint32_t off;       // this lane's (clamped) instance byte offset
+    const double* pb;   // this lane's column of the per-instance constants (ProbD::isph), or NULL
+    long ps;
     __device__ __forceinline__ T operator()(int col) const {
         return *reinterpret_cast<const T*>(w0 + (long)col * Bb + off);
     }
+    __device__ __forceinline__ double par(long i) const { return pb[i * ps]; }
 };
 
 template <class T>
 struct DevW {
     const T* __restrict__ w;
     long ws;
+    const double* pb;   // this instance's column of the per-instance constants, or NULL
+    long ps;
     __device__ __forceinline__ T operator()(int col) const { return w[(long)col * ws]; }
+    __device__ __forceinline__ double par(long i) const { return pb[i * ps]; }
 };
 
 constexpr int WAVE = 64;
@@ -266,7 +272,7 @@ __global__ __launch_bounds__(WAVE) void k_eval(ProbD p, int B, int layout, const
         if (WJ) Jb = J + (long)b * p.nnz;
         if (WF) gfb = gf + (long)b * p.nw;
     }
-    const DevW<T> W{wb, st};
+    const DevW<T> W{wb, st, p.isph ? p.isph + b : nullptr, (long)p.isph_stride};
     DevSink<T, WJ, WG> s{Jb, gb, st, st, 0, 0};
     const GradOut<T> go{gfb, st, WF ? fpart + b : nullptr, B};
     run_unit<M, T, KS, WJ || WG, WF, UMASK>(p, ut[0], ut[1], ut[2], W, s, go);
@@ -322,7 +328,8 @@ __global__ __launch_bounds__(WAVE) ATO_EVAL_ATTR void k_eval_paired(ProbD p, int
     const int bl = (FULL || b < B) ? b : B - 1;     // clamped instance for loads
     const int32_t* ut = p.units + 4 * (unit0 + blockIdx.y);   // wave-uniform: scalar loads
     const long Bb = (long)B * sizeof(T);
-    const DevWPaired<T> W{reinterpret_cast<const char*>(w + chunk), Bb, (uint32_t)((bl - chunk) * sizeof(T))};
+    const DevWPaired<T> W{reinterpret_cast<const char*>(w + chunk), Bb, (uint32_t)((bl - chunk) * sizeof(T)),
+                          p.isph ? p.isph + bl : nullptr, (long)p.isph_stride};
     const GradOut<T> go{WF ? gf + bl : nullptr, (long)B, WF ? fpart + bl : nullptr, B};
     if constexpr (QUAD) {
         DevSinkQuad<WJ, WG> s;
@@ -390,7 +397,9 @@ __global__ __launch_bounds__(WAVE) void k_hess_dual(ProbD p, int B, int layout, 
     if (b >= B) return;
     const int32_t* ut = p.units + 4 * blockIdx.y;
     const bool il = layout == ATO_LAYOUT_INTERLEAVED;
-    const ColorW<double, DevW<double>> W{DevW<double>{il ? w + b : w + (long)b * p.nw, il ? (long)B : 1L}, color, c};
+    const ColorW<double, DevW<double>> W{DevW<double>{il ? w + b : w + (long)b * p.nw, il ? (long)B : 1L,
+                                                      p.isph ? p.isph + b : nullptr, (long)p.isph_stride},
+                                         color, c};
     DevTangentSink<double> s{dJ + b, (long)B, 0};
     const TangentGrad<double> go{dgf + b, (long)B};
     run_unit<M, Dual<double, 1>, 0, true, true, UMASK>(p, ut[0], ut[1], ut[2], W, s, go);

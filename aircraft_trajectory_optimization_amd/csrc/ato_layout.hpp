@@ -59,6 +59,7 @@ struct SinkTraits<PatSink> { static constexpr bool pattern = true; };
 
 struct OnesW {
     double operator()(int) const { return 1.0; }
+    double par(long) const { return 0.0; }
 };
 
 // model dispatch: calls f.template operator()<Model>() for the problem's model variant

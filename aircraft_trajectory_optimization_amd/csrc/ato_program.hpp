@@ -80,6 +80,11 @@ struct ProbD {
     const int32_t* units;      // [n_units][4]  (UnitKind, n, k, 0)
     int32_t n_units, pad_units;
     int32_t cls_off[4];        // unit classes [cls_off[c], cls_off[c+1]): tail, ODE, node/interval
+    // per-instance sphere centres (config 4's perturbed tubes; ato_set_instance_spheres): device
+    // [P][2][isph_stride] (dy, dn of node p for instance b at (2 p + c) isph_stride + b), read through
+    // the decision-vector accessor's par(); NULL: the shared table `spheres`
+    const double* isph;
+    int64_t isph_stride;
 };
 
 // nodes per interval: compile-time KS (specialised kernels for common K) or runtime p.K1
@@ -219,12 +224,17 @@ ATO_HD void seg_stage(const ProbD& p, int n, int k, const W& w, S& s) {
 }
 
 // obstacle tube: (y - dy)^2 + (n - dn)^2 <= r_avail^2  (mesh_obstacle.py:219-237)
+// (the upper bound is the shared table's r^2; with per-instance spheres the caller holds per-instance
+// bounds, ato_sphere_rows)
 template <class M, class T, int KS, class W, class S>
 ATO_HD void seg_sphere(const ProbD& p, int n, int k, const W& w, S& s) {
     const Cols<M> c{p.N, K1S(p)};
-    const double* sp = p.spheres + (long)(n * K1S(p) + k) * 3;
-    const T ey = w(c.z(n, k, 1)) - T(sp[0]);
-    const T en = w(c.z(n, k, 2)) - T(sp[1]);
+    const long node = (long)n * K1S(p) + k;
+    const double* sp = p.spheres + node * 3;
+    const double dy = p.isph ? w.par(2 * node) : sp[0];
+    const double dn = p.isph ? w.par(2 * node + 1) : sp[1];
+    const T ey = w(c.z(n, k, 1)) - T(dy);
+    const T en = w(c.z(n, k, 2)) - T(dn);
     s.jac(c.z(n, k, 1), T(2) * ey);
     s.jac(c.z(n, k, 2), T(2) * en);
     s.row(ey * ey + en * en, -ATO_INF, sp[2] * sp[2]);

@@ -106,7 +106,8 @@ EXPORTED_SYMBOLS = ('ato_create', 'ato_destroy', 'ato_sizes', 'ato_sparsity', 'a
                     'ato_mesh_create', 'ato_mesh_destroy', 'ato_mesh_signed_distance',
                     'ato_timing', 'ato_timing_read', 'ato_timing_stride', 'ato_last_error', 'ato_version',
                     'ato_kkt_create', 'ato_kkt_destroy', 'ato_kkt_reserve', 'ato_kkt_factor', 'ato_kkt_solve',
-                    'ato_kkt_residual', 'ato_kkt_residual_list') + IPM_SYMBOLS
+                    'ato_kkt_residual', 'ato_kkt_residual_list', 'ato_set_instance_spheres',
+                    'ato_sphere_rows') + IPM_SYMBOLS
 
 
 def library_path() -> str:
@@ -138,6 +139,8 @@ def declare(lib: ctypes.CDLL, prefix: str = 'ato') -> ctypes.CDLL:
         lib.ato_timing.argtypes = [vp, ctypes.c_int32]
         lib.ato_timing_read.argtypes = [vp, _c_double_p, _c_double_p, i32p]
         lib.ato_timing_stride.argtypes = [vp, ctypes.c_int32]
+        lib.ato_set_instance_spheres.argtypes = [vp, vp, ctypes.c_int64]
+        lib.ato_sphere_rows.argtypes = [vp, i32p]
         lib.ato_kkt_create.argtypes = [vp, ctypes.POINTER(vp)]
         lib.ato_kkt_destroy.argtypes = [vp]
         lib.ato_kkt_reserve.argtypes = [vp, ctypes.c_int32]
@@ -163,7 +166,8 @@ def declare(lib: ctypes.CDLL, prefix: str = 'ato') -> ctypes.CDLL:
             getattr(lib, fn).restype = ctypes.c_int
         for fn in ('ato_create', 'ato_destroy', 'ato_sizes', 'ato_sparsity', 'ato_bounds', 'ato_reserve',
                    'ato_eval', 'ato_eval_f32', 'ato_hess_sparsity', 'ato_hess_eval', 'ato_timing',
-                   'ato_timing_read', 'ato_timing_stride', 'ato_mesh_create', 'ato_mesh_destroy', 'ato_mesh_signed_distance'):
+                   'ato_timing_read', 'ato_timing_stride', 'ato_mesh_create', 'ato_mesh_destroy', 'ato_mesh_signed_distance',
+                   'ato_set_instance_spheres', 'ato_sphere_rows'):
             getattr(lib, fn).restype = ctypes.c_int
     return lib
 
@@ -301,6 +305,16 @@ class NativeProblem:
         self._check(self.lib.ato_bounds(self.handle, lb.ctypes.data_as(_c_double_p),
                                         ub.ctypes.data_as(_c_double_p)))
         return lb, ub
+
+    def set_instance_spheres(self, centres: int, stride: int):
+        ''' per-instance sphere centres: device pointer to [P][2][stride] doubles (0 clears) '''
+        self._check(self.lib.ato_set_instance_spheres(self.handle, centres or None, int(stride)))
+
+    def sphere_rows(self, P: int) -> np.ndarray:
+        ''' row index of every node's sphere row (-1: none) '''
+        rows = np.zeros(P, np.int32)
+        self._check(self.lib.ato_sphere_rows(self.handle, rows.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))))
+        return rows
 
     def reserve(self, max_batch: int):
         ''' allocate scratch for f reductions up to max_batch '''

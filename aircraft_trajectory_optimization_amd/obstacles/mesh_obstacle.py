@@ -132,6 +132,24 @@ class ObstacleFreeTube:
         ''' [P, 3] table consumed by the sphere rows of the HIP programs '''
         return np.array([self.sphere(s) for s in node_s], float)
 
+    def perturbed_tables(self, node_s: np.ndarray, seeds) -> np.ndarray:
+        '''
+        Config 4's batch of perturbed tubes (build-defined, the reference solves one tube):
+        instance b draws, with numpy.random.default_rng(b), for every sphere of the tube a radius
+        change U[-0.05, 0.05] and centre offsets (dy, dn) ~ N(0, 0.05^2); each node then takes its
+        nearest sphere as sphere() does. Returns (B, P, 3) tables of (dy, dn, available radius).
+        '''
+        _, idx = self.ball_kd_tree.query(np.asarray(node_s, float)[:, None])
+        nb = len(self.ball_r)
+        out = []
+        for b in seeds:
+            rng = np.random.default_rng(b)
+            dr = rng.uniform(-0.05, 0.05, nb)
+            dd = rng.normal(0.0, 0.05, (nb, 2))
+            r = np.maximum(self.ball_r + dr - self.collision_r, 0.01)
+            out.append(np.stack([self.ball_p[idx, 1] + dd[idx, 0], self.ball_p[idx, 2] + dd[idx, 1], r[idx]], axis=1))
+        return np.array(out, float)
+
     def get_vertex_objects(self, ubo=None) -> Dict[str, 'TubeDrawable']:
         ''' the drawables the reference's viewer adds for the tube (mesh_obstacle.py:239-275), as data:
         instance centres, scales and (planning tube) orientations '''

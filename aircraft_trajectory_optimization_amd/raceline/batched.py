@@ -42,6 +42,37 @@ class BatchedNLP:
         self.problem.reserve(B)
         self.row_ptr, self.col = self.problem.sparsity()
         self.lbg, self.ubg = self.problem.bounds()
+        self.isph = None          # per-instance sphere centres [2 P][B] (set_instance_spheres)
+
+    def set_instance_spheres(self, tables: Optional[np.ndarray]):
+        '''
+        Per-instance obstacle tubes (config 4): tables (B, P, 3) of (dy, dn, available radius) per
+        node, one ObstacleFreeTube.sphere_table per instance (mesh_obstacle.py:219-237). The centres go
+        to the device ([2 P][B], read by the sphere rows); lbg / ubg become per-instance (ng, B) arrays
+        with each instance's radius^2 in its sphere rows. None returns to the spec's shared table.
+        '''
+        if tables is None:
+            self.isph = None
+            self.lbg, self.ubg = self.problem.bounds()
+            return
+        if self.spec.sphere_table is None:
+            raise ValueError('per-instance spheres need a problem with sphere rows (spec.sphere_table)')
+        P = self.spec.P
+        T = np.asarray(tables, np.float64).reshape(self.batch, P, 3)
+        cen = np.ascontiguousarray(T[:, :, :2].reshape(self.batch, 2 * P).T)
+        self.isph = torch.as_tensor(cen, device=self.device)
+        rows = self.problem.sphere_rows(P)
+        lb, ub = self.problem.bounds()
+        self.lbg = np.repeat(lb[:, None], self.batch, axis=1)
+        self.ubg = np.repeat(ub[:, None], self.batch, axis=1)
+        has = rows >= 0
+        self.ubg[rows[has], :] = (T[:, has, 2] ** 2).T
+        self.sphere_rows = rows
+
+    def _bind_spheres(self):
+        ''' the handle may be shared (subset evaluators): point it at this batch's centres '''
+        if self.spec.sphere_table is not None:
+            self.problem.set_instance_spheres(self.isph.data_ptr() if self.isph is not None else 0, self.batch)
 
     @property
     def sizes(self) -> Tuple[int, int, int]:
@@ -59,6 +90,7 @@ class BatchedNLP:
     def evaluate(self, g: bool = True, jac: bool = True, cost: bool = True, stream=None):
         ''' launch the evaluation (asynchronous on `stream`, default the current torch stream) '''
         st = stream if stream is not None else torch.cuda.current_stream(self.device)
+        self._bind_spheres()
         self.problem.eval_ptrs(
             self.batch, self.w.data_ptr(),
             g=self.g.data_ptr() if g else 0,
@@ -83,6 +115,7 @@ class BatchedNLP:
         lam = lam.contiguous()
         sigma = sigma.contiguous()
         st = stream if stream is not None else torch.cuda.current_stream(self.device)
+        self._bind_spheres()
         self.problem.hess_eval_ptrs(self.batch, self.w.data_ptr(), lam.data_ptr(), sigma.data_ptr(),
                                     self.hess.data_ptr(), layout=self.layout, stream=st.cuda_stream)
         return self.hess

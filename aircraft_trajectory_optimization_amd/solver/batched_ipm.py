@@ -136,27 +136,53 @@ class BatchedDeviceEvaluator:
         self._toc(t)
         return out
 
-    def subset(self, count: int) -> '_SubsetDeviceEvaluator':
+    def set_instance_spheres(self, tables):
+        ''' per-instance obstacle tubes (BatchedNLP.set_instance_spheres): (B, P, 3) or None '''
+        self.bn.set_instance_spheres(tables)
+        self.tables = tables
+        self.lbg, self.ubg = self.bn.lbg, self.bn.ubg
+
+    def subset(self, count: int, cols=None) -> '_SubsetDeviceEvaluator':
         ''' an evaluator over `count` <= batch instances (its own [element][count] buffers, the same
-        library handle): the restoration phase iterates only the instances it restores '''
-        return _SubsetDeviceEvaluator(self, count)
+        library handle): the restoration phase iterates only the instances it restores. cols: their
+        columns in this evaluator (per-instance constants follow them); None: the first count '''
+        return _SubsetDeviceEvaluator(self, count, cols)
 
     def fork(self) -> 'BatchedDeviceEvaluator':
         ''' the same problem on a second library handle (a handle serves one thread at a time) '''
-        return BatchedDeviceEvaluator(self.spec, self.batch, self.device)
+        ev = BatchedDeviceEvaluator(self.spec, self.batch, self.device)
+        if getattr(self, 'tables', None) is not None:
+            ev.set_instance_spheres(self.tables)
+        return ev
 
 
 class _SubsetDeviceEvaluator:
-    def __init__(self, base: BatchedDeviceEvaluator, count: int):
+    def __init__(self, base, count: int, cols=None):
         if not 0 < count <= base.batch:
             raise ValueError('subset size out of range')
+        if isinstance(base, _SubsetDeviceEvaluator):       # a subset of a subset: columns of the root
+            if cols is not None:
+                cols = base.cols.index_select(0, torch.as_tensor(cols, device=base.device).reshape(-1))
+            else:
+                cols = base.cols[:count]
+            base = base.base
         self.base = base
         self.problem = base.bn.problem
         self.device, self.batch = base.device, int(count)
+        self.cols = (torch.arange(count, device=base.device) if cols is None
+                     else torch.as_tensor(cols, device=base.device).reshape(-1).long())
+        if len(self.cols) != count:
+            raise ValueError('subset columns do not match its size')
         self.n, self.m, self.nnz = base.n, base.m, base.nnz
         self.j_row_ptr, self.j_col = base.j_row_ptr, base.j_col
         self.h_row_ptr, self.h_col = base.h_row_ptr, base.h_col
         self.lbg, self.ubg = base.lbg, base.ubg
+        # per-instance sphere centres of these columns (config 4's perturbed tubes)
+        self.isph = None
+        if base.bn.isph is not None:
+            self.isph = base.bn.isph.index_select(1, self.cols).contiguous()
+            c = self.cols.cpu().numpy()
+            self.lbg, self.ubg = base.lbg[:, c], base.ubg[:, c]
         self.var_stage = base.var_stage
         opts = {'device': self.device, 'dtype': torch.float64}
         B = self.batch
@@ -167,9 +193,14 @@ class _SubsetDeviceEvaluator:
         self.f = torch.zeros(B, **opts)
         self.h = torch.zeros((len(self.h_col), B), **opts)
 
+    def _bind(self):
+        if self.base.spec.sphere_table is not None:
+            self.problem.set_instance_spheres(self.isph.data_ptr() if self.isph is not None else 0, self.batch)
+
     def eval(self, X: torch.Tensor):
         self.w.copy_(X)
         st = torch.cuda.current_stream(self.device)
+        self._bind()
         self.problem.eval_ptrs(self.batch, self.w.data_ptr(), g=self.g.data_ptr(), jac=self.jac.data_ptr(),
                                f=self.f.data_ptr(), grad_f=self.gf.data_ptr(), stream=st.cuda_stream)
         return self.f.clone(), self.g.clone(), self.gf.clone(), self.jac.clone()
@@ -177,17 +208,19 @@ class _SubsetDeviceEvaluator:
     def eval_fg(self, X: torch.Tensor):
         self.w.copy_(X)
         st = torch.cuda.current_stream(self.device)
+        self._bind()
         self.problem.eval_ptrs(self.batch, self.w.data_ptr(), g=self.g.data_ptr(), f=self.f.data_ptr(),
                                grad_f=self.gf.data_ptr(), stream=st.cuda_stream)
         return self.f.clone(), self.g.clone()
 
-    def subset(self, count: int) -> '_SubsetDeviceEvaluator':
-        return _SubsetDeviceEvaluator(self.base, count)
+    def subset(self, count: int, cols=None) -> '_SubsetDeviceEvaluator':
+        return _SubsetDeviceEvaluator(self, count, cols)
 
     def hess(self, X: torch.Tensor, lam: torch.Tensor, sigma: torch.Tensor) -> torch.Tensor:
         self.w.copy_(X)
         lam, sigma = lam.contiguous(), sigma.contiguous()
         st = torch.cuda.current_stream(self.device)
+        self._bind()
         self.problem.hess_eval_ptrs(self.batch, self.w.data_ptr(), lam.data_ptr(), sigma.data_ptr(),
                                     self.h.data_ptr(), stream=st.cuda_stream)
         return self.h.clone()
@@ -765,7 +798,7 @@ class BatchedInteriorPoint:
                     wd = dict(zip(wd.keys(), self._compact(sel, tuple(wd.values()))))
                     F = F.index_select(0, sel).contiguous()
                     cols = cols.index_select(0, sel)
-                    self.ev = keep['ev'].subset(n_live)
+                    self.ev = keep['ev'].subset(n_live, cols)
                     self.kkt = keep['kkt'].view(n_live)
                     B = self.B = n_live
                     sf, sg = self.sf, self.sg
@@ -1245,7 +1278,7 @@ class BatchedInteriorPoint:
         if not (hasattr(self.ev, 'subset') and hasattr(self.kkt, 'view')):
             return self._restore_full(R, x, g, mu, theta, F, nf)
         job = self._resto_prepare(R, x, g, mu, theta, F, nf)
-        xr_c, ok_c, stats, laps = self._resto_run(job, self.ev, self.kkt, self.vk)
+        xr_c, ok_c, stats, laps = self._resto_run(job, self.ev, self.kkt, self.vk, job['sel'])
         self._resto_merge_stats(stats, laps)
         sel = job['sel']
         xr = x.clone()
@@ -1274,7 +1307,7 @@ class BatchedInteriorPoint:
         return dict(R=int(len(sel)), sel=sel, view=view, x=x_c, mu=mu_c, mu_r=mu_r, pp=pp, nn=nn,
                     theta=theta.index_select(0, sel), F=F.index_select(0, sel), nf=nf.index_select(0, sel))
 
-    def _resto_run(self, job, ev_base, kkt_base, vk_outer):
+    def _resto_run(self, job, ev_base, kkt_base, vk_outer, cols):
         ''' the nested restoration solve of a prepared job on the given evaluator handle, KKT storage
         and outer kernels (current stream): returns (x [n, R] within the bounds, success [R],
         stats, laps) '''
@@ -1282,7 +1315,7 @@ class BatchedInteriorPoint:
         n, m, dev = self.n, self.m, self.dev
         view = job['view']
         Br = job['R']
-        ev_r = ev_base.subset(Br)
+        ev_r = ev_base.subset(Br, cols)    # cols: the restored columns in ev_base
         kkt_r = kkt_base.view(Br)
         view.ev, view.vk = ev_r, vk_outer
         structure = getattr(self, '_resto_structure', None)
@@ -1350,7 +1383,7 @@ class BatchedInteriorPoint:
             st = res['stream']
             with torch.cuda.stream(st):
                 st.wait_event(ready)
-                out = self._resto_run(job, res['ev'], res['kkt'], res['vk'])
+                out = self._resto_run(job, res['ev'], res['kkt'], res['vk'], job['orig'])
                 fin = torch.cuda.Event()
                 fin.record(st)
             return out, fin

@@ -147,6 +147,19 @@ int ato_hess_sparsity(ato_handle* h, int32_t* nnz, const int32_t** row_ptr, cons
 int ato_hess_eval(ato_handle* h, int32_t batch, int32_t layout, const double* w, const double* lam,
                   const double* sigma, double* hess, void* stream);
 
+/* Per-instance obstacle-tube sphere centres (config 4's perturbed tubes; the reference builds one
+ * ObstacleFreeTube per solve, mesh_obstacle.py:219-237, so a batch of perturbed tubes is a batch of
+ * problems that differ only in these constants). centres: DEVICE array [P][2][stride] of doubles,
+ * (dy, dn) of node p for instance b at index (2 p + c) * stride + b; it must stay valid while
+ * evaluations use it. Applies to ato_eval / ato_eval_f32 / ato_hess_eval until replaced; NULL
+ * returns to the descriptor's shared table. The rows' upper bounds (available radius^2) then
+ * differ per instance and are the caller's (ato_sphere_rows gives their row indices). Requires a
+ * problem with sphere rows (has_spheres). */
+int ato_set_instance_spheres(ato_handle* h, const double* centres, int64_t stride);
+
+/* Row index of each node's sphere row, rows[P] (-1: no sphere row at that node). */
+int ato_sphere_rows(const ato_handle* h, int32_t* rows);
+
 /* Triangle mesh of an obstacle environment (MeshObstacle, drone3d/obstacles/mesh_obstacle.py:18-161;
  * replaces trimesh.proximity.signed_distance / closest_point). vertices [nv][3], faces [nf][3]
  * (0-based triangles), host arrays copied at creation. */

@@ -25,6 +25,22 @@ class HostBatchEvaluator:
         self.lbg, self.ubg = self.h.lbg, self.h.ubg
         self.var_stage = self.h.var_stage
 
+    def set_instance_spheres(self, tables):
+        ''' per-instance obstacle tubes (BatchedDeviceEvaluator.set_instance_spheres) '''
+        self.tables = None if tables is None else np.asarray(tables, np.float64)
+        if tables is None:
+            self.h.hc.set_instance_spheres(None)
+            self.lbg, self.ubg = self.h.lbg, self.h.ubg
+            return
+        P = self.spec.P
+        T = self.tables.reshape(self.batch, P, 3)
+        self.h.hc.set_instance_spheres(T[:, :, :2].reshape(self.batch, 2 * P).T)
+        rows = self.h.hc.sphere_rows(P)
+        has = rows >= 0
+        self.lbg = np.repeat(np.asarray(self.h.lbg)[:, None], self.batch, axis=1)
+        self.ubg = np.repeat(np.asarray(self.h.ubg)[:, None], self.batch, axis=1)
+        self.ubg[rows[has], :] = (T[:, has, 2] ** 2).T
+
     def eval(self, X):
         g, J, f, gf = self.h.hc.eval(X.T.contiguous().numpy())
         t = lambda a: torch.as_tensor(np.ascontiguousarray(a.T))  # noqa: E731
@@ -34,9 +50,13 @@ class HostBatchEvaluator:
         H = self.h.hc.hess(X.T.contiguous().numpy(), lam.T.contiguous().numpy(), sigma.numpy())
         return torch.as_tensor(np.ascontiguousarray(H.T))
 
-    def subset(self, count):
+    def subset(self, count, cols=None):
         ''' the solver's compacted restoration batch (BatchedDeviceEvaluator.subset) '''
-        return HostBatchEvaluator(self.spec, count)
+        sub = HostBatchEvaluator(self.spec, count)
+        if getattr(self, 'tables', None) is not None:
+            c = np.arange(count) if cols is None else np.asarray(torch.as_tensor(cols).cpu()).reshape(-1)
+            sub.set_instance_spheres(self.tables[c])
+        return sub
 
 
 class HostBlockKKT:

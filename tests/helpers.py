@@ -94,6 +94,8 @@ class HostCheck:
         lib.atoh_hess_sparsity.argtypes = [vp, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)]
         lib.atoh_hess_pattern.argtypes = [vp, vp, vp]
         lib.atoh_hess_eval.argtypes = [vp, ctypes.c_int, vp, vp, vp, vp]
+        lib.atoh_set_instance_spheres.argtypes = [vp, vp, ctypes.c_long]
+        lib.atoh_sphere_rows.argtypes = [vp, vp]
         self.lib = lib
         self.holder = native.DescHolder(spec_dict)
         h = vp()
@@ -109,6 +111,19 @@ class HostCheck:
         self.lbg = np.zeros(self.ng)
         self.ubg = np.zeros(self.ng)
         lib.atoh_bounds(h, self.lbg.ctypes.data, self.ubg.ctypes.data)
+
+    def set_instance_spheres(self, centres):
+        ''' per-instance sphere centres: host [2 P][B] array (kept alive here) or None '''
+        self._isph = None if centres is None else np.ascontiguousarray(centres, np.float64)
+        ptr = self._isph.ctypes.data if self._isph is not None else None
+        stride = self._isph.shape[1] if self._isph is not None else 0
+        if self.lib.atoh_set_instance_spheres(self.h, ptr, stride) != 0:
+            raise RuntimeError(self.lib.atoh_last_error().decode())
+
+    def sphere_rows(self, P):
+        rows = np.zeros(P, np.int32)
+        self.lib.atoh_sphere_rows(self.h, rows.ctypes.data)
+        return rows
 
     def eval(self, W):
         ''' W: (B, nw) -> g (B, ng), J (B, nnz), f (B,), grad_f (B, nw) '''

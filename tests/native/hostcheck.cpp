@@ -38,7 +38,10 @@ template <class T>
 struct HostW {
     const T* w;
     long ws;
+    const double* pb = nullptr;   // per-instance sphere centres (ProbD::isph) of this instance
+    long ps = 0;
     T operator()(int col) const { return w[(long)col * ws]; }
+    double par(long i) const { return pb[i * ps]; }
 };
 
 thread_local std::string last_err;
@@ -81,6 +84,22 @@ int atoh_create(const ato_problem_desc* d, atoh_handle** out) {
 
 void atoh_destroy(atoh_handle* h) { delete h; }
 
+// per-instance sphere centres (ato_set_instance_spheres): host table [P][2][stride], NULL clears
+int atoh_set_instance_spheres(atoh_handle* h, const double* centres, long stride) {
+    if (centres && !h->L.p.has_spheres) {
+        last_err = "per-instance spheres need a problem with sphere rows";
+        return -1;
+    }
+    h->L.p.isph = centres;
+    h->L.p.isph_stride = centres ? stride : 0;
+    return 0;
+}
+
+// row index of every node's sphere row (-1: none)
+void atoh_sphere_rows(const atoh_handle* h, int32_t* rows) {
+    for (int q = 0; q < h->L.p.P; ++q) rows[q] = h->L.seg[((size_t)q * ato::NSEG + ato::SEG_SPHERE) * 2];
+}
+
 void atoh_sizes(const atoh_handle* h, int32_t* nw, int32_t* ng, int32_t* nnz) {
     *nw = h->L.p.nw;
     *ng = h->L.p.ng;
@@ -106,7 +125,7 @@ int atoh_eval(const atoh_handle* h, int B, const double* w, double* g, double* J
     bool ok = ato::with_model(p, [&]<class M>() {
         std::vector<double> fpart(p.N);
         for (int b = 0; b < B; ++b) {
-            HostW<double> W{w + (long)b * p.nw, 1};
+            HostW<double> W{w + (long)b * p.nw, 1, p.isph ? p.isph + b : nullptr, (long)p.isph_stride};
             HostSink<double> s{J ? J + (long)b * p.nnz : nullptr, g ? g + (long)b * p.ng : nullptr, 1, 1, 0, 0};
             const ato::GradOut<double> go{gf + (long)b * p.nw, 1, fpart.data(), 1};
             for (int u = 0; u < p.n_units; ++u) {
@@ -134,7 +153,7 @@ int atoh_eval_threads(const atoh_handle* h, int B, const double* w, double* g, d
         bool lok = ato::with_model(p, [&]<class M>() {
 #pragma omp for schedule(static)
             for (int b = 0; b < B; ++b) {
-                HostW<double> W{w + (long)b * p.nw, 1};
+                HostW<double> W{w + (long)b * p.nw, 1, p.isph ? p.isph + b : nullptr, (long)p.isph_stride};
                 HostSink<double> s{J ? J + (long)b * p.nnz : nullptr, g ? g + (long)b * p.ng : nullptr, 1, 1, 0, 0};
                 const ato::GradOut<double> go{gf + (long)b * p.nw, 1, fpart.data(), 1};
                 for (int u = 0; u < p.n_units; ++u) {
@@ -186,7 +205,9 @@ int atoh_hess_eval(atoh_handle* h, int B, const double* w, const double* lam, co
     bool ok = ato::with_model(p, [&]<class M>() {
         for (int b = 0; b < B; ++b) {
             for (int c = 0; c < HL.n_colors; ++c) {
-                ato::ColorW<double, HostW<double>> W{HostW<double>{w + (long)b * p.nw, 1}, HL.color.data(), c};
+                ato::ColorW<double, HostW<double>> W{
+                    HostW<double>{w + (long)b * p.nw, 1, p.isph ? p.isph + b : nullptr, (long)p.isph_stride},
+                    HL.color.data(), c};
                 HostTangentSink<double> s{dJ.data(), 0};
                 const ato::TangentGrad<double> go{dgf.data(), 1};
                 for (int u = 0; u < p.n_units; ++u) {

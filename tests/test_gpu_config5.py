@@ -123,7 +123,7 @@ def test_config5_dcm_warm_start_solve_matches_esp_on_device():
                for n in range(1, sp_.N))
     print(f'config 5 fig-8 50x4: ESP lap {re_.time:.9f} s ({re_.solve_time:.1f} s), DCM lap {rd.time:.9f} s '
           f'({rd.solve_time:.1f} s), gap {gap:.3e} s, DCM interval-start orthonormality {orth:.2e}')
-    assert gap <= 1e-4, gap
+    assert gap <= 1e-5, gap            # measured 4.2e-6 s (profiles/r04/config5/)
     assert orth <= 1e-8, orth
     nlp = oracle_nlp(**dict(CFG, use_dcm=True))
     c = kkt_certificate(nlp, x, sd.result.lam_g[:, 0].cpu().numpy(), sd.result.lam_x[:, 0].cpu().numpy(),

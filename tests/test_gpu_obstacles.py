@@ -6,8 +6,11 @@ Config 4 on the GPU (BASELINE configs[3]: obstacle avoidance, sphere rows of the
   * the drone 50 x 4 obstacle problem (obstacles.py track, r_c = 0.4, no gates, one sphere row per
     node from the product's tube) evaluated at full size for B = 4096 seeded cold starts on one
     GPU, against the oracle on instances spread over the batch (fp64, 1e-12 of the scale).
-Per-instance tube perturbations are not modelled: a library handle carries
-one sphere table, so the instances differ in their starts.
+  * config 4 as SURVEY 8(d) specifies it: per-instance perturbed tubes (ato_set_instance_spheres;
+    radius U[-0.05, 0.05], centres N(0, 0.05^2) per sphere, seeded per instance) at B = 4096 against
+    the oracle built with each instance's own tube, and a batched 50 x 4 obstacle DRONE solve over 64
+    perturbed tubes from the point-mass warm start (obstacles.py's use_ws path), whose converged
+    instances are KKT points of their own oracle NLPs.
 '''
 import numpy as np
 import pytest
@@ -81,3 +84,90 @@ def test_obstacle_drone_full_size_b4096_matches_oracle():
         Jv = np.stack([np.add.reduceat(J[b] * V[bn.col, j], bn.row_ptr[:-1]) for j in range(2)], axis=1)
         _close(Jv, nlp.jvp(W[b], V), 1e-11)
     assert int(np.isin(nlp.ubg, table[:, 2] ** 2).sum()) >= spec.P     # one sphere row per node
+
+
+def test_config4_perturbed_tubes_b4096_match_oracle():
+    from aircraft_trajectory_optimization_amd.raceline.batched import BatchedNLP
+    from aircraft_trajectory_optimization_amd.raceline.instances import seeded_instances
+    from aircraft_trajectory_optimization_amd.obstacles.mesh_obstacle import MeshObstacle
+    from aircraft_trajectory_optimization_amd.tracks import make_line
+    from oracle.ref_transcription import RefNLP
+    from tests.helpers import oracle_line
+    spec, table = _obstacle_problem()
+    B = 4096
+    tube = MeshObstacle().compute_plannning_tube(make_line('obstacles'), spec.node_s, 0.4)
+    tables = tube.perturbed_tables(spec.node_s, range(B))
+    np.testing.assert_array_equal(tube.sphere_table(spec.node_s), table)
+    W, _, _ = seeded_instances(spec, range(B))
+    bn = BatchedNLP(spec, B)
+    bn.set_instance_spheres(tables)
+    nw, ng, _ = bn.sizes
+    bn.set_w(W)
+    bn.evaluate()
+    g, J, f, gf = bn.results()
+    line = oracle_line('obstacles', True)
+    rng = np.random.default_rng(0)
+    for b in (0, 63, 64, 2047, 4095):
+        nlp = RefNLP(line, 'drone', 'parametric', 50, 4, veh={'use_quat': True, 'global_r': True,
+                                                               'collision_radius': 0.4},
+                     fixed_gates=[], spheres=tables[b])
+        np.testing.assert_array_equal(bn.lbg[:, b], nlp.lbg)
+        np.testing.assert_array_equal(bn.ubg[:, b], nlp.ubg)
+        _close(g[b], nlp.g(W[b]))
+        _close(f[b], nlp.f(W[b]))
+        V = rng.standard_normal((nw, 2))
+        Jv = np.stack([np.add.reduceat(J[b] * V[bn.col, j], bn.row_ptr[:-1]) for j in range(2)], axis=1)
+        _close(Jv, nlp.jvp(W[b], V), 1e-11)
+
+
+def test_config4_batched_obstacle_drone_solve_over_perturbed_tubes():
+    import time
+    from aircraft_trajectory_optimization_amd.obstacles.mesh_obstacle import MeshObstacle
+    from aircraft_trajectory_optimization_amd.pytypes import DroneConfig, PointConfig
+    from aircraft_trajectory_optimization_amd.raceline.config import ParametricRacelineConfig
+    from aircraft_trajectory_optimization_amd.raceline.problem import ProblemSpec
+    from aircraft_trajectory_optimization_amd.raceline.warmstart import drone_guess
+    from aircraft_trajectory_optimization_amd.solver.batched_ipm import device_solver
+    from aircraft_trajectory_optimization_amd.solver.ipm import IPMOptions
+    from aircraft_trajectory_optimization_amd.tracks import make_line
+    from oracle.ref_transcription import RefNLP
+    from tests.helpers import kkt_certificate, oracle_line
+    line = make_line('obstacles')
+    line.config.gate_s = None
+    cfg = ParametricRacelineConfig(verbose=False, N=50, K=4)
+    cfg.closed = True
+    cfg.fixed_gates = []
+    pveh = PointConfig(global_r=True, collision_radius=0.4)
+    dveh = DroneConfig(global_r=True, use_quat=True, collision_radius=0.4)
+    probe = ProblemSpec(line, cfg.copy(), pveh, 'parametric')
+    tube = MeshObstacle().compute_plannning_tube(line, probe.node_s, 0.4)
+    table = tube.sphere_table(probe.node_s)
+    # obstacles.py's warm start: the point-mass obstacle raceline on the (unperturbed) tube
+    pspec = ProblemSpec(line, cfg.copy(), pveh, 'parametric', sphere_table=table)
+    pres = device_solver(pspec, 1, pspec.lbw[None], pspec.ubw[None], IPMOptions(max_iter=1000)).solve(pspec.w0[None])
+    assert pres.status[0] == 'optimal', pres.status
+    dprov = ProblemSpec(line, cfg.copy(), dveh, 'parametric', sphere_table=table)
+    w0, lbw, ubw, flip, wraps = drone_guess(dprov, pspec, pres.x[:, 0].cpu().numpy())
+    dspec = ProblemSpec(line, cfg.copy(), dveh, 'parametric', quat_flip=flip, euler_wraps=wraps, sphere_table=table)
+    B = 64
+    tables = tube.perturbed_tables(dspec.node_s, range(B))
+    solver = device_solver(dspec, B, lbw, ubw, IPMOptions(max_iter=1000))
+    solver.ev.set_instance_spheres(tables)
+    t0 = time.time()
+    res = solver.solve(np.repeat(w0[None], B, axis=0))
+    torch.cuda.synchronize()
+    ok = [b for b, st in enumerate(res.status) if st in ('optimal', 'acceptable')]
+    laps = res.x[:dspec.N].sum(0).cpu().numpy()
+    print(f'config 4, 64 perturbed tubes: {time.time() - t0:.1f} s, statuses',
+          {s: res.status.count(s) for s in sorted(set(res.status))},
+          f'lap {laps[ok].min():.4f} .. {laps[ok].max():.4f} s' if ok else '')
+    assert len(ok) >= 0.9 * B, res.status
+    x = res.x.cpu().numpy()
+    lg, lx = res.lam_g.cpu().numpy(), res.lam_x.cpu().numpy()
+    oline = oracle_line('obstacles', True)
+    for b in ok[::8]:
+        nlp = RefNLP(oline, 'drone', 'parametric', 50, 4, veh={'use_quat': True, 'global_r': True,
+                                                                'collision_radius': 0.4},
+                     fixed_gates=[], spheres=tables[b], quat_flip=flip)
+        c = kkt_certificate(nlp, x[:, b], lg[:, b], lx[:, b], lbw, ubw)
+        assert c['primal'] <= 1e-5 and c['dual'] <= 1e-6 and c['compl'] <= 1e-6, (b, c)

@@ -73,7 +73,7 @@ class _Toy:
             return 2 * sigma[None, :].expand(2, -1).clone()
         return np.full(2, 2.0 * sigma)
 
-    def subset(self, count):
+    def subset(self, count, cols=None):
         return _Toy(count)
 
 
