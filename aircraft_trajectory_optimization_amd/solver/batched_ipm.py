@@ -40,7 +40,8 @@ from typing import Dict, List, Optional
 import numpy as np
 import torch
 
-from aircraft_trajectory_optimization_amd.solver.ipm import INF, IPMOptions
+from aircraft_trajectory_optimization_amd.solver.ipm import DEG_UNKNOWN, DEG_YES, INF, IPMOptions, \
+    degeneracy_update_cols
 
 RUNNING, OPTIMAL, ACCEPTABLE, MAX_ITER, LS_FAILED, KKT_FAILED, STOPPED, INACTIVE, TINY_STEP = range(9)
 STATUS_NAMES = {RUNNING: 'running', OPTIMAL: 'optimal', ACCEPTABLE: 'acceptable', MAX_ITER: 'max_iter',
@@ -109,30 +110,27 @@ class BatchedDeviceEvaluator:
             e.record()
             self._events.append((start, e))
 
+    # Evaluations write straight into fresh output tensors and read X in place (no staging copies:
+    # the caching allocator orders any reuse of these blocks after the launch on the same stream)
     def eval(self, X: torch.Tensor):
         t = self._tic()
-        self.bn.w.copy_(X)
-        self.bn.evaluate()
+        out = _eval_into(self.bn.problem, self.bn, self.batch, X, self.n, self.m, self.nnz, True)
         self.counts['eval'] += 1
-        out = self.bn.f.clone(), self.bn.g.clone(), self.bn.grad_f.clone(), self.bn.jac.clone()
         self._toc(t)
         return out
 
     def eval_fg(self, X: torch.Tensor):
         ''' f and g only (no Jacobian written): the line search's trial points '''
         t = self._tic()
-        self.bn.w.copy_(X)
-        self.bn.evaluate(jac=False)
+        f, g, _, _ = _eval_into(self.bn.problem, self.bn, self.batch, X, self.n, self.m, self.nnz, False)
         self.counts['eval'] += 1
-        out = self.bn.f.clone(), self.bn.g.clone()
         self._toc(t)
-        return out
+        return f, g
 
     def hess(self, X: torch.Tensor, lam: torch.Tensor, sigma: torch.Tensor) -> torch.Tensor:
         t = self._tic()
-        self.bn.w.copy_(X)
         self.counts['hess'] += 1
-        out = self.bn.hessian(lam.contiguous(), sigma.contiguous()).clone()
+        out = _hess_into(self.bn.problem, self.bn, self.batch, X, lam, sigma, len(self.h_col))
         self._toc(t)
         return out
 
@@ -154,6 +152,30 @@ class BatchedDeviceEvaluator:
         if getattr(self, 'tables', None) is not None:
             ev.set_instance_spheres(self.tables)
         return ev
+
+
+def _eval_into(problem, binder, B, X, n, m, nnz, jac):
+    ''' one ato_eval of the batch X [n, B] into new tensors: (f, g, grad f, J or None) '''
+    X = X.contiguous()
+    dev = X.device
+    f = torch.empty(B, dtype=torch.float64, device=dev)
+    g = torch.empty((m, B), dtype=torch.float64, device=dev)
+    gf = torch.empty((n, B), dtype=torch.float64, device=dev)
+    J = torch.empty((nnz, B), dtype=torch.float64, device=dev) if jac else None
+    st = torch.cuda.current_stream(dev)
+    binder._bind_spheres()
+    problem.eval_ptrs(B, X.data_ptr(), g=g.data_ptr(), jac=J.data_ptr() if jac else 0, f=f.data_ptr(),
+                      grad_f=gf.data_ptr(), stream=st.cuda_stream)
+    return f, g, gf, J
+
+
+def _hess_into(problem, binder, B, X, lam, sigma, nnz_h):
+    X, lam, sigma = X.contiguous(), lam.contiguous(), sigma.contiguous()
+    h = torch.empty((nnz_h, B), dtype=torch.float64, device=X.device)
+    binder._bind_spheres()
+    problem.hess_eval_ptrs(B, X.data_ptr(), lam.data_ptr(), sigma.data_ptr(), h.data_ptr(),
+                           stream=torch.cuda.current_stream(X.device).cuda_stream)
+    return h
 
 
 class _SubsetDeviceEvaluator:
@@ -184,46 +206,22 @@ class _SubsetDeviceEvaluator:
             c = self.cols.cpu().numpy()
             self.lbg, self.ubg = base.lbg[:, c], base.ubg[:, c]
         self.var_stage = base.var_stage
-        opts = {'device': self.device, 'dtype': torch.float64}
-        B = self.batch
-        self.w = torch.zeros((self.n, B), **opts)
-        self.g = torch.zeros((self.m, B), **opts)
-        self.jac = torch.zeros((self.nnz, B), **opts)
-        self.gf = torch.zeros((self.n, B), **opts)
-        self.f = torch.zeros(B, **opts)
-        self.h = torch.zeros((len(self.h_col), B), **opts)
-
-    def _bind(self):
+    def _bind_spheres(self):
         if self.base.spec.sphere_table is not None:
             self.problem.set_instance_spheres(self.isph.data_ptr() if self.isph is not None else 0, self.batch)
 
     def eval(self, X: torch.Tensor):
-        self.w.copy_(X)
-        st = torch.cuda.current_stream(self.device)
-        self._bind()
-        self.problem.eval_ptrs(self.batch, self.w.data_ptr(), g=self.g.data_ptr(), jac=self.jac.data_ptr(),
-                               f=self.f.data_ptr(), grad_f=self.gf.data_ptr(), stream=st.cuda_stream)
-        return self.f.clone(), self.g.clone(), self.gf.clone(), self.jac.clone()
+        return _eval_into(self.problem, self, self.batch, X, self.n, self.m, self.nnz, True)
 
     def eval_fg(self, X: torch.Tensor):
-        self.w.copy_(X)
-        st = torch.cuda.current_stream(self.device)
-        self._bind()
-        self.problem.eval_ptrs(self.batch, self.w.data_ptr(), g=self.g.data_ptr(), f=self.f.data_ptr(),
-                               grad_f=self.gf.data_ptr(), stream=st.cuda_stream)
-        return self.f.clone(), self.g.clone()
+        f, g, _, _ = _eval_into(self.problem, self, self.batch, X, self.n, self.m, self.nnz, False)
+        return f, g
 
     def subset(self, count: int, cols=None) -> '_SubsetDeviceEvaluator':
         return _SubsetDeviceEvaluator(self, count, cols)
 
     def hess(self, X: torch.Tensor, lam: torch.Tensor, sigma: torch.Tensor) -> torch.Tensor:
-        self.w.copy_(X)
-        lam, sigma = lam.contiguous(), sigma.contiguous()
-        st = torch.cuda.current_stream(self.device)
-        self._bind()
-        self.problem.hess_eval_ptrs(self.batch, self.w.data_ptr(), lam.data_ptr(), sigma.data_ptr(),
-                                    self.h.data_ptr(), stream=st.cuda_stream)
-        return self.h.clone()
+        return _hess_into(self.problem, self, self.batch, X, lam, sigma, len(self.h_col))
 
 
 def device_solver(spec, batch: int, lbx, ubx, options: Optional[IPMOptions] = None, device=None):
@@ -554,17 +552,26 @@ class BatchedInteriorPoint:
         good = ok & torch.isfinite(y).all(0) & (y.abs().amax(0) <= self.o.constr_mult_init_max)
         return torch.where(good[None, :], y, torch.zeros_like(y))
 
-    def _kkt_step(self, W, Js, Sx, Ss, rhs_x, rhs_s, rhs_y, mu, dwl, act):
+    def _kkt_step(self, W, Js, Sx, Ss, rhs_x, rhs_s, rhs_y, mu, dwl, act, start_dw=None, start_dc=None):
         '''
         Newton step with IPOPT's inertia correction, per instance. Returns
         (dx, ds, dy, delta_w, ok, ctx) where ctx holds what a second-order-correction solve
-        needs (the factors stay in the KKT storage).
+        needs (the factors stay in the KKT storage); the delta_c of the accepted factorisation is
+        left in self.last_dc. start_dw / start_dc: instances whose Hessian / Jacobian is
+        structurally degenerate (IPOPT) start perturbed.
         '''
         o = self.o
         n, m, B = self.n, self.m, self.B
         zeros = torch.zeros(B, dtype=torch.float64, device=self.dev)
         delta_c, delta_w = zeros.clone(), zeros.clone()
         first = torch.ones(B, dtype=torch.bool, device=self.dev)
+        if start_dc is not None:
+            delta_c = torch.where(start_dc, o.delta_c_base * mu ** o.kappa_c, delta_c)
+        if start_dw is not None:
+            dw_first0 = torch.where(dwl == 0, torch.full_like(dwl, o.delta_w_0),
+                                    torch.clamp(o.kappa_w_minus * dwl, min=o.delta_w_min))
+            delta_w = torch.where(start_dw, dw_first0, delta_w)
+            first = first & ~start_dw
         pend = act.clone()
         ok_all = torch.zeros(B, dtype=torch.bool, device=self.dev)
         sol = torch.zeros((n + m, B), dtype=torch.float64, device=self.dev)
@@ -572,6 +579,7 @@ class BatchedInteriorPoint:
         dx_used = torch.zeros((n, B), dtype=torch.float64, device=self.dev)
         dr_used = torch.zeros((m, B), dtype=torch.float64, device=self.dev)
         dw_out = zeros.clone()
+        dc_out = zeros.clone()
         pidx = _idx(pend)
         npass = 0
         tosolve = torch.zeros(B, dtype=torch.bool, device=self.dev)
@@ -619,6 +627,7 @@ class BatchedInteriorPoint:
                 dx_used = torch.where(g2, dx, dx_used)
                 dr_used = torch.where(g2, dr, dr_used)
                 dw_out = torch.where(good, delta_w, dw_out)
+                dc_out = torch.where(good, delta_c, dc_out)
                 tosolve = tosolve | good
                 pend = next_pass(pend & ~good, sing)
                 pidx = _idx(pend)
@@ -641,6 +650,7 @@ class BatchedInteriorPoint:
         dxs, dy = sol[:n], sol[n:]
         ds = (rhs_s + dy[self.iin]) / Ds_used
         ctx = (W, Js, dx_used, dr_used, Ds_used)
+        self.last_dc = dc_out
         return dxs, ds, dy, dw_out, ok_all, ctx
 
     # ------------------------------------------------------------------ solve
@@ -717,6 +727,9 @@ class BatchedInteriorPoint:
         n_resto = torch.zeros(B, dtype=torch.long, device=dev)
         # watchdog / tiny steps (solver/ipm.py): shortened-step counter, watchdog flag and trial count,
         # the tiny-step flag that forces a barrier decrease; wd: the stored watchdog points
+        hdeg = torch.full((B,), DEG_UNKNOWN, dtype=torch.long, device=dev)    # IPOPT's degeneracy test
+        jdeg = torch.full((B,), DEG_UNKNOWN, dtype=torch.long, device=dev)
+        diters = torch.zeros(B, dtype=torch.long, device=dev)
         ws_short = torch.zeros(B, dtype=torch.long, device=dev)
         in_wd = torch.zeros(B, dtype=torch.bool, device=dev)
         wd_trial = torch.zeros(B, dtype=torch.long, device=dev)
@@ -792,9 +805,9 @@ class BatchedInteriorPoint:
                     save(cols, x, y, zl, zu, status, iters, n_resto)
                     sel = torch.nonzero(live).reshape(-1)
                     (x, s, f, g, gf, jv, y, zl, zu, vl, vu, mu, tau, nf, dwl, n_acc, status, n_resto, own, waiting,
-                     iters, act, infl, ws_short, in_wd, wd_trial, tiny_flag) = self._compact(
+                     iters, act, infl, ws_short, in_wd, wd_trial, tiny_flag, hdeg, jdeg, diters) = self._compact(
                         sel, (x, s, f, g, gf, jv, y, zl, zu, vl, vu, mu, tau, nf, dwl, n_acc, status, n_resto, own,
-                              waiting, iters, act, infl, ws_short, in_wd, wd_trial, tiny_flag))
+                              waiting, iters, act, infl, ws_short, in_wd, wd_trial, tiny_flag, hdeg, jdeg, diters))
                     wd = dict(zip(wd.keys(), self._compact(sel, tuple(wd.values()))))
                     F = F.index_select(0, sel).contiguous()
                     cols = cols.index_select(0, sel)
@@ -887,7 +900,11 @@ class BatchedInteriorPoint:
                     rhs_s = -(gs - y[self.iin])
                     rhs_y = -r
                 laps.lap('rhs')
-                dx, ds, dy, delta_w, ok, ctx = self._kkt_step(W, Js, Sx, Ss, rhs_x, rhs_s, rhs_y, mu, dwl, act)
+                testing = act & ((hdeg == DEG_UNKNOWN) | (jdeg == DEG_UNKNOWN))
+                dx, ds, dy, delta_w, ok, ctx = self._kkt_step(W, Js, Sx, Ss, rhs_x, rhs_s, rhs_y, mu, dwl, act,
+                                                              start_dw=hdeg == DEG_YES, start_dc=jdeg == DEG_YES)
+                hdeg, jdeg, diters = degeneracy_update_cols(hdeg, jdeg, diters, self.last_dc > 0, delta_w > 0,
+                                                            o.degen_iters_max, testing & ok)
                 laps.lap('kkt_other')
                 kfail = act & ~ok
                 # IPOPT: no direction inside the watchdog -> back to the watchdog point (below)
@@ -936,17 +953,22 @@ class BatchedInteriorPoint:
                 dirs = {'dx': dx, 'ds': ds, 'dy': dy, 'dzl': dzl, 'dzu': dzu, 'dvl': dvl, 'dvu': dvu}
                 nosoc = torch.zeros_like(act)
                 wdm = torch.zeros_like(act)
+                any_kwd = any_wd = False
                 if wd_on:
                     start = act & ~tiny & ~in_wd & ~kwd & (ws_short >= o.watchdog_shortened_iter_trigger)
-                    cur = {'x': x, 's': s, 'y': y, 'zl': zl, 'zu': zu, 'vl': vl, 'vu': vu, **dirs,
-                           'alpha_max': alpha_max, 'alpha_z': alpha_z, 'theta': theta, 'phi': phi, 'gphi_d': gphi_d}
-                    if not wd:
-                        wd = {k: torch.zeros_like(cur[k]) for k in WD_VECS + WD_SCAL}
-                    wd = {k: torch.where(start[None, :] if v.dim() == 2 else start, cur[k], v) for k, v in wd.items()}
-                    in_wd = in_wd | start
-                    wd_trial = torch.where(start, torch.zeros_like(wd_trial), wd_trial)
-                    wdst[0] += start.sum()
-                    wdm = act & in_wd
+                    wdm = act & (in_wd | start)
+                    any_start, any_kwd, any_wd = torch.stack([start.any(), kwd.any(), wdm.any()]).tolist()
+                    if any_start:
+                        cur = {'x': x, 's': s, 'y': y, 'zl': zl, 'zu': zu, 'vl': vl, 'vu': vu, **dirs,
+                               'alpha_max': alpha_max, 'alpha_z': alpha_z, 'theta': theta, 'phi': phi,
+                               'gphi_d': gphi_d}
+                        if not wd:
+                            wd = {k: torch.zeros_like(cur[k]) for k in WD_VECS + WD_SCAL}
+                        wd = {k: torch.where(start[None, :] if v.dim() == 2 else start, cur[k], v)
+                              for k, v in wd.items()}
+                        in_wd = in_wd | start
+                        wd_trial = torch.where(start, torch.zeros_like(wd_trial), wd_trial)
+                        wdst[0] += start.sum()
 
                 def revert(msk):
                     # stop the watchdog of the masked columns: their iterate and direction go back to the
@@ -981,13 +1003,11 @@ class BatchedInteriorPoint:
                                                    torch.full_like(t1, o.gamma_theta)))
                     return o.alpha_min_frac * amin
 
-                any_kwd = wd_on and bool(kwd.any())
                 if any_kwd:
                     revert(kwd)
                 dx, ds, dy, dzl, dzu, dvl, dvu = (dirs[k] for k in ('dx', 'ds', 'dy', 'dzl', 'dzu', 'dvl', 'dvu'))
                 alpha_min = alpha_min_of(theta, gphi_d)
                 alpha = torch.where(kwd, alpha_max * 0.5, alpha_max) if any_kwd else alpha_max.clone()
-                any_wd = wd_on and bool(wdm.any())
                 wd_succ = torch.zeros_like(act)
                 wd_cols = wdm.clone()
                 pend = act.clone()

@@ -12,8 +12,14 @@ IPOPT's default options:
   * monotone (Fiacco-McCormick) barrier: mu0 = 0.1, kappa_mu = 0.2, theta_mu = 1.5,
     kappa_eps = 10, tau = max(0.99, 1 - mu), linear damping 1e-5 of one-sided bounds
   * Newton step on the primal-dual system with the slack block eliminated; regularisation
-    delta_w / delta_c by IPOPT's rules; the KKT factorisation gives no inertia here, so the
-    inertia-free curvature test (Chiang & Zavala 2016) decides when delta_w must grow
+    delta_w / delta_c by IPOPT's rules (PDPerturbationHandler), including its structural
+    degeneracy test: while undetermined, every iteration first tries delta_w = delta_c = 0; an
+    iteration that needs no perturbation marks the Hessian and the Jacobian non-degenerate for
+    good, and after degen_iters_max (3) iterations that needed one, the Hessian (delta_w > 0) or the
+    Jacobian (delta_c > 0) is declared degenerate: its perturbation then starts at
+    max(delta_w_min, kappa_w^- delta_w_last) (resp. delta_c > 0) without the unperturbed attempt.
+    Without the stage structure (no inertia from the sparse LU) the inertia-free curvature test
+    (Chiang & Zavala 2016) decides when delta_w must grow
   * filter line search with switching / Armijo conditions and second-order corrections
   * convergence on the scaled optimality error E_0 <= tol (1e-8) plus IPOPT's unscaled
     dual / constraint / complementarity limits; "acceptable" level 1e-6 for 15 iterations
@@ -91,6 +97,7 @@ class IPMOptions:
     kappa_w_plus_bar: float = 100.0
     delta_c_base: float = 1e-8
     kappa_c: float = 0.25
+    degen_iters_max: int = 3
     honor_original_bounds: bool = True
     nlp_scaling: bool = True
     resto_penalty: float = 1000.0
@@ -117,6 +124,53 @@ class IPMResult:
     iters: int
     stats: dict = field(default_factory=dict)
     history: List[dict] = field(default_factory=list)
+
+
+DEG_UNKNOWN, DEG_NO, DEG_YES = 0, 1, 2
+
+
+def degeneracy_update(hdeg, jdeg, diters, dc_pos, dw_pos, iters_max):
+    '''
+    IPOPT's structural-degeneracy test (PDPerturbationHandler::finalize_test) after an iteration
+    whose perturbation was tested from zero: (hdeg, jdeg, diters) updated from whether the accepted
+    factorisation needed delta_c > 0 / delta_w > 0
+    '''
+    if not dc_pos and not dw_pos:         # no perturbation needed: nothing is degenerate
+        return (DEG_NO if hdeg == DEG_UNKNOWN else hdeg), (DEG_NO if jdeg == DEG_UNKNOWN else jdeg), diters
+    if dw_pos and not dc_pos:
+        jdeg = DEG_NO if jdeg == DEG_UNKNOWN else jdeg
+        if hdeg == DEG_UNKNOWN:
+            diters += 1
+            if diters >= iters_max:
+                hdeg = DEG_YES
+        return hdeg, jdeg, diters
+    if dc_pos and not dw_pos:
+        hdeg = DEG_NO if hdeg == DEG_UNKNOWN else hdeg
+        if jdeg == DEG_UNKNOWN:
+            diters += 1
+            if diters >= iters_max:
+                jdeg = DEG_YES
+        return hdeg, jdeg, diters
+    diters += 1
+    if diters >= iters_max:
+        hdeg = DEG_YES if hdeg == DEG_UNKNOWN else hdeg
+        jdeg = DEG_YES if jdeg == DEG_UNKNOWN else jdeg
+    return hdeg, jdeg, diters
+
+
+def degeneracy_update_cols(hdeg, jdeg, diters, dc_pos, dw_pos, iters_max, testing):
+    ''' degeneracy_update per column (torch tensors); only the `testing` columns change '''
+    import torch
+    unk_h, unk_j = hdeg == DEG_UNKNOWN, jdeg == DEG_UNKNOWN
+    none = testing & ~dc_pos & ~dw_pos
+    only_w, only_c, both = testing & dw_pos & ~dc_pos, testing & dc_pos & ~dw_pos, testing & dc_pos & dw_pos
+    diters = torch.where((only_w & unk_h) | (only_c & unk_j) | both, diters + 1, diters)
+    reach = diters >= iters_max
+    hdeg = torch.where(((none | only_c) & unk_h), torch.full_like(hdeg, DEG_NO),
+                       torch.where((only_w | both) & unk_h & reach, torch.full_like(hdeg, DEG_YES), hdeg))
+    jdeg = torch.where(((none | only_w) & unk_j), torch.full_like(jdeg, DEG_NO),
+                       torch.where((only_c | both) & unk_j & reach, torch.full_like(jdeg, DEG_YES), jdeg))
+    return hdeg, jdeg, diters
 
 
 def _lower_to_full(n, row_ptr, col, vals):
@@ -280,6 +334,8 @@ class InteriorPointSolver:
         history = []
         status = 'max_iter'
         it = 0
+        hdeg = jdeg = DEG_UNKNOWN      # structural degeneracy of the Hessian / the Jacobian (IPOPT)
+        diters = 0
         ws_short = 0              # consecutive accepted steps shorter than alpha_max (watchdog trigger)
         wd = None                 # watchdog point and direction while the watchdog is active
         tiny_flag = False         # the last step was tiny: force a barrier decrease
@@ -334,7 +390,12 @@ class InteriorPointSolver:
             rhs_x = -(gx + J.T @ y)
             rhs_s = -(gs - y[iin])
             rhs_y = -r
-            step = self._kkt(W, J, Sx, Ss, rhs_x, rhs_s, rhs_y, iin, mu, delta_w_last)
+            testing = hdeg == DEG_UNKNOWN or jdeg == DEG_UNKNOWN
+            step = self._kkt(W, J, Sx, Ss, rhs_x, rhs_s, rhs_y, iin, mu, delta_w_last,
+                             start_dw=hdeg == DEG_YES, start_dc=jdeg == DEG_YES)
+            if testing and step is not None:
+                hdeg, jdeg, diters = degeneracy_update(hdeg, jdeg, diters, self._last_dc > 0, step[3] > 0,
+                                                       o.degen_iters_max)
             if step is None and wd is not None:
                 # IPOPT: no direction inside the watchdog -> back to the watchdog point, and the line
                 # search continues along its stored direction
@@ -611,20 +672,26 @@ class InteriorPointSolver:
             return x
         return solve, inertia
 
-    def _kkt(self, W, J, Sx, Ss, rhs_x, rhs_s, rhs_y, iin, mu, delta_w_last):
+    def _kkt(self, W, J, Sx, Ss, rhs_x, rhs_s, rhs_y, iin, mu, delta_w_last, start_dw=False, start_dc=False):
         '''
         Solve the primal-dual system with the slack block eliminated,
             [W + Sx + dw I   J^T ] [dx]   [rhs_x                 ]
             [J              -D   ] [dy] = [rhs_y + rhs_s / (Ss+dw)]   (slack rows of D: 1/(Ss+dw) + dc)
         with IPOPT's inertia correction (IC-1 ... IC-6): the inertia must be (n, m, 0).
         Without inertia (sparse LU fallback) the curvature test of Chiang & Zavala decides.
-        Returns (dx, ds, dy, delta_w, solve) or None when delta_w exceeds its maximum.
+        Returns (dx, ds, dy, delta_w, solve) or None when delta_w exceeds its maximum (delta_c in
+        self._last_dc). start_dw / start_dc: the Hessian / Jacobian is structurally degenerate, the
+        first attempt is already perturbed.
         '''
         o = self.o
         n, m = self.n, self.m
-        delta_c = 0.0
+        delta_c = o.delta_c_base * mu ** o.kappa_c if start_dc else 0.0
         delta_w = 0.0
         first = True
+        if start_dw:
+            delta_w = o.delta_w_0 if delta_w_last == 0 else max(o.delta_w_min, o.kappa_w_minus * delta_w_last)
+            first = False
+        self._last_dc = delta_c
         while True:
             Ds_tot = Ss + delta_w
             D = np.full(m, delta_c)
@@ -664,6 +731,7 @@ class InteriorPointSolver:
                 delta_w = o.delta_w_0 if delta_w_last == 0 else max(o.delta_w_min, o.kappa_w_minus * delta_w_last)
             else:
                 delta_w *= o.kappa_w_plus_bar if delta_w_last == 0 else o.kappa_w_plus
+            self._last_dc = delta_c
             if delta_w > o.delta_w_max:
                 return None
 

@@ -169,6 +169,17 @@ def cpu_baseline(W, budget_s, spec_kw):
 
     r1, n1 = rate(1, budget_s / 4)
     rT, nT = rate(threads, budget_s / 4)
+    # the same SQP on every core: one cold start per worker process (tools/cpu_baseline.py, a child
+    # process that never touches the GPU), same wall-time budget as the 1-core solve
+    import subprocess
+    allc = None
+    try:
+        cp = subprocess.run([sys.executable, os.path.join(ROOT, 'tools', 'cpu_baseline.py'), '--workers', str(threads),
+                             '--budget', str(budget_s / 2), '--spec', json.dumps(spec_kw)],
+                            capture_output=True, text=True, timeout=budget_s * 4 + 120, check=False)
+        allc = json.loads(cp.stdout.strip().splitlines()[-1]) if cp.returncode == 0 else {'error': cp.stderr[-400:]}
+    except (subprocess.TimeoutExpired, ValueError, IndexError) as exc:
+        allc = {'error': repr(exc)}
     nlp = oracle_nlp(**spec_kw)
     t0 = time.perf_counter()
     for k in range(2):
@@ -181,7 +192,13 @@ def cpu_baseline(W, budget_s, spec_kw):
                       f'(cap {cap}) in {t_solve:.1f} s; twin evaluations: {nT} on {threads} threads, {n1} on 1 '
                       f'thread; numpy oracle 2 instances',
             'evals_per_s_1_thread': r1, 'evals_per_s_all_threads': rT, 'eval_threads': threads,
-            'numpy_oracle_evals_per_s': r_np}
+            'numpy_oracle_evals_per_s': r_np,
+            'sqp_all_cores': None if allc is None or 'error' in allc else
+            {'cores': allc['workers'], 'iterations_per_s': allc['iterations_per_s'], 'budget_s': allc['budget_s'],
+             'sample': f"{allc['workers']} worker processes, one config-3 cold start each (seeds 0..), the same "
+                       f"solver on the C++ twin + host block LDL^T, {allc['budget_s']:.0f} s each: "
+                       f"{allc['iterations']} iterations"},
+            'sqp_all_cores_error': allc.get('error') if allc else None}
 
 
 def main():

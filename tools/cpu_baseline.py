@@ -1,0 +1,62 @@
+'''
+CPU baseline of the batched SQP solve on ALL host cores (bench.py's cpu_baseline): one
+seeded cold start of the bench workload per worker process, each running the same interior-point
+algorithm (solver/ipm.py) with every evaluation by the C++ CPU twin of the programs
+(tests/native/hostcheck.cpp, g++ -O3) and the host block LDL^T KKT, single-threaded BLAS, for a fixed
+wall-time budget (a solve is not capped in iterations: it stops at the budget or at convergence).
+Prints one JSON line: iterations done per worker, aggregate SQP iterations/s, worker count.
+
+Run as its own process (no HIP initialisation here), e.g. from bench.py:
+    python tools/cpu_baseline.py --workers 16 --budget 20 --seeds 0 1 ...
+'''
+import argparse
+import json
+import os
+import sys
+import time
+from multiprocessing import get_context
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def _work(args):
+    seed, budget, spec_kw = args
+    import numpy as np
+    from aircraft_trajectory_optimization_amd.raceline.instances import seeded_instances
+    from aircraft_trajectory_optimization_amd.solver.ipm import InteriorPointSolver, IPMOptions
+    from aircraft_trajectory_optimization_amd.tracks import make_spec
+    from tests.helpers import HostEvaluator
+    spec = make_spec(**spec_kw)
+    ev = HostEvaluator(spec)
+    W, L, U = seeded_instances(spec, [seed])
+    t0 = time.perf_counter()
+    deadline = t0 + budget
+    r = InteriorPointSolver(ev, L[0], U[0], ev.lbg, ev.ubg, IPMOptions(max_iter=1000)).solve(
+        W[0], stop_check=lambda x: time.perf_counter() > deadline)
+    return {'seed': int(seed), 'iterations': int(r.iters), 'seconds': time.perf_counter() - t0,
+            'status': r.status, 'lap': float(np.sum(r.x[:spec.N]))}
+
+
+def run(workers, budget, seeds, spec_kw):
+    ctx = get_context('fork')
+    t0 = time.perf_counter()
+    with ctx.Pool(workers) as pool:
+        res = pool.map(_work, [(s, budget, spec_kw) for s in seeds])
+    wall = time.perf_counter() - t0
+    iters = sum(r['iterations'] for r in res)
+    secs = max(r['seconds'] for r in res)
+    return {'workers': workers, 'budget_s': budget, 'wall_s': wall, 'iterations': iters,
+            'iterations_per_s': iters / secs, 'per_worker': res}
+
+
+if __name__ == '__main__':
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--workers', type=int, default=int(os.environ.get('OMP_NUM_THREADS', '8')))
+    ap.add_argument('--budget', type=float, default=20.0)
+    ap.add_argument('--seeds', type=int, nargs='*', default=None)
+    ap.add_argument('--spec', default='{}', help='make_spec keyword arguments (JSON)')
+    a = ap.parse_args()
+    os.environ['OMP_NUM_THREADS'] = '1'          # one core per worker (BLAS inside the KKT blocks)
+    seeds = a.seeds if a.seeds else list(range(a.workers))
+    print(json.dumps(run(a.workers, a.budget, seeds, json.loads(a.spec))), flush=True)
