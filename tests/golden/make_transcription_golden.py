@@ -16,6 +16,9 @@ evaluated at seeded points:
     dg/dw and grad f(w) by complex-step differentiation of the same graph (exact to rounding).
 Each case is written to tests/golden/transcription/<name>.npz. Cases use the same keyword
 dictionary as tests/helpers.product_spec / oracle_nlp, so the tests compare like with like.
+The bench-size cases (DIRECTIONAL: the headline racetrack 50x4 and its obstacle variant) are too
+large for a dense Jacobian; they record g, f and the directional derivatives J V, grad f . V along
+four seeded unit directions V (complex step along each column of V), in tests/golden/directional/.
 
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_transcription_golden.py [--only NAME]
 '''
@@ -30,6 +33,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 OUT = os.path.join(HERE, 'transcription')
+OUT_DIR = os.path.join(HERE, 'directional')
 REFERENCE = os.environ.get('ATO_REFERENCE', '/root/reference')
 
 # scenario waypoints (data of scripts/race.py:12-14, scripts/fig_8.py:10-12, scripts/obstacles.py:14-16)
@@ -82,6 +86,12 @@ CASES = {
     # the reference refuses this guess (vertical drop between race gates 3 and 4: the heading jumps,
     # drone_raceline.py:223-235); the fixture records the refusal
     'race_global_ypr_warm_refused': dict(track='race', frame='global', N=21, K=2, use_quat=False, warm=4),
+}
+
+# bench-size cases: g, f and four complex-step directional derivatives (no dense Jacobian)
+DIRECTIONAL = {
+    'race_param_esp_N50K4': dict(track='race', N=50, K=4),
+    'race_param_esp_spheres_N50K4': dict(track='race', N=50, K=4, spheres=3),
 }
 
 
@@ -252,6 +262,44 @@ def evaluate_nlp(obj, W):
     return np.array(G), np.array(F), np.array(GF), np.array(JD)
 
 
+def evaluate_directional(obj, W, V):
+    ''' g, f by float evaluation and J V, grad f . V by complex step along the columns of V '''
+    import casadi as ca
+    w_sym = obj.nlp['w'].entries()
+    g_ent = ca.vertcat(obj.nlp['g']).entries()
+    f_ent = ca._to_mat(obj.nlp['J']).entries()
+    order = ca._topo(list(g_ent) + list(f_ent))
+    G, F, JV, GFV = [], [], [], []
+    hstep = 1e-100
+    for w in W:
+        val = ca.evaluate(order, {s.id: float(v) for s, v in zip(w_sym, w)})
+        G.append([float(val[e.id]) if isinstance(e, ca._N) else float(e) for e in g_ent])
+        F.append(float(val[f_ent[0].id]))
+        val = ca.evaluate(order, {s.id: w[j] + 1j * hstep * V[j] for j, s in enumerate(w_sym)})
+        JV.append([np.imag(val[e.id]) / hstep if isinstance(e, ca._N) else np.zeros(V.shape[1]) for e in g_ent])
+        GFV.append(np.imag(val[f_ent[0].id]) / hstep)
+    return np.array(G), np.array(F), np.array(JV), np.array(GFV)
+
+
+def make_directional(name, cfg, seed, ndir=4):
+    t0 = time.time()
+    obj, extra = build_reference(cfg)
+    w0 = np.array(obj.solver_w0, float)
+    N = obj.config.N
+    rng = np.random.default_rng(seed)
+    W = _points(w0, N, rng)
+    V = rng.standard_normal((len(w0), ndir))
+    V /= np.linalg.norm(V, axis=0)
+    G, F, JV, GFV = evaluate_directional(obj, W, V)
+    out = dict(cfg=np.array(json.dumps(cfg)), nw=np.array(len(w0)), ng=np.array(G.shape[1]),
+               w0=w0, lbw=np.array(obj.solver_lbw, float), ubw=np.array(obj.solver_ubw, float),
+               lbg=np.array(obj.solver_lbg, float), ubg=np.array(obj.solver_ubg, float),
+               W=W, V=V, G=G, F=F, JV=JV, GFV=GFV, **extra)
+    os.makedirs(OUT_DIR, exist_ok=True)
+    np.savez_compressed(os.path.join(OUT_DIR, f'{name}.npz'), **out)
+    print(f'{name}: nw={len(w0)} ng={G.shape[1]} ({time.time() - t0:.1f} s)', flush=True)
+
+
 def make_case(name, cfg, seed):
     t0 = time.time()
     obj, extra = build_reference(cfg)
@@ -395,6 +443,10 @@ def main():
         if a.only and a.only != name:
             continue
         make_case(name, cfg, seed=1000 + i)
+    for i, (name, cfg) in enumerate(DIRECTIONAL.items()):
+        if a.only and a.only != name:
+            continue
+        make_directional(name, cfg, seed=2000 + i)
 
 
 if __name__ == '__main__':

@@ -209,19 +209,25 @@ def var_stages(spec):
 
 # ------------------------------------------------------------------ golden fixtures of the reference's own transcription
 GOLDEN_DIR = os.path.join(REPO, 'tests', 'golden', 'transcription')
+DIRECTIONAL_DIR = os.path.join(REPO, 'tests', 'golden', 'directional')
 
 
-def golden_names():
-    return sorted(f[:-4] for f in os.listdir(GOLDEN_DIR) if f.endswith('.npz'))
+def golden_names(directory=GOLDEN_DIR):
+    return sorted(f[:-4] for f in os.listdir(directory) if f.endswith('.npz'))
 
 
-def golden_case(name):
+def directional_names():
+    ''' the bench-size fixtures: g, f, J V and grad f . V along seeded directions V '''
+    return golden_names(DIRECTIONAL_DIR)
+
+
+def golden_case(name, directory=GOLDEN_DIR):
     ''' (fixture dict, keyword arguments for product_spec / oracle_nlp) of one golden case
     (tests/golden/make_transcription_golden.py). Warm-started cases carry the closure sign /
     Euler wraps the reference derives from its first and last guessed attitude
     (drone_raceline.py:81-95). '''
     import json
-    d = dict(np.load(os.path.join(GOLDEN_DIR, f'{name}.npz')))
+    d = dict(np.load(os.path.join(directory, f'{name}.npz')))
     cfg = json.loads(str(d['cfg']))
     kw = {k: v for k, v in cfg.items() if k not in ('spheres', 'warm')}
     if 'spheres' in d:
@@ -233,6 +239,13 @@ def golden_case(name):
         else:
             kw['euler_wraps'] = float(np.round((last - first)[0] / 2 / np.pi))
     return d, kw
+
+
+def csr_matvec(row_ptr, col, vals, V):
+    ''' (CSR values) @ V for a dense V (n, k) '''
+    import scipy.sparse as sp
+    n = len(row_ptr) - 1
+    return sp.csr_matrix((vals, col, row_ptr), shape=(n, V.shape[0])) @ V
 
 
 def golden_jacobian(d, i):

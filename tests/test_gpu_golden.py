@@ -7,11 +7,15 @@ one batch of 2 instances.
 Tolerance (fp64): 1e-12 * max(1, max |reference|) per quantity (RK4 cases 1e-10: dual-number
 step Jacobians through four chained model evaluations; see the CPU test). fp32 (config 5
 precision): 2e-4 * max(1, max |reference|) for g and f on the collocation cases.
+
+The bench-size fixtures (tests/golden/directional: racetrack 50x4 with and without obstacle
+spheres) are checked through g, f, J V and grad f . V along their four seeded directions.
 '''
 import numpy as np
 import pytest
 
-from tests.helpers import csr_dense, golden_jacobian, golden_names
+from tests.helpers import (DIRECTIONAL_DIR, csr_dense, csr_matvec, directional_names, golden_case,
+                           golden_jacobian, golden_names, product_spec)
 from tests.test_golden_transcription_cpu import _spec
 
 pytestmark = pytest.mark.gpu
@@ -57,3 +61,18 @@ def test_ato_eval_f32_matches_reference_transcription(name):
     for i in range(len(d['W'])):
         _close(g[i], d['G'][i], 2e-4)
         _close(f[i], d['F'][i], 2e-4)
+
+
+@pytest.mark.parametrize('name', directional_names())
+def test_ato_eval_matches_reference_at_bench_size(name):
+    d, kw = golden_case(name, DIRECTIONAL_DIR)
+    spec = product_spec(**kw)
+    bn, (g, J, f, gf) = _evaluate(spec, d['W'], torch.float64)
+    assert bn.sizes[:2] == (int(d['nw']), int(d['ng']))
+    np.testing.assert_array_equal(bn.lbg, d['lbg'])
+    np.testing.assert_array_equal(bn.ubg, d['ubg'])
+    for i in range(len(d['W'])):
+        _close(g[i], d['G'][i], 1e-12)
+        _close(f[i], d['F'][i], 1e-12)
+        _close(csr_matvec(bn.row_ptr, bn.col, J[i], d['V']), d['JV'][i], 1e-12)
+        _close(gf[i] @ d['V'], d['GFV'][i], 1e-12)

@@ -31,7 +31,7 @@ run() {  # run <name> <seconds> <cmd...>
 
 for s in $STEPS; do
     case $s in
-        tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider ;;
+        tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider ${GPU_TESTS:-} ;;
         smoke) run smoke 300 python -c 'import __graft_entry__ as g; g.smoke()' ;;
         bench) run bench 900 python bench.py --steps 50 --warmup 10 ;;
         bench32) run bench_f32 300 python bench.py --steps 50 --warmup 10 --dtype f32 --no-cpu-baseline --no-solve ;;
