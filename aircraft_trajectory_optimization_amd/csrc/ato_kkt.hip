@@ -47,7 +47,11 @@ struct ato_kkt {
     int32_t *d_kres_ptr = nullptr, *d_kres_col = nullptr, *d_kres_src = nullptr;
     int64_t *d_l_off = nullptr, *d_cb_off = nullptr;
     int32_t* d_forder = nullptr;     // [F] fronts of every level grouped by kernel class (factor launches)
-    struct Seg { int start, count, cls; };
+    int32_t* d_n_sad = nullptr;      // [F] saddle fronts: nS, else 0 (NULL: the plan has none)
+    // cls: kernel class; saddle segments (cls SADDLE_CLS): nsm = the k_front_saddle variant, lds its
+    // shared-memory bytes, cls2 the Bunch-Kaufman class of the fallback launch
+    struct Seg { int start, count, cls, nsm = 0, cls2 = 0; size_t lds = 0; };
+    std::vector<char> level_sad;     // per level: holds saddle fronts
     std::vector<std::vector<Seg>> segs;   // per level: contiguous runs of d_forder of one class
     hipStream_t side = nullptr;      // second stream for the other classes of a level
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
@@ -109,6 +113,10 @@ static_assert(CH >= 2 * 32 * 8, "solve ring chunk smaller than the largest colum
 constexpr int MAXT = 8;                   // strips per front in ent_ptr
 constexpr double BK_ALPHA = 0.64038820320220756872767623199676;   // (1 + sqrt(17)) / 8
 constexpr int SRC_SHIFT = 29;
+constexpr int SAD_DONE = -1;              // sinfo.x of a saddle front factorised by k_front_saddle
+constexpr int SAD_FALLBACK = -2;          // ... left to the Bunch-Kaufman launch that follows
+constexpr int SADDLE_CLS = 200;           // kernel class of the saddle fronts
+constexpr double SAD_PIVOT_TOL = 1e-12;   // LU pivot of J_YX against max |J_YX| (tests/kkt_emulation.py)
 
 struct Plan {
     int n, m, dim, F;
@@ -126,6 +134,7 @@ struct Plan {
     const long long* cb_off;
     const int* sc_off;
     const int* forder;            // factor launches: front = forder[f0 + blockIdx.x]
+    const int* n_sad;             // [F] saddle fronts: nS (NULL: none)
     long long l_size, cb_size;
     int sc_size;
 };
@@ -362,6 +371,7 @@ __global__ __launch_bounds__(FTT) __attribute__((amdgpu_waves_per_eu(W))) void k
     const int bi = blockIdx.y;
     if (bi >= batch) return;
     const int b = list ? __builtin_amdgcn_readfirstlane(list[bi]) : bi;
+    if (P.n_sad && P.n_sad[f] > 0 && sinfo[(long long)b * P.F + f].x != SAD_FALLBACK) return;
     const int tid = threadIdx.x;
     const int ti = tid & 31, tj = tid >> 5;
     const int lane = tid & 63;
@@ -752,6 +762,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void k
     const int bi = blockIdx.y;
     if (bi >= batch) return;
     const int b = list ? __builtin_amdgcn_readfirstlane(list[bi]) : bi;
+    if (P.n_sad && P.n_sad[f] > 0 && sinfo[(long long)b * P.F + f].x != SAD_FALLBACK) return;
     const int tid = threadIdx.x;
     const int ti = tid & 15, tj = tid >> 4;
     const int lane = tid & 63;
@@ -1023,6 +1034,311 @@ size_t factor_s_lds() {
 
 
 // ------------------------------------------------------------------------------------------
+// Saddle fronts (solver/kkt_plan.py collocation_saddle): own = nS states X of nodes 1..K of an
+// interval, then their nS ODE defect rows Y; trailing T (controls, h, the anchor node, continuity
+// and path rows). With no row diagonal on Y (delta_c = 0) the block
+//     K_SS = [[H, J^T], [J, 0]]     (H = H_XX + diag_x, J = J_YX square)
+// has the inverse [[0, E], [E^T, G]], E = J^-1, G = -E^T H E, and the inertia (nS, nS, 0) whatever
+// H is; so it is eliminated WITHOUT a pivot chain across the workgroup:
+//   one wave: LU of J with partial pivoting, each lane one row in registers (the pivot row by
+//            readlane, no barrier), then E column by column (lane = column) from the LU in LDS;
+//   all:     HE = H E, G = -E^T (HE), W = K_TS K_SS^-1 = [B_y E^T, B_x E + B_y G] and the
+//            contribution block S = -W K_ST (lower triangle, mirrored: one writer per entry) as
+//            4x4 register-tiled LDS products.
+// Stored for the solve (the front's factor-column slice): K_SS^-1 (2nS x 2nS, symmetric) and W
+// (T x 2nS), sinfo = {SAD_DONE, doubles}. A J_YX pivot below SAD_PIVOT_TOL max|J_YX| or a nonzero
+// Y diagonal marks the (front, instance) SAD_FALLBACK instead, and the Bunch-Kaufman launch that
+// follows factorises exactly those (tests/kkt_emulation.py restates both paths).
+// ------------------------------------------------------------------------------------------
+// C[i][j] = sum_k a(i, k) b(k, j) over an M x N output in 4 x 4 register tiles (all threads);
+// out-of-range rows / columns read a clamped index and are not written
+template <class FA, class FB, class FC>
+__device__ __forceinline__ void sad_gemm(int M, int N, int K, FA a, FB b, FC c, int tid, int nthr, bool lower = false) {
+    const int tm = (M + 3) >> 2, tn = (N + 3) >> 2;
+    for (int tile = tid; tile < tm * tn; tile += nthr) {
+        const int i0 = (tile / tn) * 4, j0 = (tile % tn) * 4;
+        if (lower && j0 > i0) continue;
+        int ii[4], jj[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            ii[q] = min(i0 + q, M - 1);
+            jj[q] = min(j0 + q, N - 1);
+        }
+        double acc[4][4];
+#pragma unroll
+        for (int x = 0; x < 4; ++x)
+#pragma unroll
+            for (int y = 0; y < 4; ++y) acc[x][y] = 0.0;
+        for (int k = 0; k < K; ++k) {
+            double av[4], bv[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                av[q] = a(ii[q], k);
+                bv[q] = b(k, jj[q]);
+            }
+#pragma unroll
+            for (int x = 0; x < 4; ++x)
+#pragma unroll
+                for (int y = 0; y < 4; ++y) acc[x][y] = fma(av[x], bv[y], acc[x][y]);
+        }
+#pragma unroll
+        for (int x = 0; x < 4; ++x)
+#pragma unroll
+            for (int y = 0; y < 4; ++y)
+                if (i0 + x < M && j0 + y < N) c(i0 + x, j0 + y, acc[x][y]);
+    }
+}
+
+struct SadLds {      // shared-memory carve of one saddle front (runtime sizes)
+    double *J, *H, *B, *W, *rinv;
+    int *perm, *flag;
+    int ldn, ldb;
+};
+
+__device__ __forceinline__ SadLds sad_lds(double* smem, int nS, int T) {
+    SadLds L;
+    L.ldn = nS + 1;
+    L.ldb = 2 * nS + 1;
+    L.J = smem;
+    L.H = L.J + nS * L.ldn;
+    L.B = L.H + nS * L.ldn;
+    L.W = L.B + T * L.ldb;                      // also the H E scratch (nS x ldn)
+    L.rinv = L.W + max(T * L.ldb, nS * L.ldn);
+    L.perm = reinterpret_cast<int*>(L.rinv + nS);
+    L.flag = L.perm + nS;
+    return L;
+}
+
+inline size_t sad_lds_bytes(int nS, int T) {
+    const size_t d = (size_t)2 * nS * (nS + 1) + (size_t)T * (2 * nS + 1) + std::max((size_t)T * (2 * nS + 1),
+                                                                                     (size_t)nS * (nS + 1)) + nS;
+    return d * sizeof(double) + sizeof(int) * (nS + 1);
+}
+
+template <int NSM>
+__global__ __launch_bounds__(256) void k_front_saddle(Plan P, Vals V, int f0, int batch, const int* __restrict__ list,
+                                                      double* __restrict__ Lst, int2* __restrict__ sinfo,
+                                                      double* __restrict__ CB, int* __restrict__ inertia) {
+    static_assert(NSM <= 64, "one LU row per lane");
+    extern __shared__ double smem[];
+    const int f = P.forder[f0 + blockIdx.x];
+    const int bi = blockIdx.y;
+    if (bi >= batch) return;
+    const int b = list ? __builtin_amdgcn_readfirstlane(list[bi]) : bi;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int p0 = P.pos_ptr[f];
+    const int A = P.pos_ptr[f + 1] - p0;
+    const int nS = P.n_sad[f], n2 = 2 * nS, T = A - n2;
+    const SadLds L = sad_lds(smem, nS, T);
+    KST_DECL(f == ATO_KKT_STAMP_FRONT && blockIdx.y == 0)
+
+    // ---- assembly: J (Y x X), H (X x X), B = K_TS ([T][X | Y]); a Y diagonal (delta_c) -> fallback
+    for (int i = tid; i < 2 * nS * L.ldn + T * L.ldb; i += 256) L.J[i] = 0.0;
+    if (tid == 0) *L.flag = 0;
+    __syncthreads();
+    {
+        const int e0 = P.ent_ptr[f * MAXT], e1 = P.ent_ptr[(f + 1) * MAXT];
+        for (int e = e0 + tid; e < e1; e += 256) {
+            const int ep = P.ent_pos[e];
+            const int pa = ep >> 16, pb = ep & 0xffff;
+            const int2 sc = P.ent_src[e];
+            const double v = src_value(V, sc.x, b) + src_value(V, sc.y, b);
+            if (pa < nS) {
+                L.H[pa * L.ldn + pb] = v;
+                L.H[pb * L.ldn + pa] = v;
+            } else if (pa < n2) {
+                if (pb < nS) L.J[(pa - nS) * L.ldn + pb] = v;
+                else if (v != 0.0) *L.flag = 1;
+            } else if (pb < n2) {
+                L.B[(pa - n2) * L.ldb + pb] = v;
+            }
+        }
+    }
+    __syncthreads();
+
+    KST(0);                      // assembly
+    // ---- wave 0: LU of J with partial pivoting (lane i = row i), then E = J^-1 (lane c = column c)
+    if (tid < 64) {
+        double r[NSM];
+#pragma unroll
+        for (int j = 0; j < NSM; ++j) r[j] = (lane < nS && j < nS) ? L.J[lane * L.ldn + j] : 0.0;
+        double mx = 0.0;
+#pragma unroll
+        for (int j = 0; j < NSM; ++j) mx = fmax(mx, fabs(r[j]));
+        {   // max |J| over the wave (as a float key: the tolerance needs no more)
+            const unsigned km = wave_max_u32(__float_as_uint((float)mx));
+            mx = (double)__uint_as_float(km);
+        }
+        bool live = lane < nS;
+        int mystep = -1, pk = 0;
+        bool bad = false;
+#pragma unroll
+        for (int k = 0; k < NSM; ++k) {
+            if (k < nS) {
+                const unsigned key = wave_max_u32(live ? mag_key(r[k], lane) : 0u);
+                const int p = key ? 511 - (int)(key & 0x1FFu) : 0;
+                const double piv = readlane_f64(r[k], p);
+                bad = bad || !(fabs(piv) > SAD_PIVOT_TOL * mx) || key == 0u;
+                const double inv = 1.0 / piv;
+                const bool upd = live && lane != p;
+                const double l = r[k] * inv;
+                if (lane == p) {
+                    live = false;
+                    mystep = k;
+                }
+                if (lane == k) pk = p;
+                if (upd) r[k] = l;
+#pragma unroll
+                for (int j = k + 1; j < NSM; ++j) {
+                    const double u = readlane_f64(r[j], p);
+                    if (upd) r[j] = fma(-l, u, r[j]);
+                }
+                if (lane == 0) L.rinv[k] = inv;
+            }
+        }
+        // L \ U in pivot order: row k of P J = J[perm[k]] is held by the lane that pivoted at step k
+        if (lane < nS && mystep >= 0) {
+#pragma unroll
+            for (int j = 0; j < NSM; ++j)
+                if (j < nS) L.J[mystep * L.ldn + j] = r[j];
+            L.perm[lane] = pk;
+        }
+        if (bad && lane == 0) *L.flag = 1;
+        KST(1);                  // LU
+        __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");    // the LDS stores are visible to the wave
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (!bad) {
+            // column c of J^-1 = U^-1 L^-1 (P e_c): (P e_c)_k = 1 where perm[k] == c
+            double y[NSM];
+#pragma unroll
+            for (int k = 0; k < NSM; ++k) y[k] = (k < nS && L.perm[k] == lane) ? 1.0 : 0.0;
+#pragma unroll
+            for (int j = 0; j < NSM; ++j) {          // L y = P e_c (unit lower), column-oriented
+                if (j < nS) {
+#pragma unroll
+                    for (int k = j + 1; k < NSM; ++k)
+                        if (k < nS) y[k] = fma(-L.J[k * L.ldn + j], y[j], y[k]);
+                }
+            }
+#pragma unroll
+            for (int k = NSM - 1; k >= 0; --k) {     // U x = y, column-oriented
+                if (k < nS) {
+                    y[k] *= L.rinv[k];
+#pragma unroll
+                    for (int i = 0; i < k; ++i) y[i] = fma(-L.J[i * L.ldn + k], y[k], y[i]);
+                }
+            }
+            __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_wave_barrier();
+            if (lane < nS) {
+#pragma unroll
+                for (int i = 0; i < NSM; ++i)
+                    if (i < nS) L.J[i * L.ldn + lane] = y[i];    // E[i][c]
+            }
+        }
+    }
+    __syncthreads();
+    KST(2);                      // E = J^-1
+    int2* si = sinfo + (long long)b * P.F + f;
+    if (*L.flag) {
+        if (tid == 0) *si = make_int2(SAD_FALLBACK, 0);
+#ifdef ATO_KKT_STAMPS
+        if (tid == 0) atomicAdd(&g_kkt_stamps[14], 1ull);
+#endif
+        return;
+    }
+    // ---- HE = H E (scratch in W), G = -E^T (HE) (over H)
+    const double* J = L.J;
+    double* Hm = L.H;
+    double* Wm = L.W;
+    const double* Bm = L.B;
+    const int ldn = L.ldn, ldb = L.ldb;
+    sad_gemm(nS, nS, nS, [&](int i, int k) { return Hm[i * ldn + k]; }, [&](int k, int j) { return J[k * ldn + j]; },
+             [&](int i, int j, double v) { Wm[i * ldn + j] = v; }, tid, 256);
+    __syncthreads();
+    sad_gemm(nS, nS, nS, [&](int i, int k) { return J[k * ldn + i]; }, [&](int k, int j) { return Wm[k * ldn + j]; },
+             [&](int i, int j, double v) { Hm[i * ldn + j] = -v; }, tid, 256);
+    __syncthreads();
+    KST(3);                      // H E, G
+    // ---- W = [B_y E^T, B_x E + B_y G]
+    sad_gemm(T, nS, nS, [&](int t, int k) { return Bm[t * ldb + nS + k]; }, [&](int k, int i) { return J[i * ldn + k]; },
+             [&](int t, int i, double v) { Wm[t * ldb + i] = v; }, tid, 256);
+    sad_gemm(T, nS, n2, [&](int t, int k) { return Bm[t * ldb + k]; },
+             [&](int k, int i) { return k < nS ? J[k * ldn + i] : Hm[(k - nS) * ldn + i]; },
+             [&](int t, int i, double v) { Wm[t * ldb + nS + i] = v; }, tid, 256);
+    __syncthreads();
+    KST(4);                      // W
+    // ---- contribution block S = -W B^T (lower tiles, mirrored), K_SS^-1 and W to the factor slice
+    if (T > 0) {
+        double* cb = CB + (long long)b * P.cb_size + P.cb_off[f];
+        sad_gemm(T, T, n2, [&](int s, int k) { return Wm[s * ldb + k]; }, [&](int k, int t) { return Bm[t * ldb + k]; },
+                 [&](int s, int t, double v) {
+                     if (s >= t) {
+                         cb[(long long)s * T + t] = -v;
+                         cb[(long long)t * T + s] = -v;
+                     }
+                 }, tid, 256, true);
+    }
+    KST(5);                      // S
+    double* Lb = Lst + (long long)b * P.l_size + P.l_off[f];
+    for (int q = tid; q < n2 * n2; q += 256) {
+        const int i = q / n2, j = q - i * n2;
+        double v;
+        if (i < nS) v = j < nS ? 0.0 : J[i * ldn + (j - nS)];
+        else v = j < nS ? J[j * ldn + (i - nS)] : Hm[(i - nS) * ldn + (j - nS)];
+        Lb[q] = v;
+    }
+    for (int q = tid; q < T * n2; q += 256) {
+        const int t = q / n2, k = q - t * n2;
+        Lb[n2 * n2 + q] = Wm[t * ldb + k];
+    }
+    KST(6);                      // stores
+    KST_DUMP(1);
+    if (tid == 0) {
+        *si = make_int2(SAD_DONE, n2 * n2 + T * n2);
+        atomicAdd(&inertia[3 * b + 0], nS);
+        atomicAdd(&inertia[3 * b + 1], nS);
+    }
+}
+
+// solve of a saddle front: forward u = K_SS^-1 b_S (into x), contribution -W b_S to the parent;
+// backward x_S = u - W^T x_T. 128 threads; thread r < 2 nS owns row r of K_SS^-1 (symmetric, so
+// column r: coalesced reads), thread t < T row t of W
+__device__ void saddle_fwd(const Plan& P, int f, int b, const double* Lb, double* scf, double* xb, long long se,
+                           double* sbuf, int tid) {
+    const int p0 = P.pos_ptr[f], A = P.pos_ptr[f + 1] - p0, nS = P.n_sad[f], n2 = 2 * nS, T = A - n2;
+    for (int i = tid; i < n2; i += ST) sbuf[i] = xb[(long long)P.pos_index[p0 + i] * se];
+    __syncthreads();
+    double u = 0.0;
+    if (tid < n2) {
+        for (int k = tid < nS ? nS : 0; k < n2; ++k) u = fma(Lb[(long long)k * n2 + tid], sbuf[k], u);
+    }
+    const double* W = Lb + (long long)n2 * n2;
+    for (int t = tid; t < T; t += ST) {
+        double acc = 0.0;
+        for (int k = 0; k < n2; ++k) acc = fma(W[(long long)t * n2 + k], sbuf[k], acc);
+        scf[t] = -acc;
+    }
+    if (tid < n2) xb[(long long)P.pos_index[p0 + tid] * se] = u;
+}
+
+__device__ void saddle_bwd(const Plan& P, int f, int b, const double* Lb, double* xb, long long se, double* sbuf,
+                           int tid) {
+    const int p0 = P.pos_ptr[f], A = P.pos_ptr[f + 1] - p0, nS = P.n_sad[f], n2 = 2 * nS, T = A - n2;
+    for (int t = tid; t < T; t += ST) sbuf[t] = xb[(long long)P.pos_index[p0 + n2 + t] * se];
+    __syncthreads();
+    const double* W = Lb + (long long)n2 * n2;
+    for (int k = tid; k < n2; k += ST) {
+        double acc = 0.0;
+        for (int t = 0; t < T; ++t) acc = fma(W[(long long)t * n2 + k], sbuf[t], acc);
+        const long long o = (long long)P.pos_index[p0 + k] * se;
+        xb[o] = xb[o] - acc;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // solve
 // ------------------------------------------------------------------------------------------
 // Stream of the front's factor columns through a two-slot LDS ring. Forward: chunks 0, 1, 2,
@@ -1121,6 +1437,10 @@ __global__ __launch_bounds__(ST) void k_front_fwd(Plan P, int f0, int batch, con
     const int b = list ? __builtin_amdgcn_readfirstlane(list[bi]) : bi;
     const FrontSolve F = front_solve_setup(P, f0 + blockIdx.x, b, Lst, piv, dinv, sinfo, x, sb);
     const int tid = threadIdx.x;
+    if (P.n_sad && P.n_sad[F.f] > 0 && sinfo[(long long)b * P.F + F.f].x == SAD_DONE) {
+        saddle_fwd(P, F.f, b, F.Lb, SC + (long long)b * P.sc_size + P.sc_off[F.f], F.xb, se, cvec, tid);
+        return;
+    }
     const int lane = tid & 63;
     const bool w0 = tid < 64;
     Ring ring{ring_buf};
@@ -1249,6 +1569,10 @@ __global__ __launch_bounds__(ST) void k_front_bwd(Plan P, int f0, int batch, con
     const int b = list ? __builtin_amdgcn_readfirstlane(list[bi]) : bi;
     const FrontSolve F = front_solve_setup(P, f0 + blockIdx.x, b, Lst, piv, dinv, sinfo, x, sb);
     const int tid = threadIdx.x;
+    if (P.n_sad && P.n_sad[F.f] > 0 && sinfo[(long long)b * P.F + F.f].x == SAD_DONE) {
+        saddle_bwd(P, F.f, b, F.Lb, F.xb, se, cvec, tid);
+        return;
+    }
     const int lane = tid & 63;
     const bool w0 = tid < 64;
     Ring ring{ring_buf};
@@ -1486,9 +1810,32 @@ int s16_min_workgroups() {
     return v;
 }
 
+int launch_saddle(const ato_kkt* h, const Plan& P, const Vals& V, const ato_kkt::Seg& sg, int batch,
+                  const int* list, int* inertia, hipStream_t st) {
+    const dim3 grid(sg.count, batch);
+#define ATO_SAD(N_) hipLaunchKernelGGL((k_front_saddle<N_>), grid, dim3(256), sg.lds, st, P, V, sg.start, batch, list, \
+                                       h->d_L, h->d_sinfo, h->d_cb, inertia)
+    switch (sg.nsm) {
+        case 32: ATO_SAD(32); break;
+        case 48: ATO_SAD(48); break;
+        case 56: ATO_SAD(56); break;
+        case 64: ATO_SAD(64); break;
+        default: return fail(ATO_ERR_UNSUPPORTED, "KKT saddle front size");
+    }
+#undef ATO_SAD
+    KKT_HIP(hipGetLastError());
+    return ATO_OK;
+}
+
 int launch_segment(const ato_kkt* h, const Plan& P, const Vals& V, const ato_kkt::Seg& sg, int batch,
                    const int* list, int* inertia, hipStream_t st) {
     const int f0 = sg.start, nf = sg.count;
+    if (sg.cls == SADDLE_CLS) {
+        // the structured elimination, then Bunch-Kaufman for the (front, instance) pairs it left
+        // (SAD_FALLBACK); the other workgroups of that launch return at once
+        if (int rc = launch_saddle(h, P, V, sg, batch, list, inertia, st)) return rc;
+        return launch_segment(h, P, V, ato_kkt::Seg{sg.start, sg.count, sg.cls2}, batch, list, inertia, st);
+    }
 #define ATO_CALL(T_) launch_factor_level<T_>(h, P, V, f0, nf, batch, list, inertia, st)
     switch (sg.cls) {
         case 1: return ATO_CALL(1);
@@ -1518,7 +1865,7 @@ int factor_level(ato_kkt* h, const Plan& P, const Vals& V, int l, int batch, con
     // few workgroups (small batches): one launch at the level's tile count -- the level's time is
     // one front's latency, which a second launch and the stream fork / join only add to
     // (the kernel variant never changes the factors)
-    if (sg.size() > 1 && (long long)nfl * batch < 4 * CUS)
+    if (sg.size() > 1 && (long long)nfl * batch < 4 * CUS && !h->level_sad[l])
         return launch_segment(h, P, V, ato_kkt::Seg{h->level_ptr[l], nfl, h->level_tiles[l]}, batch, list, inertia, st);
     if (sg.size() == 1) return launch_segment(h, P, V, sg[0], batch, list, inertia, st);
     if (!h->side) {
@@ -1584,6 +1931,7 @@ Plan make_plan(const ato_kkt* h) {
     P.cb_off = reinterpret_cast<const long long*>(h->d_cb_off);
     P.sc_off = h->d_sc_off;
     P.forder = h->d_forder;
+    P.n_sad = h->d_n_sad;
     P.l_size = h->l_size;
     P.cb_size = h->cb_size;
     P.sc_size = h->sc_size;
@@ -1691,18 +2039,40 @@ int ato_kkt_create(const ato_kkt_plan_desc* d, ato_kkt** out) {
         std::vector<int32_t> order;
         order.reserve(F);
         h->segs.assign(L, {});
+        h->level_sad.assign(L, 0);
+        auto is_sad = [&](int f) { return d->n_sad && d->n_sad[f] > 0; };
         for (int l = 0; l < L; ++l) {
             std::vector<std::pair<int, int>> fc;   // (-class, front)
             for (int f = d->level_ptr[l]; f < d->level_ptr[l + 1]; ++f)
-                fc.push_back({split ? -front_class(d->pos_ptr[f + 1] - d->pos_ptr[f], s16) : -d->level_tiles[l], f});
+                fc.push_back({is_sad(f) ? -SADDLE_CLS
+                                        : split ? -front_class(d->pos_ptr[f + 1] - d->pos_ptr[f], s16) : -d->level_tiles[l], f});
             std::stable_sort(fc.begin(), fc.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
             for (size_t i = 0; i < fc.size(); ++i) {
                 if (i == 0 || fc[i].first != fc[i - 1].first)
                     h->segs[l].push_back({(int)order.size(), 0, -fc[i].first});
-                ++h->segs[l].back().count;
+                ato_kkt::Seg& sg = h->segs[l].back();
+                ++sg.count;
                 order.push_back(fc[i].second);
+                if (sg.cls == SADDLE_CLS) {
+                    const int f = fc[i].second;
+                    const int A = d->pos_ptr[f + 1] - d->pos_ptr[f], nS = d->n_sad[f];
+                    if (d->n_own[f] != 2 * nS || nS > 64 || d->child_ptr[f + 1] != d->child_ptr[f]) {
+                        ato_kkt_destroy(h);
+                        return fail(ATO_ERR_ARG, "KKT plan: a saddle front must own 2 nS <= 128 positions and have no children");
+                    }
+                    h->level_sad[l] = 1;
+                    sg.nsm = std::max(sg.nsm, nS <= 32 ? 32 : nS <= 48 ? 48 : nS <= 56 ? 56 : 64);
+                    sg.cls2 = std::max(sg.cls2, front_class(A, false));
+                    sg.lds = std::max(sg.lds, sad_lds_bytes(nS, A - 2 * nS));
+                }
             }
         }
+        for (auto& lv : h->segs)
+            for (auto& sg : lv)
+                if (sg.cls == SADDLE_CLS && sg.lds > 160 * 1024) {
+                    ato_kkt_destroy(h);
+                    return fail(ATO_ERR_UNSUPPORTED, "KKT plan: saddle front larger than the LDS");
+                }
         if (int rc = upload(order.data(), order.size(), &h->d_forder)) {
             ato_kkt_destroy(h);
             return rc;
@@ -1721,7 +2091,8 @@ int ato_kkt_create(const ato_kkt_plan_desc* d, ato_kkt** out) {
         (rc = upload(d->l_off, F, &h->d_l_off)) || (rc = upload(d->cb_off, F, &h->d_cb_off)) ||
         (rc = upload(d->sc_off, F, &h->d_sc_off)) || (rc = upload(d->kres_ptr, h->dim + 1, &h->d_kres_ptr)) ||
         (rc = upload(d->kres_col, (size_t)d->kres_ptr[h->dim], &h->d_kres_col)) ||
-        (rc = upload(d->kres_src, (size_t)d->kres_ptr[h->dim], &h->d_kres_src))) {
+        (rc = upload(d->kres_src, (size_t)d->kres_ptr[h->dim], &h->d_kres_src)) ||
+        (d->n_sad && (rc = upload(d->n_sad, F, &h->d_n_sad)))) {
         ato_kkt_destroy(h);
         return rc;
     }
@@ -1742,7 +2113,7 @@ int ato_kkt_destroy(ato_kkt* h) {
                     (void*)h->d_child_ptr, (void*)h->d_child_list, (void*)h->d_ent_ptr, (void*)h->d_ent_pos,
                     (void*)h->d_ent_src, (void*)h->d_piv_off, (void*)h->d_l_off, (void*)h->d_cb_off,
                     (void*)h->d_sc_off, (void*)h->d_kres_ptr, (void*)h->d_kres_col, (void*)h->d_kres_src,
-                    (void*)h->d_forder})
+                    (void*)h->d_forder, (void*)h->d_n_sad})
         (void)hipFree(p);
     delete h;
     return ATO_OK;

@@ -227,9 +227,13 @@ class _SubsetDeviceEvaluator:
 def device_solver(spec, batch: int, lbx, ubx, options: Optional[IPMOptions] = None, device=None):
     ''' BatchedInteriorPoint over the HIP evaluation library and the device KKT factorisation '''
     from aircraft_trajectory_optimization_amd.solver.kkt_device import DeviceKKT
-    from aircraft_trajectory_optimization_amd.solver.kkt_plan import build_plan
+    from aircraft_trajectory_optimization_amd.solver.kkt_plan import build_plan, collocation_saddle
     ev = BatchedDeviceEvaluator(spec, batch, device)
-    plan = build_plan(ev.n, ev.m, ev.var_stage, ev.j_row_ptr, ev.j_col, ev.h_row_ptr, ev.h_col)
+    # saddle fronts (the collocation states and their ODE defect rows: structured elimination) with
+    # ATO_KKT_SADDLE=1; by default every front is factorised by Bunch-Kaufman
+    sad = None if os.environ.get('ATO_KKT_SADDLE', '0') == '0' else \
+        collocation_saddle(spec.N, spec.K1, spec.nv, spec.nz, ev.m, ev.j_row_ptr, ev.j_col)
+    plan = build_plan(ev.n, ev.m, ev.var_stage, ev.j_row_ptr, ev.j_col, ev.h_row_ptr, ev.h_col, saddle=sad)
     kkt = DeviceKKT(plan, batch, ev.device)
     return BatchedInteriorPoint(ev, kkt, lbx, ubx, options)
 
@@ -319,16 +323,10 @@ class BatchedInteriorPoint:
         self.lbx0, self.ubx0 = per_inst(lbx), per_inst(ubx)
         if self.lbx0.shape != (n, B):
             raise ValueError('lbx / ubx must be [n], [n, B] or [B, n]')
-        lbg = ev.lbg.cpu().numpy() if torch.is_tensor(ev.lbg) else np.asarray(ev.lbg, float)
-        ubg = ev.ubg.cpu().numpy() if torch.is_tensor(ev.ubg) else np.asarray(ev.ubg, float)
-        eq = (lbg == ubg) if lbg.ndim == 1 else (lbg[:, 0] == ubg[:, 0])
-        if lbg.ndim == 1:               # shared by every instance
-            lbg, ubg = lbg[:, None], ubg[:, None]
+        eq = self._load_row_bounds()
         self.ieq = t(np.nonzero(eq)[0], torch.long)
         self.iin = t(np.nonzero(~eq)[0], torch.long)
         self.mi = int((~eq).sum())
-        self.lbg0 = t(np.where(lbg <= -INF, -np.inf, lbg))
-        self.ubg0 = t(np.where(ubg >= INF, np.inf, ubg))
         for k_, v_ in _structure(ev, dev).items():
             setattr(self, k_, v_)
         self.stats = {'factorizations': 0, 'solves': 0, 'evals': 0, 'hess': 0, 'compactions': 0}
@@ -341,6 +339,22 @@ class BatchedInteriorPoint:
         if torch.device(dev).type == 'cuda':
             from aircraft_trajectory_optimization_amd.solver.ipm_device import DeviceIPMKernels
             self.vk = DeviceIPMKernels(n, m, self.iin, self.ieq, dev)
+
+    def _load_row_bounds(self):
+        ''' lbg / ubg of the evaluator (shared [m] or per instance [m, B]: per-instance obstacle tubes
+        set by ev.set_instance_spheres), read at construction and again at every solve(); returns
+        the equality-row mask, which must not change '''
+        ev = self.ev
+        lbg = ev.lbg.cpu().numpy() if torch.is_tensor(ev.lbg) else np.asarray(ev.lbg, float)
+        ubg = ev.ubg.cpu().numpy() if torch.is_tensor(ev.ubg) else np.asarray(ev.ubg, float)
+        eq = (lbg == ubg) if lbg.ndim == 1 else (lbg[:, 0] == ubg[:, 0])
+        if lbg.ndim == 1:               # shared by every instance
+            lbg, ubg = lbg[:, None], ubg[:, None]
+        if hasattr(self, 'ieq') and not np.array_equal(np.nonzero(eq)[0], self.ieq.cpu().numpy()):
+            raise ValueError('the evaluator changed which rows are equalities')
+        self.lbg0 = torch.as_tensor(np.where(lbg <= -INF, -np.inf, lbg), dtype=torch.float64, device=self.dev)
+        self.ubg0 = torch.as_tensor(np.where(ubg >= INF, np.inf, ubg), dtype=torch.float64, device=self.dev)
+        return eq
 
     # ------------------------------------------------------------------ sparse products
     @staticmethod
@@ -667,6 +681,7 @@ class BatchedInteriorPoint:
         '''
         o = self.o
         self._progress = progress
+        self._load_row_bounds()
         n, m, B, dev = self.n, self.m, self.B, self.dev
         x = torch.as_tensor(np.asarray(X0, float) if not torch.is_tensor(X0) else X0, dtype=torch.float64,
                             device=dev)

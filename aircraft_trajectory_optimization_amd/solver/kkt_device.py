@@ -47,6 +47,7 @@ class AtoKKTPlanDesc(ctypes.Structure):
         ('kres_ptr', _i32p),
         ('kres_col', _i32p),
         ('kres_src', _i32p),
+        ('n_sad', _i32p),
     ]
 
 
@@ -88,6 +89,8 @@ class DeviceKKT:
         d.kres_ptr = arr(plan.kres_ptr, np.int32, _i32p)
         d.kres_col = arr(plan.kres_col, np.int32, _i32p)
         d.kres_src = arr(plan.kres_src, np.int32, _i32p)
+        n_sad = getattr(plan, 'n_sad', None)
+        d.n_sad = arr(n_sad, np.int32, _i32p) if n_sad is not None and np.any(n_sad) else None
         self.desc = d
         h = ctypes.c_void_p()
         with torch.cuda.device(self.device):

@@ -33,7 +33,13 @@ diagonal by interval, almost every row touches one interval or two neighbouring 
            intervals) form the root. The critical path of one factorisation is one leaf plus
            log2(N) separators instead of the whole chain. Variable / row pairs isolated inside an
            interval (the input rates and their defect rows) form a child front of the leaf
-           (split_pairs), which shrinks the leaf block.
+           (split_pairs), which shrinks the leaf block. With `saddle` pairs (collocation_saddle:
+           the states of nodes 1..K of an interval and their ODE defect rows) a second child front
+           of the leaf holds the saddle block [[H_XX, J_YX^T], [J_YX, 0]]; J_YX is square and (for
+           a collocation step) non-singular, so the block has the fixed inertia (nS, nS, 0) and the
+           device eliminates it by one LU of J_YX and dense products instead of a Bunch-Kaufman
+           pivot chain (csrc/ato_kkt.hip, k_front_saddle; Bunch-Kaufman on the same front when
+           J_YX is singular or the rows carry a delta_c).
   'chain'  the staged elimination of solver/kkt_blocks.py: front s owns interval s's variables
            and rows (a row touching two intervals joins the later one), its child is front s-1,
            the border is the root. One front per level.
@@ -86,6 +92,7 @@ class KKTPlan:
     sc_off: np.ndarray          # [F] offset of the front's solve contribution (tq doubles)
     sc_size: int
     block_sizes: np.ndarray     # [F] own + trailing
+    n_sad: np.ndarray           # [F] saddle fronts: nS (own = nS states, then their nS defect rows); else 0
     kres_ptr: np.ndarray        # [dim+1] CSR of the whole K (both triangles) for residuals r - K x
     kres_col: np.ndarray        # [nnz_K] column (KKT index), ascending within a row
     kres_src: np.ndarray        # [nnz_K] source code of the value (a diagonal with two sources: two entries)
@@ -137,7 +144,60 @@ def _fronts_chain(n, var_stage, lo, hi):
     return own, children
 
 
-def _fronts_nd(n, var_stage, lo, hi, j_row_ptr, j_col, split_pairs=True):
+def collocation_saddle(N, K1, nv, nz, m, j_row_ptr, j_col):
+    '''
+    Saddle pairs of a collocation transcription, from the Jacobian structure alone: the states of
+    nodes 1..K of every interval (variables N + (n K1 + k) nv + [0, nz)) and the rows that are
+    their ODE defects. The defect of state component c at node k of interval n,
+        sum_j C_jk z_j[c] - h_n f_c(z_k, u_k) = 0,
+    is the row with entries on component c at EVERY node of the interval (the collocation
+    derivative), on other node variables of node k only (f_c), and on nothing of another interval.
+    (The s-dot rows have no f term; a gate row has no single node.) Returns (cols, rows), the
+    defect of (n, k, c) paired with state (n, k, c), or None when some (n, k >= 1, c) has no unique
+    defect row (RK4 steps, other transcriptions).
+    '''
+    j_row_ptr = np.asarray(j_row_ptr, np.int64)
+    j_col = np.asarray(j_col, np.int64)
+    if K1 < 2:
+        return None
+    jr = np.repeat(np.arange(m), np.diff(j_row_ptr))
+    node_var = j_col >= N
+    q = np.where(node_var, (j_col - N) // nv, -1)          # node of the entry
+    comp = np.where(node_var, (j_col - N) % nv, -1)
+    stage = np.where(node_var, q // K1, j_col)              # h_n -> n
+    lo = np.full(m, np.iinfo(np.int64).max)
+    hi = np.full(m, -1)
+    np.minimum.at(lo, jr, stage)
+    np.maximum.at(hi, jr, stage)
+    found = {}
+    for c in range(nz):
+        # per row: bit k set when the row has an entry on component c (resp. another node
+        # variable) of node k of its interval
+        on_c = node_var & (comp == c)
+        bits_c = np.zeros(m, np.int64)
+        np.bitwise_or.at(bits_c, jr[on_c], np.left_shift(1, q[on_c] % K1))
+        other = node_var & (comp != c)
+        bits_o = np.zeros(m, np.int64)
+        np.bitwise_or.at(bits_o, jr[other], np.left_shift(1, q[other] % K1))
+        single = (bits_o > 0) & ((bits_o & (bits_o - 1)) == 0)
+        for r in np.nonzero((bits_c == (1 << K1) - 1) & (lo == hi) & single)[0]:
+            k = int(bits_o[r]).bit_length() - 1
+            key = (int(lo[r]), k, c)
+            if k == 0 or key in found:
+                return None
+            found[key] = int(r)
+    cols, rows = [], []
+    for st in range(N):
+        for k in range(1, K1):
+            for c in range(nz):
+                if (st, k, c) not in found:
+                    return None
+                cols.append(N + (st * K1 + k) * nv + c)
+                rows.append(found[(st, k, c)])
+    return np.asarray(cols, np.int64), np.asarray(rows, np.int64)
+
+
+def _fronts_nd(n, var_stage, lo, hi, j_row_ptr, j_col, split_pairs=True, saddle=None):
     S = int(var_stage.max()) + 1
     m = len(lo)
     link = hi - lo == 1
@@ -194,15 +254,40 @@ def _fronts_nd(n, var_stage, lo, hi, j_row_ptr, j_col, split_pairs=True):
             pre_id[st] = len(own)
             own.append(pre[st])
             children.append([])
+    # saddle fronts: the states of nodes 1..K and their ODE defect rows (collocation_saddle), when
+    # every one of them lies inside the leaf (not an anchor, not in a pre-front pair)
+    sad_id = [-1] * S
+    n_sad: List[int] = [0] * len(own)
+    sad = [np.zeros(0, np.int64) for _ in range(S)]
+    if saddle is not None:
+        scols, srows = (np.asarray(a, np.int64) for a in saddle)
+        for st in range(S):
+            xs = np.sort(scols[var_stage[scols] == st])
+            ys = np.sort(srows[(lo[srows] == st) & (hi[srows] == st)])
+            if not len(xs) or len(xs) != len(ys) or len(xs) > 64:
+                continue
+            inner_ok = not (anchor[xs].any() or root_anchor[xs].any() or (~interior[ys]).any() or
+                            anchor_only[ys].any() or root_only[ys].any())
+            if len(pre[st]):
+                inner_ok = inner_ok and not np.isin(np.concatenate([xs, n + ys]), pre[st]).any()
+            if not inner_ok:
+                continue
+            sad[st] = np.concatenate([xs, n + ys])
+            sad_id[st] = len(own)
+            own.append(sad[st])
+            children.append([])
+            n_sad.append(len(xs))
     leaf_id = []
     for st in range(S):                          # leaves
         inner = np.concatenate([np.nonzero((var_stage == st) & ~anchor & ~root_anchor)[0],
                                 n + np.nonzero(interior & ~anchor_only & ~root_only & (lo == st))[0]])
         if len(pre[st]):
             inner = inner[~np.isin(inner, pre[st])]
+        if len(sad[st]):
+            inner = inner[~np.isin(inner, sad[st])]
         leaf_id.append(len(own))
         own.append(inner)
-        children.append([pre_id[st]] if pre_id[st] >= 0 else [])
+        children.append([c for c in (pre_id[st], sad_id[st]) if c >= 0])
 
     def sep(j):
         return np.concatenate([np.nonzero((var_stage == j) & anchor)[0],
@@ -222,11 +307,16 @@ def _fronts_nd(n, var_stage, lo, hi, j_row_ptr, j_col, split_pairs=True):
     if len(border):
         own.append(border)
         children.append([top])
-    return own, children
+    n_sad += [0] * (len(own) - len(n_sad))
+    return own, children, n_sad
 
 
 def build_plan(n: int, m: int, var_stage, j_row_ptr, j_col, h_row_ptr, h_col, ordering: str = 'nd',
-               split_pairs: bool = True) -> KKTPlan:
+               split_pairs: bool = True, saddle=None) -> KKTPlan:
+    '''
+    saddle: optional (cols, rows) saddle pairs (collocation_saddle) for the 'nd' ordering: every
+    interval's set becomes a saddle front, a child of the interval's leaf.
+    '''
     var_stage = np.asarray(var_stage, np.int64)
     j_row_ptr = np.asarray(j_row_ptr, np.int64)
     j_col = np.asarray(j_col, np.int64)
@@ -238,9 +328,10 @@ def build_plan(n: int, m: int, var_stage, j_row_ptr, j_col, h_row_ptr, h_col, or
         raise ValueError('Hessian couples different stages; the staged KKT does not apply')
     lo, hi = row_span(n, m, var_stage, j_row_ptr, j_col)
     if ordering == 'nd':
-        own, children = _fronts_nd(n, var_stage, lo, hi, j_row_ptr, j_col, split_pairs)
+        own, children, n_sad = _fronts_nd(n, var_stage, lo, hi, j_row_ptr, j_col, split_pairs, saddle)
     elif ordering == 'chain':
         own, children = _fronts_chain(n, var_stage, lo, hi)
+        n_sad = [0] * len(own)
     else:
         raise ValueError(f'unknown KKT ordering {ordering!r}')
     F0 = len(own)
@@ -258,6 +349,7 @@ def build_plan(n: int, m: int, var_stage, j_row_ptr, j_col, h_row_ptr, h_col, or
     new_id[order] = np.arange(F0)
     own = [own[f] for f in order]
     children = [sorted(int(new_id[c]) for c in children[f]) for f in order]
+    n_sad = np.asarray([n_sad[f] for f in order], np.int64)
     level = level[order]
     F = F0
     parent = np.full(F, -1, np.int64)
@@ -389,6 +481,9 @@ def build_plan(n: int, m: int, var_stage, j_row_ptr, j_col, h_row_ptr, h_col, or
     n_own = np.array([len(o) for o in own])
     tq = sizes - n_own
     l_sz = n_own * sizes - n_own * (n_own + 1) // 2
+    # a saddle front stores either the Bunch-Kaufman columns (fallback) or K_SS^-1 (2nS x 2nS) and
+    # W = K_TS K_SS^-1 (tq x 2nS)
+    l_sz = np.maximum(l_sz, np.where(n_sad > 0, (2 * n_sad) ** 2 + tq * 2 * n_sad, 0))
     l_off = np.concatenate([[0], np.cumsum(l_sz)])
     piv_off = np.concatenate([[0], np.cumsum(n_own)])
     cb_off = np.concatenate([[0], np.cumsum(tq * tq)])
@@ -401,5 +496,5 @@ def build_plan(n: int, m: int, var_stage, j_row_ptr, j_col, h_row_ptr, h_col, or
                    ent_ptr=i32(ent_ptr), ent_pos=i32(ent_pos), ent_src=i32(ent_src).reshape(-1, 2),
                    l_off=np.asarray(l_off[:-1], np.int64), l_size=int(l_off[-1]),
                    piv_off=i32(piv_off[:-1]), cb_off=np.asarray(cb_off[:-1], np.int64), cb_size=int(cb_off[-1]),
-                   sc_off=i32(sc_off[:-1]), sc_size=int(sc_off[-1]), block_sizes=i32(sizes),
+                   sc_off=i32(sc_off[:-1]), sc_size=int(sc_off[-1]), block_sizes=i32(sizes), n_sad=i32(n_sad),
                    kres_ptr=i32(kres_ptr), kres_col=i32(cc[o]), kres_src=i32(ss[o]))

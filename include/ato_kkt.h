@@ -60,6 +60,11 @@ typedef struct ato_kkt_plan_desc {
     const int32_t* kres_ptr;    /* [n + m + 1] CSR of the whole K (both triangles): residuals    */
     const int32_t* kres_col;    /* [nnz_K] column (KKT index) of every entry                     */
     const int32_t* kres_src;    /* [nnz_K] source code of every entry (as ent_src, one source)   */
+    const int32_t* n_sad;       /* [F] or NULL: nS of a SADDLE front (own = nS states, then their *
+                                 * nS ODE defect rows; no children), 0 for the others. Its block  *
+                                 * [[H, J^T], [J, 0]] is eliminated by an LU of the square J and *
+                                 * dense products (inertia (nS, nS, 0)); Bunch-Kaufman when J is  *
+                                 * singular or the rows carry a diagonal (delta_c).              */
 } ato_kkt_plan_desc;
 
 typedef struct ato_kkt ato_kkt;

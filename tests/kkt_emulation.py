@@ -5,12 +5,38 @@ children's contribution blocks assembled by extend-add, Bunch-Kaufman pivoting r
 the own positions, the trailing Schur complement handed to the parent) and the same compact
 factor-column storage, in plain numpy. It checks the plan and the algorithm on CPU; the GPU
 tests compare the kernels with dense linear algebra.
+
+Saddle fronts (plan.n_sad > 0: nS states X, then their nS ODE defect rows Y, then the trailing
+positions T) take the device's structured path when the Y rows carry no diagonal (delta_c = 0)
+and J_YX is safely non-singular: K_SS = [[H, J^T], [J, 0]] has the inverse [[0, E], [E^T, G]] with
+E = J^-1 and G = -E^T H E and the inertia (nS, nS, 0); W = K_TS K_SS^-1 is stored with K_SS^-1, the
+contribution block is -W K_ST, and the solve applies K_SS^-1 and W (forward: u = K_SS^-1 b_S, the
+parent gets -W b_S; backward: x_S = u - W^T x_T). Otherwise the front is factorised by
+Bunch-Kaufman like any other.
 '''
+import scipy.linalg
 import numpy as np
 
 from aircraft_trajectory_optimization_amd.solver.kkt_plan import MAX_TILES, SRC_DR, SRC_DX, SRC_H, SRC_J, SRC_SHIFT
 
 ALPHA = (1.0 + np.sqrt(17.0)) / 8.0
+SADDLE_PIVOT_TOL = 1e-12     # |u_kk| of the LU of J_YX against max |J_YX| (csrc/ato_kkt.hip: the same rule)
+
+
+def saddle_factor(M, nS):
+    ''' structured elimination of a saddle front's block M (own = 2 nS): (Kinv, W, S) or None '''
+    H, J = M[:nS, :nS], M[nS:2 * nS, :nS]
+    if np.any(M[nS:2 * nS, nS:2 * nS] != 0.0):
+        return None                                   # delta_c on the defect rows
+    lu, piv = scipy.linalg.lu_factor(J, check_finite=False)
+    if not np.all(np.abs(np.diag(lu)) > SADDLE_PIVOT_TOL * np.abs(J).max()):
+        return None
+    E = scipy.linalg.lu_solve((lu, piv), np.eye(nS))
+    G = -E.T @ H @ E
+    Kinv = np.block([[np.zeros((nS, nS)), E], [E.T, G]])
+    W = M[2 * nS:, :2 * nS] @ Kinv
+    S = M[2 * nS:, 2 * nS:] - W @ M[2 * nS:, :2 * nS].T
+    return Kinv, W, S
 
 
 def _value(code, H, J, dx, dr):
@@ -42,7 +68,8 @@ class Factor:
     def __init__(self, plan, H, J, dx, dr):
         self.plan = plan
         self.L = np.zeros(plan.l_size)
-        self.steps = []               # per front: list of (type, p, r, dinv(3))
+        self.steps = []               # per front: list of (type, p, r, dinv(3)), or 'saddle'
+        self.sad = {}                 # saddle fronts factorised by the structured path: (Kinv, W)
         pos = neg = zero = 0
         cb = {}
         for f in range(plan.n_fronts):
@@ -51,6 +78,16 @@ class Factor:
                 pm = _parent_map(plan, c)
                 M[np.ix_(pm, pm)] += cb.pop(int(c))
             A, own = int(plan.block_sizes[f]), int(plan.n_own[f])
+            nS = int(plan.n_sad[f]) if hasattr(plan, 'n_sad') else 0
+            sf = saddle_factor(M, nS) if nS and not len(plan.children(f)) else None
+            if sf is not None:
+                self.sad[f] = sf[:2]
+                self.steps.append('saddle')
+                pos += nS
+                neg += nS
+                if plan.parent[f] >= 0:
+                    cb[f] = sf[2]
+                continue
             live = np.ones(A, bool)
             off = int(plan.l_off[f])
             st = []
@@ -159,6 +196,12 @@ class Factor:
             y[:own] = x[gi[:own]]
             for c in plan.children(f):
                 y[_parent_map(plan, c)] += sc.pop(int(c))
+            if f in self.sad:
+                Kinv, W = self.sad[f]
+                x[gi[:own]] = Kinv @ y[:own]
+                if plan.parent[f] >= 0:
+                    sc[f] = y[own:] - W @ y[:own]
+                continue
             live = np.ones(A, bool)
             for (typ, p, r, _), off in zip(self.steps[f], self._offsets(f)):
                 if typ == 1:
@@ -182,6 +225,9 @@ class Factor:
             gi = plan.front_positions(f)
             A, own = int(plan.block_sizes[f]), int(plan.n_own[f])
             v = x[gi].copy()
+            if f in self.sad:
+                x[gi[:own]] = v[:own] - self.sad[f][1].T @ v[own:]
+                continue
             live = np.zeros(A, bool)
             live[own:] = True
             for (typ, p, r, _), off in zip(reversed(self.steps[f]), reversed(self._offsets(f))):

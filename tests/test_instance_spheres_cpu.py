@@ -101,10 +101,11 @@ def test_batched_solver_over_perturbed_tubes_follows_single_instances():
     tables = tube.perturbed_tables(spec0.node_s, range(3))
     B = len(tables)
     ev = HostBatchEvaluator(spec0, B)
-    ev.set_instance_spheres(tables)
     o = IPMOptions(max_iter=300)
     W = np.repeat(spec0.w0[None], B, axis=0)
-    res = BatchedInteriorPoint(ev, HostBlockKKT(ev), spec0.lbw, spec0.ubw, o).solve(W)
+    solver = BatchedInteriorPoint(ev, HostBlockKKT(ev), spec0.lbw, spec0.ubw, o)
+    ev.set_instance_spheres(tables)         # after construction: solve() reads the per-instance bounds
+    res = solver.solve(W)
     x = res.x.numpy() if torch.is_tensor(res.x) else res.x
     laps = []
     for b in range(B):

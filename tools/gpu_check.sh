@@ -72,6 +72,14 @@ for s in $STEPS; do
                    ATO_LIB_PATH=$PWD/tools/diag/_lib/libato_base.so run kkt_base_b$b 200 python tools/bench_kkt.py --batch $b --reps 7 --out "$OUT/kkt_base_b$b.json"
                    run kkt_cur_b$b 200 python tools/bench_kkt.py --batch $b --reps 7 --out "$OUT/kkt_cur_b$b.json"
                done ;;
+        sadab) for b in 512 64 1; do
+                   run kkt_bk_b$b 200 python tools/bench_kkt.py --batch $b --reps 7 --saddle 0 --out "$OUT/kkt_bk_b$b.json"
+                   run kkt_sad_b$b 200 python tools/bench_kkt.py --batch $b --reps 7 --saddle 1 --out "$OUT/kkt_sad_b$b.json"
+               done ;;
+        sadphase) ATO_LIB_PATH=$PWD/tools/diag/_lib/libato_stamps.so run saddle_phase 120 python tools/diag/saddle_phase.py
+               ATO_PHASE_B=1 ATO_LIB_PATH=$PWD/tools/diag/_lib/libato_stamps.so run saddle_phase_b1 120 python tools/diag/saddle_phase.py ;;
+        sadprof) run saddle_prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/saddle_prof" -o run -- \
+                   python tools/bench_kkt.py --batch 512 --reps 5 --saddle 1 --out "$OUT/saddle_prof.json" ;;
         kktq)  run kkt_b512 200 python tools/bench_kkt.py --batch 512 --out "$OUT/kkt_b512.json"
                run kkt_b1 200 python tools/bench_kkt.py --batch 1 --out "$OUT/kkt_b1.json" ;;
         ipmktests) run pytest_ipmk 300 python -u -m pytest tests/test_gpu_ipm_kernels.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider ;;
