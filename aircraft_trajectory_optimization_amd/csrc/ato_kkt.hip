@@ -48,6 +48,7 @@ struct ato_kkt {
     int64_t *d_l_off = nullptr, *d_cb_off = nullptr;
     int32_t* d_forder = nullptr;     // [F] fronts of every level grouped by kernel class (factor launches)
     int32_t* d_n_sad = nullptr;      // [F] saddle fronts: nS, else 0 (NULL: the plan has none)
+    int32_t* d_sad_txy = nullptr;    // [F][2] saddle fronts: (tx, ty)
     // cls: kernel class; saddle segments (cls SADDLE_CLS): nsm = the k_front_saddle variant, lds its
     // shared-memory bytes, cls2 the Bunch-Kaufman class of the fallback launch
     struct Seg { int start, count, cls, nsm = 0, cls2 = 0; size_t lds = 0; };
@@ -135,6 +136,7 @@ struct Plan {
     const int* sc_off;
     const int* forder;            // factor launches: front = forder[f0 + blockIdx.x]
     const int* n_sad;             // [F] saddle fronts: nS (NULL: none)
+    const int2* sad_txy;          // [F] saddle fronts: trailing rows [0, tx) coupled to X, [T - ty, T) to Y
     long long l_size, cb_size;
     int sc_size;
 };
@@ -1039,208 +1041,192 @@ size_t factor_s_lds() {
 // and path rows). With no row diagonal on Y (delta_c = 0) the block
 //     K_SS = [[H, J^T], [J, 0]]     (H = H_XX + diag_x, J = J_YX square)
 // has the inverse [[0, E], [E^T, G]], E = J^-1, G = -E^T H E, and the inertia (nS, nS, 0) whatever
-// H is; so it is eliminated WITHOUT a pivot chain across the workgroup:
-//   one wave: LU of J with partial pivoting, each lane one row in registers (the pivot row by
-//            readlane, no barrier), then E column by column (lane = column) from the LU in LDS;
-//   all:     HE = H E, G = -E^T (HE), W = K_TS K_SS^-1 = [B_y E^T, B_x E + B_y G] and the
-//            contribution block S = -W K_ST (lower triangle, mirrored: one writer per entry) as
-//            4x4 register-tiled LDS products.
+// H is; so it is eliminated without the Bunch-Kaufman pivot chain over 2 nS positions:
+//   E:   Gauss-Jordan inversion of J with partial pivoting, held in REGISTERS (lane = row, the eight
+//        waves own the columns j = wave mod 8): the wave owning column k picks the pivot and
+//        publishes the column, one barrier per step, every thread updates its entries (the pivot
+//        row by readlane). No row swaps: the result is E with permuted rows and columns,
+//        E[k][c] = M[p_k][j : p_j = c], written unscrambled to LDS;
+//   all: HE = H E, G = -E^T (HE), W = K_TS K_SS^-1 = [B_y E^T, B_x E + B_y G] and the contribution
+//        block S = -W K_ST (lower tiles, mirrored: one writer per entry) as 16 x 16 fp64 MFMA
+//        tiles (v_mfma_f64_16x16x4_f64) from LDS operands.
 // Stored for the solve (the front's factor-column slice): K_SS^-1 (2nS x 2nS, symmetric) and W
-// (T x 2nS), sinfo = {SAD_DONE, doubles}. A J_YX pivot below SAD_PIVOT_TOL max|J_YX| or a nonzero
-// Y diagonal marks the (front, instance) SAD_FALLBACK instead, and the Bunch-Kaufman launch that
+// (T x 2nS), sinfo = {SAD_DONE, doubles}. A pivot below SAD_PIVOT_TOL max|J_YX| or a nonzero Y
+// diagonal marks the (front, instance) SAD_FALLBACK instead, and the Bunch-Kaufman launch that
 // follows factorises exactly those (tests/kkt_emulation.py restates both paths).
 // ------------------------------------------------------------------------------------------
-// C[i][j] = sum_k a(i, k) b(k, j) over an M x N output in 4 x 4 register tiles (all threads);
-// out-of-range rows / columns read a clamped index and are not written
+constexpr int SAD_NT = 512;           // threads per (saddle front, instance): eight waves
+constexpr int SAD_NW = SAD_NT / 64;
+
+typedef double sad_v4d __attribute__((ext_vector_type(4)));
+
+// C[i][j] = sum_k a(i, k) b(k, j) over an M x N output in 16 x 16 tiles, one wave per tile, K in
+// steps of 4 (v_mfma_f64_16x16x4_f64: lane l holds A[l & 15][k + l / 16] and B[k + l / 16][l & 15],
+// result row l / 16 + 4 q, column l & 15 in register q). Out-of-range operands are zero.
 template <class FA, class FB, class FC>
-__device__ __forceinline__ void sad_gemm(int M, int N, int K, FA a, FB b, FC c, int tid, int nthr, bool lower = false) {
-    const int tm = (M + 3) >> 2, tn = (N + 3) >> 2;
-    for (int tile = tid; tile < tm * tn; tile += nthr) {
-        const int i0 = (tile / tn) * 4, j0 = (tile % tn) * 4;
+__device__ __forceinline__ void sad_mfma(int M, int N, int K, FA a, FB b, FC c, int wave, int lane,
+                                         bool lower = false) {
+    const int tm = (M + 15) >> 4, tn = (N + 15) >> 4;
+    for (int tile = wave; tile < tm * tn; tile += SAD_NW) {
+        const int i0 = (tile / tn) * 16, j0 = (tile % tn) * 16;
         if (lower && j0 > i0) continue;
-        int ii[4], jj[4];
+        const int ai = i0 + (lane & 15), bj = j0 + (lane & 15), kk = lane >> 4;
+        sad_v4d acc = {0.0, 0.0, 0.0, 0.0};
+        for (int k0 = 0; k0 < K; k0 += 32) {     // eight k-steps of operands in flight, then the MFMAs
+            double av[8], bv[8];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            ii[q] = min(i0 + q, M - 1);
-            jj[q] = min(j0 + q, N - 1);
-        }
-        double acc[4][4];
-#pragma unroll
-        for (int x = 0; x < 4; ++x)
-#pragma unroll
-            for (int y = 0; y < 4; ++y) acc[x][y] = 0.0;
-        for (int k = 0; k < K; ++k) {
-            double av[4], bv[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                av[q] = a(ii[q], k);
-                bv[q] = b(k, jj[q]);
+            for (int q = 0; q < 8; ++q) {
+                const int k = k0 + 4 * q + kk;
+                av[q] = (ai < M && k < K) ? a(ai, k) : 0.0;
+                bv[q] = (k < K && bj < N) ? b(k, bj) : 0.0;
             }
 #pragma unroll
-            for (int x = 0; x < 4; ++x)
-#pragma unroll
-                for (int y = 0; y < 4; ++y) acc[x][y] = fma(av[x], bv[y], acc[x][y]);
+            for (int q = 0; q < 8; ++q) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[q], bv[q], acc, 0, 0, 0);
         }
 #pragma unroll
-        for (int x = 0; x < 4; ++x)
-#pragma unroll
-            for (int y = 0; y < 4; ++y)
-                if (i0 + x < M && j0 + y < N) c(i0 + x, j0 + y, acc[x][y]);
+        for (int q = 0; q < 4; ++q) {
+            const int i = i0 + (lane >> 4) + 4 * q, j = j0 + (lane & 15);
+            if (i < M && j < N) c(i, j, acc[q]);
+        }
     }
 }
 
 struct SadLds {      // shared-memory carve of one saddle front (runtime sizes)
-    double *J, *H, *B, *W, *rinv;
-    int *perm, *flag;
-    int ldn, ldb;
+    double *E, *H, *Bx, *By, *col, *dv, *mx, *prow;
+    int *piv, *pp, *flag;
+    int ldn;
 };
 
-__device__ __forceinline__ SadLds sad_lds(double* smem, int nS, int T) {
+// E and H / G (nS x nS), K_TX rows [0, tx) and K_TY rows [T - ty, T) (the others are zero), the
+// published pivot columns: 68 KB on the racetrack (nS 52, tx <= 27, ty 30), two fronts per CU
+__device__ __forceinline__ SadLds sad_lds(double* smem, int nS, int tx, int ty) {
     SadLds L;
     L.ldn = nS + 1;
-    L.ldb = 2 * nS + 1;
-    L.J = smem;
-    L.H = L.J + nS * L.ldn;
-    L.B = L.H + nS * L.ldn;
-    L.W = L.B + T * L.ldb;                      // also the H E scratch (nS x ldn)
-    L.rinv = L.W + max(T * L.ldb, nS * L.ldn);
-    L.perm = reinterpret_cast<int*>(L.rinv + nS);
-    L.flag = L.perm + nS;
+    L.E = smem;                                  // J (assembly) -> E
+    L.H = L.E + nS * L.ldn;                      // H -> G
+    L.Bx = L.H + nS * L.ldn;                     // [tx][X]
+    L.By = L.Bx + tx * L.ldn;                    // [ty][Y]
+    L.col = L.By + ty * L.ldn;                   // [2][64] published pivot columns
+    L.dv = L.col + 128;                          // [2] pivots
+    L.mx = L.dv + 2;                             // [SAD_NW] max |J| per wave
+    L.prow = L.mx + SAD_NW;                      // [64] the pivot row (each wave its own columns)
+    L.piv = reinterpret_cast<int*>(L.prow + 64);     // [nS] pivot row of every step
+    L.pp = L.piv + nS;                           // [2]
+    L.flag = L.pp + 2;
     return L;
 }
 
-inline size_t sad_lds_bytes(int nS, int T) {
-    const size_t d = (size_t)2 * nS * (nS + 1) + (size_t)T * (2 * nS + 1) + std::max((size_t)T * (2 * nS + 1),
-                                                                                     (size_t)nS * (nS + 1)) + nS;
-    return d * sizeof(double) + sizeof(int) * (nS + 1);
+inline size_t sad_lds_bytes(int nS, int tx, int ty) {
+    const size_t d = (size_t)(2 * nS + tx + ty) * (nS + 1) + 128 + 2 + SAD_NW + 64;
+    return d * sizeof(double) + sizeof(int) * (nS + 3);
 }
 
 template <int NSM>
-__global__ __launch_bounds__(256) void k_front_saddle(Plan P, Vals V, int f0, int batch, const int* __restrict__ list,
-                                                      double* __restrict__ Lst, int2* __restrict__ sinfo,
-                                                      double* __restrict__ CB, int* __restrict__ inertia) {
-    static_assert(NSM <= 64, "one LU row per lane");
+__global__ __launch_bounds__(SAD_NT) void k_front_saddle(Plan P, Vals V, int f0, int batch, const int* __restrict__ list,
+                                                         double* __restrict__ Lst, int2* __restrict__ sinfo,
+                                                         double* __restrict__ CB, int* __restrict__ inertia) {
+    static_assert(NSM <= 64, "one Gauss-Jordan row per lane");
+    constexpr int CM = (NSM + SAD_NW - 1) / SAD_NW;          // columns per thread
     extern __shared__ double smem[];
     const int f = P.forder[f0 + blockIdx.x];
     const int bi = blockIdx.y;
     if (bi >= batch) return;
     const int b = list ? __builtin_amdgcn_readfirstlane(list[bi]) : bi;
-    const int tid = threadIdx.x, lane = tid & 63;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int p0 = P.pos_ptr[f];
     const int A = P.pos_ptr[f + 1] - p0;
     const int nS = P.n_sad[f], n2 = 2 * nS, T = A - n2;
-    const SadLds L = sad_lds(smem, nS, T);
+    const int2 txy = P.sad_txy[f];
+    const int tx = txy.x, ty0 = T - txy.y;        // K_TX rows [0, tx), K_TY rows [ty0, T)
+    const SadLds L = sad_lds(smem, nS, tx, txy.y);
+    const int ldn = L.ldn;
     KST_DECL(f == ATO_KKT_STAMP_FRONT && blockIdx.y == 0)
 
-    // ---- assembly: J (Y x X), H (X x X), B = K_TS ([T][X | Y]); a Y diagonal (delta_c) -> fallback
-    for (int i = tid; i < 2 * nS * L.ldn + T * L.ldb; i += 256) L.J[i] = 0.0;
+    // ---- assembly: J (Y x X) into E, H (X x X), K_TX, K_TY; a Y diagonal -> fallback
+    for (int i = tid; i < (2 * nS + tx + txy.y) * ldn; i += SAD_NT) L.E[i] = 0.0;
     if (tid == 0) *L.flag = 0;
     __syncthreads();
     {
         const int e0 = P.ent_ptr[f * MAXT], e1 = P.ent_ptr[(f + 1) * MAXT];
-        for (int e = e0 + tid; e < e1; e += 256) {
+        for (int e = e0 + tid; e < e1; e += SAD_NT) {
             const int ep = P.ent_pos[e];
             const int pa = ep >> 16, pb = ep & 0xffff;
             const int2 sc = P.ent_src[e];
             const double v = src_value(V, sc.x, b) + src_value(V, sc.y, b);
             if (pa < nS) {
-                L.H[pa * L.ldn + pb] = v;
-                L.H[pb * L.ldn + pa] = v;
+                L.H[pa * ldn + pb] = v;
+                L.H[pb * ldn + pa] = v;
             } else if (pa < n2) {
-                if (pb < nS) L.J[(pa - nS) * L.ldn + pb] = v;
+                if (pb < nS) L.E[(pa - nS) * ldn + pb] = v;
                 else if (v != 0.0) *L.flag = 1;
+            } else if (pb < nS) {
+                L.Bx[(pa - n2) * ldn + pb] = v;
             } else if (pb < n2) {
-                L.B[(pa - n2) * L.ldb + pb] = v;
+                L.By[(pa - n2 - ty0) * ldn + (pb - nS)] = v;
             }
         }
     }
     __syncthreads();
-
     KST(0);                      // assembly
-    // ---- wave 0: LU of J with partial pivoting (lane i = row i), then E = J^-1 (lane c = column c)
-    if (tid < 64) {
-        double r[NSM];
+
+    // ---- Gauss-Jordan inversion of J in registers: row `lane`, columns wave + 8 m
+    double Mr[CM];
+    double lmx = 0.0;
 #pragma unroll
-        for (int j = 0; j < NSM; ++j) r[j] = (lane < nS && j < nS) ? L.J[lane * L.ldn + j] : 0.0;
-        double mx = 0.0;
-#pragma unroll
-        for (int j = 0; j < NSM; ++j) mx = fmax(mx, fabs(r[j]));
-        {   // max |J| over the wave (as a float key: the tolerance needs no more)
-            const unsigned km = wave_max_u32(__float_as_uint((float)mx));
-            mx = (double)__uint_as_float(km);
-        }
-        bool live = lane < nS;
-        int mystep = -1, pk = 0;
-        bool bad = false;
-#pragma unroll
-        for (int k = 0; k < NSM; ++k) {
-            if (k < nS) {
-                const unsigned key = wave_max_u32(live ? mag_key(r[k], lane) : 0u);
-                const int p = key ? 511 - (int)(key & 0x1FFu) : 0;
-                const double piv = readlane_f64(r[k], p);
-                bad = bad || !(fabs(piv) > SAD_PIVOT_TOL * mx) || key == 0u;
-                const double inv = 1.0 / piv;
-                const bool upd = live && lane != p;
-                const double l = r[k] * inv;
-                if (lane == p) {
-                    live = false;
-                    mystep = k;
-                }
-                if (lane == k) pk = p;
-                if (upd) r[k] = l;
-#pragma unroll
-                for (int j = k + 1; j < NSM; ++j) {
-                    const double u = readlane_f64(r[j], p);
-                    if (upd) r[j] = fma(-l, u, r[j]);
-                }
-                if (lane == 0) L.rinv[k] = inv;
-            }
-        }
-        // L \ U in pivot order: row k of P J = J[perm[k]] is held by the lane that pivoted at step k
-        if (lane < nS && mystep >= 0) {
-#pragma unroll
-            for (int j = 0; j < NSM; ++j)
-                if (j < nS) L.J[mystep * L.ldn + j] = r[j];
-            L.perm[lane] = pk;
-        }
-        if (bad && lane == 0) *L.flag = 1;
-        KST(1);                  // LU
-        __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");    // the LDS stores are visible to the wave
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (!bad) {
-            // column c of J^-1 = U^-1 L^-1 (P e_c): (P e_c)_k = 1 where perm[k] == c
-            double y[NSM];
-#pragma unroll
-            for (int k = 0; k < NSM; ++k) y[k] = (k < nS && L.perm[k] == lane) ? 1.0 : 0.0;
-#pragma unroll
-            for (int j = 0; j < NSM; ++j) {          // L y = P e_c (unit lower), column-oriented
-                if (j < nS) {
-#pragma unroll
-                    for (int k = j + 1; k < NSM; ++k)
-                        if (k < nS) y[k] = fma(-L.J[k * L.ldn + j], y[j], y[k]);
-                }
-            }
-#pragma unroll
-            for (int k = NSM - 1; k >= 0; --k) {     // U x = y, column-oriented
-                if (k < nS) {
-                    y[k] *= L.rinv[k];
-#pragma unroll
-                    for (int i = 0; i < k; ++i) y[i] = fma(-L.J[i * L.ldn + k], y[k], y[i]);
-                }
-            }
-            __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_wave_barrier();
-            if (lane < nS) {
-#pragma unroll
-                for (int i = 0; i < NSM; ++i)
-                    if (i < nS) L.J[i * L.ldn + lane] = y[i];    // E[i][c]
-            }
-        }
+    for (int m = 0; m < CM; ++m) {
+        const int j = wave + SAD_NW * m;
+        Mr[m] = (lane < nS && j < nS) ? L.E[lane * ldn + j] : 0.0;
+        lmx = fmax(lmx, fabs(Mr[m]));
+    }
+    {
+        const unsigned km = wave_max_u32(__float_as_uint((float)lmx));
+        if (lane == 0) L.mx[wave] = (double)__uint_as_float(km);
     }
     __syncthreads();
-    KST(2);                      // E = J^-1
+    double mx = 0.0;
+#pragma unroll
+    for (int w = 0; w < SAD_NW; ++w) mx = fmax(mx, L.mx[w]);
+    bool used = false;
+    int mystep = -1;
+    for (int k = 0; k < nS; ++k) {
+        const int par = k & 1;
+        if (wave == (k & (SAD_NW - 1))) {        // owner of column k: pivot search, publish the column
+            const int mk = k / SAD_NW;
+            double v = Mr[0];
+#pragma unroll
+            for (int m = 1; m < CM; ++m) v = blend(v, Mr[m], m == mk ? ~0ull : 0ull);
+            const unsigned key = wave_max_u32(lane < nS && !used ? mag_key(v, lane) : 0u);
+            const int p = key ? 511 - (int)(key & 0x1FFu) : 0;
+            const double d = readlane_f64(v, p);
+            L.col[par * 64 + lane] = v;
+            if (lane == 0) {
+                L.piv[k] = p;
+                L.pp[par] = p;
+                L.dv[par] = 1.0 / d;
+                if (key == 0u || !(fabs(d) > SAD_PIVOT_TOL * mx)) *L.flag = 1;
+            }
+        }
+        KST(7);                  // owner: search and publish (wave 0 owns every eighth column)
+        __syncthreads();
+        const int p = __builtin_amdgcn_readfirstlane(L.pp[par]);
+        const double inv = L.dv[par];
+        const double fr = L.col[par * 64 + lane];
+        if (lane == p) {
+            used = true;
+            mystep = k;
+#pragma unroll
+            for (int m = 0; m < CM; ++m) L.prow[wave + SAD_NW * m] = Mr[m];   // this wave's columns of row p
+        }
+        KST(8);                  // barrier, published pivot read
+#pragma unroll
+        for (int m = 0; m < CM; ++m) {
+            const int j = wave + SAD_NW * m;
+            const double pr = j == k ? inv : L.prow[j] * inv;
+            Mr[m] = lane == p ? pr : fma(-fr, pr, j == k ? 0.0 : Mr[m]);
+        }
+        KST(9);                  // update
+    }
+    KST(1);                      // Gauss-Jordan
     int2* si = sinfo + (long long)b * P.F + f;
     if (*L.flag) {
         if (tid == 0) *si = make_int2(SAD_FALLBACK, 0);
@@ -1249,50 +1235,62 @@ __global__ __launch_bounds__(256) void k_front_saddle(Plan P, Vals V, int f0, in
 #endif
         return;
     }
-    // ---- HE = H E (scratch in W), G = -E^T (HE) (over H)
-    const double* J = L.J;
-    double* Hm = L.H;
-    double* Wm = L.W;
-    const double* Bm = L.B;
-    const int ldn = L.ldn, ldb = L.ldb;
-    sad_gemm(nS, nS, nS, [&](int i, int k) { return Hm[i * ldn + k]; }, [&](int k, int j) { return J[k * ldn + j]; },
-             [&](int i, int j, double v) { Wm[i * ldn + j] = v; }, tid, 256);
+    // E[k][c] = M[p_k][j] with p_j = c: row `lane` was the pivot of step mystep
+    if (lane < nS) {
+#pragma unroll
+        for (int m = 0; m < CM; ++m) {
+            const int j = wave + SAD_NW * m;
+            if (j < nS) L.E[mystep * ldn + L.piv[j]] = Mr[m];
+        }
+    }
     __syncthreads();
-    sad_gemm(nS, nS, nS, [&](int i, int k) { return J[k * ldn + i]; }, [&](int k, int j) { return Wm[k * ldn + j]; },
-             [&](int i, int j, double v) { Hm[i * ldn + j] = -v; }, tid, 256);
+    KST(2);                      // unscramble
+    // ---- HE = H E (scratch: the front's factor slice, rewritten below), G = -E^T (HE) (over H)
+    const double* E = L.E;
+    double* Hm = L.H;
+    const double* Bx = L.Bx;
+    const double* By = L.By;
+    double* Lb = Lst + (long long)b * P.l_size + P.l_off[f];
+    double* Wg = Lb + (long long)n2 * n2;         // W [T][2 nS] in the factor slice
+    double* HE = Lb;
+    // K_TS (t, k): k < nS from K_TX, k >= nS from K_TY (zero outside their row ranges)
+    auto kts = [&](int t, int k) {
+        return k < nS ? (t < tx ? Bx[t * ldn + k] : 0.0) : (t >= ty0 ? By[(t - ty0) * ldn + (k - nS)] : 0.0);
+    };
+    sad_mfma(nS, nS, nS, [&](int i, int k) { return Hm[i * ldn + k]; }, [&](int k, int j) { return E[k * ldn + j]; },
+             [&](int i, int j, double v) { HE[i * nS + j] = v; }, wave, lane);
+    __syncthreads();
+    sad_mfma(nS, nS, nS, [&](int i, int k) { return E[k * ldn + i]; }, [&](int k, int j) { return HE[k * nS + j]; },
+             [&](int i, int j, double v) { Hm[i * ldn + j] = -v; }, wave, lane);
     __syncthreads();
     KST(3);                      // H E, G
-    // ---- W = [B_y E^T, B_x E + B_y G]
-    sad_gemm(T, nS, nS, [&](int t, int k) { return Bm[t * ldb + nS + k]; }, [&](int k, int i) { return J[i * ldn + k]; },
-             [&](int t, int i, double v) { Wm[t * ldb + i] = v; }, tid, 256);
-    sad_gemm(T, nS, n2, [&](int t, int k) { return Bm[t * ldb + k]; },
-             [&](int k, int i) { return k < nS ? J[k * ldn + i] : Hm[(k - nS) * ldn + i]; },
-             [&](int t, int i, double v) { Wm[t * ldb + nS + i] = v; }, tid, 256);
+    // ---- W = [K_TY E^T, K_TX E + K_TY G] into the factor slice
+    sad_mfma(T, nS, nS, [&](int t, int k) { return kts(t, nS + k); }, [&](int k, int i) { return E[i * ldn + k]; },
+             [&](int t, int i, double v) { Wg[(long long)t * n2 + i] = v; }, wave, lane);
+    sad_mfma(T, nS, n2, [&](int t, int k) { return kts(t, k); },
+             [&](int k, int i) { return k < nS ? E[k * ldn + i] : Hm[(k - nS) * ldn + i]; },
+             [&](int t, int i, double v) { Wg[(long long)t * n2 + nS + i] = v; }, wave, lane);
     __syncthreads();
     KST(4);                      // W
-    // ---- contribution block S = -W B^T (lower tiles, mirrored), K_SS^-1 and W to the factor slice
+    // ---- contribution block S = -W K_ST (lower tiles, mirrored), then K_SS^-1 to the factor slice
     if (T > 0) {
         double* cb = CB + (long long)b * P.cb_size + P.cb_off[f];
-        sad_gemm(T, T, n2, [&](int s, int k) { return Wm[s * ldb + k]; }, [&](int k, int t) { return Bm[t * ldb + k]; },
+        sad_mfma(T, T, n2, [&](int s, int k) { return Wg[(long long)s * n2 + k]; }, [&](int k, int t) { return kts(t, k); },
                  [&](int s, int t, double v) {
                      if (s >= t) {
                          cb[(long long)s * T + t] = -v;
                          cb[(long long)t * T + s] = -v;
                      }
-                 }, tid, 256, true);
+                 }, wave, lane, true);
     }
+    __syncthreads();             // the H E scratch is read by the other waves until here
     KST(5);                      // S
-    double* Lb = Lst + (long long)b * P.l_size + P.l_off[f];
-    for (int q = tid; q < n2 * n2; q += 256) {
+    for (int q = tid; q < n2 * n2; q += SAD_NT) {
         const int i = q / n2, j = q - i * n2;
         double v;
-        if (i < nS) v = j < nS ? 0.0 : J[i * ldn + (j - nS)];
-        else v = j < nS ? J[j * ldn + (i - nS)] : Hm[(i - nS) * ldn + (j - nS)];
+        if (i < nS) v = j < nS ? 0.0 : E[i * ldn + (j - nS)];
+        else v = j < nS ? E[j * ldn + (i - nS)] : Hm[(i - nS) * ldn + (j - nS)];
         Lb[q] = v;
-    }
-    for (int q = tid; q < T * n2; q += 256) {
-        const int t = q / n2, k = q - t * n2;
-        Lb[n2 * n2 + q] = Wm[t * ldb + k];
     }
     KST(6);                      // stores
     KST_DUMP(1);
@@ -1813,7 +1811,7 @@ int s16_min_workgroups() {
 int launch_saddle(const ato_kkt* h, const Plan& P, const Vals& V, const ato_kkt::Seg& sg, int batch,
                   const int* list, int* inertia, hipStream_t st) {
     const dim3 grid(sg.count, batch);
-#define ATO_SAD(N_) hipLaunchKernelGGL((k_front_saddle<N_>), grid, dim3(256), sg.lds, st, P, V, sg.start, batch, list, \
+#define ATO_SAD(N_) hipLaunchKernelGGL((k_front_saddle<N_>), grid, dim3(SAD_NT), sg.lds, st, P, V, sg.start, batch, list, \
                                        h->d_L, h->d_sinfo, h->d_cb, inertia)
     switch (sg.nsm) {
         case 32: ATO_SAD(32); break;
@@ -1932,6 +1930,7 @@ Plan make_plan(const ato_kkt* h) {
     P.sc_off = h->d_sc_off;
     P.forder = h->d_forder;
     P.n_sad = h->d_n_sad;
+    P.sad_txy = reinterpret_cast<const int2*>(h->d_sad_txy);
     P.l_size = h->l_size;
     P.cb_size = h->cb_size;
     P.sc_size = h->sc_size;
@@ -2040,7 +2039,29 @@ int ato_kkt_create(const ato_kkt_plan_desc* d, ato_kkt** out) {
         order.reserve(F);
         h->segs.assign(L, {});
         h->level_sad.assign(L, 0);
-        auto is_sad = [&](int f) { return d->n_sad && d->n_sad[f] > 0; };
+        // saddle fronts the kernel takes: own = 2 nS <= 128, no children, blocks within the LDS;
+        // any other front the plan marks is factorised by Bunch-Kaufman like the rest
+        std::vector<int32_t> nsad(F, 0), txy(2 * (size_t)F, 0);
+        bool any_sad = false;
+        for (int f = 0; f < F && d->n_sad; ++f) {
+            const int nS = d->n_sad[f], A = d->pos_ptr[f + 1] - d->pos_ptr[f], T = A - 2 * nS;
+            if (nS <= 0 || nS > 64 || d->n_own[f] != 2 * nS || d->child_ptr[f + 1] != d->child_ptr[f]) continue;
+            // trailing rows coupled to X end at tx, those coupled to Y start at T - ty (the plan orders them)
+            int tx = 0, ty = 0;
+            for (int e = d->ent_ptr[f * MAXT]; e < d->ent_ptr[(f + 1) * MAXT]; ++e) {
+                const int pa = d->ent_pos[e] >> 16, pb = d->ent_pos[e] & 0xffff;
+                if (pa < 2 * nS) continue;
+                if (pb < nS) tx = std::max(tx, pa - 2 * nS + 1);
+                else if (pb < 2 * nS) ty = std::max(ty, T - (pa - 2 * nS));
+            }
+            if (sad_lds_bytes(nS, tx, ty) <= 160 * 1024) {
+                nsad[f] = nS;
+                txy[2 * f] = tx;
+                txy[2 * f + 1] = ty;
+                any_sad = true;
+            }
+        }
+        auto is_sad = [&](int f) { return nsad[f] > 0; };
         for (int l = 0; l < L; ++l) {
             std::vector<std::pair<int, int>> fc;   // (-class, front)
             for (int f = d->level_ptr[l]; f < d->level_ptr[l + 1]; ++f)
@@ -2055,24 +2076,23 @@ int ato_kkt_create(const ato_kkt_plan_desc* d, ato_kkt** out) {
                 order.push_back(fc[i].second);
                 if (sg.cls == SADDLE_CLS) {
                     const int f = fc[i].second;
-                    const int A = d->pos_ptr[f + 1] - d->pos_ptr[f], nS = d->n_sad[f];
-                    if (d->n_own[f] != 2 * nS || nS > 64 || d->child_ptr[f + 1] != d->child_ptr[f]) {
-                        ato_kkt_destroy(h);
-                        return fail(ATO_ERR_ARG, "KKT plan: a saddle front must own 2 nS <= 128 positions and have no children");
-                    }
+                    const int A = d->pos_ptr[f + 1] - d->pos_ptr[f], nS = nsad[f];
                     h->level_sad[l] = 1;
                     sg.nsm = std::max(sg.nsm, nS <= 32 ? 32 : nS <= 48 ? 48 : nS <= 56 ? 56 : 64);
                     sg.cls2 = std::max(sg.cls2, front_class(A, false));
-                    sg.lds = std::max(sg.lds, sad_lds_bytes(nS, A - 2 * nS));
+                    (void)A;
+                    sg.lds = std::max(sg.lds, sad_lds_bytes(nS, txy[2 * f], txy[2 * f + 1]));
                 }
             }
         }
-        for (auto& lv : h->segs)
-            for (auto& sg : lv)
-                if (sg.cls == SADDLE_CLS && sg.lds > 160 * 1024) {
-                    ato_kkt_destroy(h);
-                    return fail(ATO_ERR_UNSUPPORTED, "KKT plan: saddle front larger than the LDS");
-                }
+        if (any_sad) {
+            int rc = upload(nsad.data(), nsad.size(), &h->d_n_sad);
+            if (rc == ATO_OK) rc = upload(txy.data(), txy.size(), &h->d_sad_txy);
+            if (rc != ATO_OK) {
+                ato_kkt_destroy(h);
+                return rc;
+            }
+        }
         if (int rc = upload(order.data(), order.size(), &h->d_forder)) {
             ato_kkt_destroy(h);
             return rc;
@@ -2091,8 +2111,7 @@ int ato_kkt_create(const ato_kkt_plan_desc* d, ato_kkt** out) {
         (rc = upload(d->l_off, F, &h->d_l_off)) || (rc = upload(d->cb_off, F, &h->d_cb_off)) ||
         (rc = upload(d->sc_off, F, &h->d_sc_off)) || (rc = upload(d->kres_ptr, h->dim + 1, &h->d_kres_ptr)) ||
         (rc = upload(d->kres_col, (size_t)d->kres_ptr[h->dim], &h->d_kres_col)) ||
-        (rc = upload(d->kres_src, (size_t)d->kres_ptr[h->dim], &h->d_kres_src)) ||
-        (d->n_sad && (rc = upload(d->n_sad, F, &h->d_n_sad)))) {
+        (rc = upload(d->kres_src, (size_t)d->kres_ptr[h->dim], &h->d_kres_src))) {
         ato_kkt_destroy(h);
         return rc;
     }
@@ -2113,7 +2132,7 @@ int ato_kkt_destroy(ato_kkt* h) {
                     (void*)h->d_child_ptr, (void*)h->d_child_list, (void*)h->d_ent_ptr, (void*)h->d_ent_pos,
                     (void*)h->d_ent_src, (void*)h->d_piv_off, (void*)h->d_l_off, (void*)h->d_cb_off,
                     (void*)h->d_sc_off, (void*)h->d_kres_ptr, (void*)h->d_kres_col, (void*)h->d_kres_src,
-                    (void*)h->d_forder, (void*)h->d_n_sad})
+                    (void*)h->d_forder, (void*)h->d_n_sad, (void*)h->d_sad_txy})
         (void)hipFree(p);
     delete h;
     return ATO_OK;

@@ -386,6 +386,18 @@ def build_plan(n: int, m: int, var_stage, j_row_ptr, j_col, h_row_ptr, h_col, or
             raise AssertionError(f'front {f}: a child hands over positions eliminated outside its ancestry')
         cand = np.unique(np.concatenate([nb, ct]))
         cand = cand[~isown[cand]]
+        if n_sad[f] > 0:
+            # saddle front: trailing positions coupled to the states only, then to states and defect
+            # rows, then to the defect rows only, so that K_TX and K_TY are row ranges [0, tx) and
+            # [T - ty, T) (k_front_saddle keeps only those rows)
+            ns = int(n_sad[f])
+            cls = np.zeros(len(cand), np.int64)
+            for q, i in enumerate(cand):
+                nbi = adj_c[adj_ptr[i]:adj_ptr[i + 1]]
+                to_x = np.isin(nbi, o[:ns]).any()
+                to_y = np.isin(nbi, o[ns:]).any()
+                cls[q] = 0 if not to_y else (1 if to_x else 2)
+            cand = cand[np.lexsort((cand, cls))]
         trailing.append(cand)
         eliminated[o] = True
     if any(len(trailing[f]) for f in range(len(own)) if parent[f] < 0):

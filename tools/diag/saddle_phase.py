@@ -52,9 +52,11 @@ def main():
     out = (ctypes.c_ulonglong * 16)()
     assert lib.ato_kkt_diag_stamps(out) == 0
     v = list(out)
-    names = ['assembly', 'LU (wave 0)', 'E = J^-1 (wave 0)', 'HE, G', 'W', 'S', 'stores']
+    names = ['assembly', 'Gauss-Jordan', 'unscramble', 'HE, G', 'W', 'S', 'stores']
     res = {n: int(v[i]) for i, n in enumerate(names)}
-    res['total_cycles'] = int(sum(v[:7]))
+    res['total_cycles'] = int(sum(v[:10]))
+    res['gauss_jordan_split'] = {'owner search (wave 0: every 8th step)': int(v[7]), 'barrier + pivot read': int(v[8]),
+                                 'update': int(v[9])}
     res['fallback_pairs_per_factorisation'] = v[14] / reps
     res['saddle_pairs_per_factorisation'] = int((plan.n_sad > 0).sum()) * B
     print(json.dumps(res))

@@ -80,6 +80,9 @@ for s in $STEPS; do
                ATO_PHASE_B=1 ATO_LIB_PATH=$PWD/tools/diag/_lib/libato_stamps.so run saddle_phase_b1 120 python tools/diag/saddle_phase.py ;;
         sadprof) run saddle_prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/saddle_prof" -o run -- \
                    python tools/bench_kkt.py --batch 512 --reps 5 --saddle 1 --out "$OUT/saddle_prof.json" ;;
+        solvesad) for v in 0 1; do
+                   ATO_KKT_SADDLE=$v run solve_sad$v 600 python tools/solve_batched.py --batch 512 --max-iter 1000 --cold --no-host --out "$OUT/solve_sad$v.json"
+               done ;;
         kktq)  run kkt_b512 200 python tools/bench_kkt.py --batch 512 --out "$OUT/kkt_b512.json"
                run kkt_b1 200 python tools/bench_kkt.py --batch 1 --out "$OUT/kkt_b1.json" ;;
         ipmktests) run pytest_ipmk 300 python -u -m pytest tests/test_gpu_ipm_kernels.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider ;;
