@@ -40,6 +40,7 @@ static void release(ato_handle* h) {
     (void)hipFree(h->d_node_s);
     (void)hipFree(h->d_interval_s);
     (void)hipFree(h->d_spheres);
+    (void)hipFree(h->d_cpc_wp);
     (void)hipFree(h->d_gates);
     (void)hipFree(h->d_seg);
     (void)hipFree(h->d_tail);
@@ -100,7 +101,7 @@ int ato_create(const ato_problem_desc* desc, ato_handle** out) {
         (rc = upload(h->L.interval_s, &h->d_interval_s)) || (rc = upload(h->L.spheres, &h->d_spheres)) ||
         (rc = upload(h->L.gates, &h->d_gates)) || (rc = upload(h->L.seg, &h->d_seg)) ||
         (rc = upload(h->L.tail, &h->d_tail)) || (rc = upload(h->L.units, &h->d_units)) ||
-        (rc = upload(h->L.units_lf, &h->d_units_lf))) {
+        (rc = upload(h->L.units_lf, &h->d_units_lf)) || (rc = upload(h->L.cpc_wp, &h->d_cpc_wp))) {
         release(h);
         delete h;
         return rc;
@@ -110,6 +111,7 @@ int ato_create(const ato_problem_desc* desc, ato_handle** out) {
     h->pd.node_s = h->d_node_s;
     h->pd.interval_s = h->d_interval_s;
     h->pd.spheres = h->d_spheres;
+    h->pd.cpc_wp = h->d_cpc_wp;
     h->pd.gates = h->d_gates;
     h->pd.seg = h->d_seg;
     h->pd.tail = h->d_tail;

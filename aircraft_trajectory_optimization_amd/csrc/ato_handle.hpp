@@ -14,6 +14,7 @@ struct ato_handle {
     double* d_node_s = nullptr;
     double* d_interval_s = nullptr;
     double* d_spheres = nullptr;
+    double* d_cpc_wp = nullptr;
     ato_gate* d_gates = nullptr;
     int32_t* d_seg = nullptr;
     int32_t* d_tail = nullptr;

@@ -107,6 +107,9 @@ ATO_HD void run_node_seg(const ProbD& p, int kind, int n, int k, const W& w, S& 
         case SEG_RK4:
             if constexpr (RK4) seg_rk4<M, T, KS>(p, n, grp, w, s);
             break;
+        case SEG_CPC_COMP: seg_cpc_comp<M, T, KS>(p, n, k, w, s); break;
+        case SEG_CPC_ORDER: seg_cpc_order<M, T, KS>(p, n, k, w, s); break;
+        case SEG_CPC_PROG: seg_cpc_prog<M, T, KS>(p, n, k, w, s); break;
         default: break;
     }
 }
@@ -216,6 +219,11 @@ ATO_HD void run_unit(const ProbD& p, int kind, int n, int k, const W& w, S& s, c
                 seg(SEG_STAGE);
                 seg(SEG_SPHERE);
                 seg(SEG_RK4S);
+                if (p.cpc_m > 0) {
+                    seg(SEG_CPC_COMP);
+                    seg(SEG_CPC_ORDER);
+                    seg(SEG_CPC_PROG);
+                }
             }
             if (GRAD) {
                 const Cols<M> c{p.N, K1S(p)};
@@ -229,6 +237,10 @@ ATO_HD void run_unit(const ProbD& p, int kind, int n, int k, const W& w, S& s, c
                 for (int i = 0; i < NU; ++i) go.put_gf(base + NZ + i, hB * gu[i]);
 #pragma unroll
                 for (int i = 0; i < NU; ++i) go.put_gf(base + NZ + NU + i, hB * gdu[i]);
+                if (p.cpc_m > 0) {      // the progress variables are not in the cost
+                    const long cb = p.cpc_off + 3L * p.cpc_m * ((long)n * K1S(p) + k);
+                    for (int i = 0; i < 3 * p.cpc_m; ++i) go.put_gf(cb + i, T(0));
+                }
             }
             break;
         case UNIT_INTERVAL:
@@ -257,7 +269,7 @@ ATO_HD void run_unit(const ProbD& p, int kind, int n, int k, const W& w, S& s, c
 
 struct Layout {
     ProbD p{};                        // host pointers into the vectors below
-    std::vector<double> geom, node_s, interval_s, spheres;
+    std::vector<double> geom, node_s, interval_s, spheres, cpc_wp;
     std::vector<ato_gate> gates;
     std::vector<int32_t> seg, tail;   // segment tables (see ProbD)
     std::vector<int32_t> units;       // work-unit table (see ProbD)
@@ -272,6 +284,7 @@ struct Layout {
         p.interval_s = interval_s.data();
         p.gates = gates.data();
         p.spheres = spheres.empty() ? nullptr : spheres.data();
+        p.cpc_wp = cpc_wp.empty() ? nullptr : cpc_wp.data();
         p.seg = seg.data();
         p.tail = tail.data();
         p.units = units.data();
@@ -319,6 +332,15 @@ struct Layout {
         p.NU = nu;
         p.NV = nz + 2 * nu;
         p.nw = p.N + p.P * p.NV;
+        if (d.cpc_m < 0 || d.cpc_m > ATO_CPC_MAX) return "cpc_m out of range [0, ATO_CPC_MAX]";
+        if (d.cpc_m > 0) {
+            if (d.frame != ATO_FRAME_GLOBAL) return "CPC gate progress needs the global frame";
+            if (d.n_gates != 0 || d.has_spheres) return "CPC gate progress replaces the gate and obstacle rows";
+            p.cpc_m = d.cpc_m;
+            p.cpc_off = p.nw;
+            p.nw += p.P * 3 * d.cpc_m;
+            cpc_wp.assign(d.cpc_wp, d.cpc_wp + 3 * d.cpc_m);
+        }
         p.closed = d.closed;
         p.cleanly_closed = d.cleanly_closed;
         p.quat_flip = d.quat_flip;
@@ -563,6 +585,14 @@ struct Layout {
             if (!param) return "obstacle spheres need the parametric frame";
             for (int n = 0; n < p.N; ++n)
                 for (int k = 0; k < p.K1; ++k) ATO_TRY(node_segment<M>(SEG_SPHERE, n, k));
+        }
+        if (p.cpc_m > 0) {      // CPC gate progress, node by node in time order
+            for (int n = 0; n < p.N; ++n)
+                for (int k = 0; k < p.K1; ++k) {
+                    ATO_TRY(node_segment<M>(SEG_CPC_COMP, n, k));
+                    if (p.cpc_m > 1) ATO_TRY(node_segment<M>(SEG_CPC_ORDER, n, k));
+                    if (n * p.K1 + k + 1 < p.P) ATO_TRY(node_segment<M>(SEG_CPC_PROG, n, k));
+                }
         }
         if (p.closed && M::IS_DRONE) ATO_TRY(tail_segment<M>(TAIL_DRONE_CLOSURE, 0));
 #undef ATO_TRY

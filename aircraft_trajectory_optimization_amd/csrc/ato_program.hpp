@@ -31,7 +31,7 @@ namespace ato {
 // Row segments of node (n, k) in reference order: s-dot row, ODE rows (two groups), dU rows;
 // then per interval: regularity rows, stage rows, continuity, fixed-s rows.
 enum SegKind { SEG_SDOT = 0, SEG_ODE_A, SEG_ODE_B, SEG_DU, SEG_REG, SEG_STAGE, SEG_SPHERE, SEG_CONT,
-               SEG_SROWS, SEG_RK4S, SEG_RK4, NSEG };
+               SEG_SROWS, SEG_RK4S, SEG_RK4, SEG_CPC_COMP, SEG_CPC_ORDER, SEG_CPC_PROG, NSEG };
 enum TailKind { TAIL_HEQ = 0, TAIL_CLOSURE_BASE, TAIL_INITIAL, TAIL_TERMINAL, TAIL_GATE,
                 TAIL_DRONE_CLOSURE };
 // Work units of the evaluation kernel (one per grid.y index; see ato_layout.hpp)
@@ -85,6 +85,11 @@ struct ProbD {
     // the decision-vector accessor's par(); NULL: the shared table `spheres`
     const double* isph;
     int64_t isph_stride;
+    // CPC gate progress (cpc_m > 0): node q's lambda, mu, nu at cpc_off + 3 cpc_m q + [0, cpc_m),
+    // [cpc_m, 2 cpc_m), [2 cpc_m, 3 cpc_m); waypoints [cpc_m][3] (a table like the spheres: in the
+    // kernel argument an indexed array would be copied into registers)
+    int32_t cpc_m, cpc_off;
+    const double* cpc_wp;
 };
 
 // nodes per interval: compile-time KS (specialised kernels for common K) or runtime p.K1
@@ -238,6 +243,54 @@ ATO_HD void seg_sphere(const ProbD& p, int n, int k, const W& w, S& s) {
     s.jac(c.z(n, k, 1), T(2) * ey);
     s.jac(c.z(n, k, 2), T(2) * en);
     s.row(ey * ey + en * en, -ATO_INF, sp[2] * sp[2]);
+}
+
+// ---- CPC gate progress (build-side: Foehn et al. 2021; the reference only displays a CPC
+// trajectory, cpc_utils.py:14-101). Global frame: the position is z[0:3] of the node.
+// complementarity: mu_j (|p - w_j|^2 - nu_j) = 0, j < M
+template <class M, class T, int KS, class W, class S>
+ATO_HD void seg_cpc_comp(const ProbD& p, int n, int k, const W& w, S& s) {
+    const Cols<M> c{p.N, K1S(p)};
+    const int m = p.cpc_m;
+    const long base = p.cpc_off + 3L * m * ((long)n * K1S(p) + k);
+    const T px = w(c.z(n, k, 0)), py = w(c.z(n, k, 1)), pz = w(c.z(n, k, 2));
+    for (int j = 0; j < m; ++j) {
+        const T ex = px - T(p.cpc_wp[3 * j]), ey = py - T(p.cpc_wp[3 * j + 1]), ez = pz - T(p.cpc_wp[3 * j + 2]);
+        const T mu = w(base + m + j), nu = w(base + 2 * m + j);
+        const T d2 = ex * ex + ey * ey + ez * ez - nu;
+        s.jac(c.z(n, k, 0), T(2) * mu * ex);
+        s.jac(c.z(n, k, 1), T(2) * mu * ey);
+        s.jac(c.z(n, k, 2), T(2) * mu * ez);
+        s.jac(base + m + j, d2);
+        s.jac(base + 2 * m + j, -mu);
+        s.row(mu * d2, 0.0, 0.0);
+    }
+}
+
+// waypoint order: lambda_j - lambda_{j+1} <= 0, j < M - 1
+template <class M, class T, int KS, class W, class S>
+ATO_HD void seg_cpc_order(const ProbD& p, int n, int k, const W& w, S& s) {
+    const int m = p.cpc_m;
+    const long base = p.cpc_off + 3L * m * ((long)n * K1S(p) + k);
+    for (int j = 0; j + 1 < m; ++j) {
+        s.jac(base + j, T(1));
+        s.jac(base + j + 1, T(-1));
+        s.row(w(base + j) - w(base + j + 1), -ATO_INF, 0.0);
+    }
+}
+
+// progress: lambda_{q+1,j} - lambda_{q,j} + mu_{q,j} = 0 (q = the node, q + 1 the next one in time)
+template <class M, class T, int KS, class W, class S>
+ATO_HD void seg_cpc_prog(const ProbD& p, int n, int k, const W& w, S& s) {
+    const int m = p.cpc_m;
+    const long base = p.cpc_off + 3L * m * ((long)n * K1S(p) + k);
+    const long next = base + 3L * m;
+    for (int j = 0; j < m; ++j) {
+        s.jac(base + j, T(-1));
+        s.jac(base + m + j, T(1));
+        s.jac(next + j, T(1));
+        s.row(w(next + j) - w(base + j) + w(base + m + j), 0.0, 0.0);
+    }
 }
 
 // quaternion normalisation op(q) = q / |q| and its Jacobian (drone_raceline.py:42-45)

@@ -19,7 +19,8 @@ ATO_FRAME_GLOBAL, ATO_FRAME_PARAMETRIC = 0, 1
 ATO_TRANS_COLLOCATION, ATO_TRANS_RK4 = 0, 1
 ATO_GATE_CIRCLE, ATO_GATE_SQUARE = 0, 1
 ATO_LAYOUT_INTERLEAVED, ATO_LAYOUT_INSTANCE_MAJOR = 0, 1
-ABI_VERSION = 2
+ABI_VERSION = 3
+CPC_MAX = 16                 # ATO_CPC_MAX
 
 _c_double_p = ctypes.POINTER(ctypes.c_double)
 
@@ -84,6 +85,9 @@ class AtoProblemDesc(ctypes.Structure):
         ('interval_s', _c_double_p),
         ('gates', ctypes.POINTER(AtoGate)),
         ('spheres', _c_double_p),
+        ('cpc_m', ctypes.c_int32),
+        ('pad1', ctypes.c_int32),
+        ('cpc_wp', ctypes.c_double * (CPC_MAX * 3)),
     ]
 
 
@@ -264,6 +268,13 @@ class DescHolder:
         spheres = spec.get('spheres')
         d.has_spheres = 1 if spheres is not None else 0
         d.spheres = ptr(spheres)
+        wp = spec.get('cpc_waypoints')
+        if wp is not None:
+            wp = np.asarray(wp, float).reshape(-1, 3)
+            if len(wp) > CPC_MAX:
+                raise ValueError(f'at most {CPC_MAX} CPC waypoints')
+            d.cpc_m = len(wp)
+            d.cpc_wp = _carr(ctypes.c_double, wp.reshape(-1), CPC_MAX * 3)
         self.desc = d
 
 

@@ -19,7 +19,10 @@ def variable_stages(spec: ProblemSpec) -> np.ndarray:
     ''' interval of every decision variable (h_n -> n, node (n, k) -> n): the KKT block order '''
     st = np.zeros(spec.nw, dtype=np.int64)
     st[:spec.N] = np.arange(spec.N)
-    st[spec.N:] = np.repeat(np.arange(spec.P) // spec.K1, spec.nv)
+    nodes = spec.N + spec.P * spec.nv
+    st[spec.N:nodes] = np.repeat(np.arange(spec.P) // spec.K1, spec.nv)
+    if nodes < spec.nw:      # CPC progress variables of node q: q's interval
+        st[nodes:] = np.repeat(np.arange(spec.P) // spec.K1, (spec.nw - nodes) // spec.P)
     return st
 
 

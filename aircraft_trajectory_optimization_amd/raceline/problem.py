@@ -49,11 +49,17 @@ class ProblemSpec:
     frame: 'parametric' or 'global'; vehicle: DroneConfig (drone) or PointConfig (point mass).
     quat_flip / euler_wraps: closure branch chosen from a warm start (drone_raceline.py:78-95).
     tube: optional obstacle-free tube (per-node dy, dn, radius) for the obstacle variant.
+    cpc: optional CPC gate progress (config 5; build-side, Foehn et al. 2021 -- the reference only
+    displays a CPC trajectory, utils/cpc_utils.py): {'waypoints': (M, 3) or None for the gates of the
+    line, 'tol': d_tol}. Global frame only; it replaces the gate rows: per node progress lambda,
+    its decrease mu and tolerance nu (M each, after all node variables), complementarity
+    mu_j (|p - w_j|^2 - nu_j) = 0, order lambda_j <= lambda_{j+1}, progress lambda_{q+1} =
+    lambda_q - mu_q, lambda = 1 at the first node and 0 at the last, one total time (all h equal).
     '''
 
     def __init__(self, line: BaseCenterline, config: RacelineConfig, vehicle: RacerConfig,
                  frame: str, quat_flip: bool = False, euler_wraps: float = 0.0,
-                 sphere_table: Optional[np.ndarray] = None):
+                 sphere_table: Optional[np.ndarray] = None, cpc: Optional[dict] = None):
         self.line = line
         self.config = config
         self.vehicle = vehicle
@@ -100,6 +106,22 @@ class ProblemSpec:
         self.K1 = self.K + 1
         self.P = self.N * self.K1
         self.nw = self.N + self.P * self.nv
+        self.cpc = None
+        self.guess_phase_len = self.phase_len
+        if cpc is not None:
+            if self.param:
+                raise NotImplementedError('CPC gate progress needs the global frame')
+            wp = cpc.get('waypoints')
+            if wp is None:
+                x = np.array([config.gate_xi, config.gate_xj, config.gate_xk], dtype=float)
+                if config.closed and (x[:, 0] == x[:, -1]).all():
+                    x = x[:, :-1]
+                wp = x.T
+            self.cpc = {'waypoints': np.asarray(wp, float).reshape(-1, 3), 'tol': float(cpc.get('tol', 0.3))}
+            self.cpc_m = len(self.cpc['waypoints'])
+            self.cpc_off = self.nw
+            self.nw += self.P * 3 * self.cpc_m
+            self.phase_len = self.N             # one total time: every h equal
         if self.rk4:
             # one node per interval; the stage cost is weighted by h_n alone (base_raceline.py:610-611)
             self.tau, self.B, self.C, self.D = np.zeros(1), np.ones(1), np.zeros((1, 1)), np.ones(1)
@@ -120,7 +142,7 @@ class ProblemSpec:
         self.quat_flip = bool(quat_flip)
         self.euler_wraps = float(euler_wraps)
         self.sphere_table = sphere_table
-        self.gates = self._gates()
+        self.gates = [] if self.cpc is not None else self._gates()
         self.w0, self.lbw, self.ubw = self._decision_vector()
 
     # ------------------------------------------------------------------ helpers
@@ -236,7 +258,7 @@ class ProblemSpec:
                 v = self.config.v0 * self.line.p2es(s)
                 z[3], z[4], z[5] = v
         else:
-            gate_no = n / self.phase_len if self.rk4 else (n + k / self.K) / self.phase_len
+            gate_no = n / self.guess_phase_len if self.rk4 else (n + k / self.K) / self.guess_phase_len
             xg = self.line.p2xc(gate_no)
             vg = self.line.p2es(gate_no)
             vg = vg / np.linalg.norm(vg) * self.config.v0
@@ -273,7 +295,30 @@ class ProblemSpec:
                 w0 += [0.] * self.nu
                 lbw += [v.dT_min] * self.nu
                 ubw += [v.dT_max] * self.nu
+        if self.cpc is not None:
+            w0, lbw, ubw = self._cpc_block(w0, lbw, ubw)
         return np.array(w0, float), np.array(lbw, float), np.array(ubw, float)
+
+    def _cpc_block(self, w0, lbw, ubw):
+        ''' CPC progress guess and bounds: waypoint j is passed at the node of the guess closest to
+        it (lambda_j drops from 1 to 0 after that node, mu_j = 1 there, nu_j the squared distance
+        clipped to tol^2); lambda = 1 at the first node, 0 at the last '''
+        M, P, tol2 = self.cpc_m, self.P, self.cpc['tol'] ** 2
+        pos = np.array([w0[self.col_z(q // self.K1, q % self.K1):self.col_z(q // self.K1, q % self.K1) + 3]
+                        for q in range(P)])
+        wp = self.cpc['waypoints']
+        d2 = ((pos[:, None, :] - wp[None, :, :]) ** 2).sum(-1)          # (P, M)
+        qj = np.minimum(np.maximum.accumulate(d2.argmin(0)), P - 2)      # passing node, non-decreasing in j
+        lam = (np.arange(P)[:, None] <= qj[None, :]).astype(float)
+        mu = (np.arange(P)[:, None] == qj[None, :]).astype(float)
+        nu = np.where(mu > 0, np.minimum(d2, tol2), 0.0)
+        for q in range(P):
+            w0 += [*lam[q], *mu[q], *nu[q]]
+            lo = [1.] * M if q == 0 else [0.] * M
+            hi = [0.] * M if q == P - 1 else [1.] * M
+            lbw += lo + [0.] * M + [0.] * M
+            ubw += hi + [1.] * M + [tol2] * M
+        return w0, lbw, ubw
 
     # ------------------------------------------------------------------ native spec
     def skew_closure_matrix(self):
@@ -313,4 +358,5 @@ class ProblemSpec:
             'node_geom': self.node_geom, 'node_s': self.node_s, 'interval_s': self.interval_s,
             'gates': self.gates,
             'spheres': self.sphere_table,
+            'cpc_waypoints': None if self.cpc is None else self.cpc['waypoints'],
         }

@@ -38,7 +38,7 @@ def make_line(track: str, closed: bool = True) -> SplineCenterline:
 
 def make_spec(track='race', model='drone', frame='parametric', N=50, K=4, use_quat=True, global_r=True,
               fix_gate_center=False, quat_flip=False, spheres=None, v0=1.0, h0=1, rk4=False,
-              euler_wraps=0.0, closed=True, use_dcm=False) -> ProblemSpec:
+              euler_wraps=0.0, closed=True, use_dcm=False, cpc=None) -> ProblemSpec:
     ''' ProblemSpec of a scenario the way solve_util configures it (utils/solve_util.py:29-75) '''
     line = make_line(track, closed)
     if frame == 'parametric':
@@ -54,7 +54,8 @@ def make_spec(track='race', model='drone', frame='parametric', N=50, K=4, use_qu
         veh = DroneConfig(global_r=True if frame == 'global' else global_r, use_quat=use_quat, use_dcm=use_dcm)
     else:
         veh = PointConfig(global_r=global_r)
-    return ProblemSpec(line, cfg, veh, frame, quat_flip=quat_flip, euler_wraps=euler_wraps, sphere_table=spheres)
+    return ProblemSpec(line, cfg, veh, frame, quat_flip=quat_flip, euler_wraps=euler_wraps, sphere_table=spheres,
+                       cpc=cpc)
 
 
 def make_warm_spec(x_point, **kw) -> ProblemSpec:

@@ -58,6 +58,10 @@ def parse():
     ap.add_argument('--pose', choices=['esp', 'dcm'], default='esp',
                     help='attitude: esp (quaternion, the reference\'s) or dcm (config 5\'s direction-cosine-matrix '
                          'pose, build-side): --track fig8 --pose dcm --dtype f32 --batch 8192 --no-solve')
+    ap.add_argument('--cpc', action='store_true',
+                    help='config 5\'s CPC gate-progress formulation (build-side, global frame, the gates as '
+                         'waypoints; N rounds up to the gate phases): --track fig8 --pose dcm --cpc --dtype f32 '
+                         '--batch 8192 --no-solve')
     ap.add_argument('--cpu-seconds', type=float, default=15.0, help='budget of the CPU baselines')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-solve', action='store_true', help='evaluation kernel only')
@@ -114,8 +118,8 @@ def eval_bench(spec, W, args, dev, world):
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json, encoding='utf-8'))
-            if (tj.get('batch'), tj.get('dtype'), tj.get('layout'), tj.get('track', 'race'), tj.get('pose', 'esp')) == \
-                    (B, args.dtype, args.layout, args.track, args.pose):
+            if (tj.get('batch'), tj.get('dtype'), tj.get('layout'), tj.get('track', 'race'), tj.get('pose', 'esp'),
+                    tj.get('cpc', False)) == (B, args.dtype, args.layout, args.track, args.pose, args.cpc):
                 traffic = tj.get('hbm_bytes_per_launch')
         except (OSError, ValueError):
             traffic = None
@@ -221,6 +225,10 @@ def main():
         dist.init_process_group('nccl', device_id=dev)
 
     spec_kw = dict(SPEC_KW, track=args.track, use_dcm=args.pose == 'dcm')
+    if args.cpc:
+        if not args.no_solve:
+            raise SystemExit('--cpc is an evaluation workload: add --no-solve')
+        spec_kw.update(frame='global', cpc={'waypoints': None, 'tol': 0.3})
     spec = make_spec(**spec_kw)
     B = args.batch
     track = 'racetrack' if args.track == 'race' else 'fig8'
@@ -326,7 +334,8 @@ def main():
                'steps': args.eval_steps, 'warmup': args.eval_warmup, 'ms_per_step': evals['ms_per_step'],
                'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': args.dtype,
                'data': 'synthetic: seeded cold-start instances (evaluation kernel only, --no-solve)',
-               'config': {'workload': f'{track}_parametric_{args.pose}_drone_colloc_N50_K4_eval', 'batch_per_gpu': B,
+               'config': {'workload': (f'{track}_global_{args.pose}_cpc_drone_colloc_N{spec.N}_K4_eval' if args.cpc else
+                                       f'{track}_parametric_{args.pose}_drone_colloc_N50_K4_eval'), 'batch_per_gpu': B,
                           'nz': spec.nz,
                           'global_batch': world * B, 'layout': args.layout},
                'roofline': roofline, 'cpu_baseline': None, 'evals': evals}

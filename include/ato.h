@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define ATO_ABI_VERSION 2
+#define ATO_ABI_VERSION 3
 #define ATO_KMAX 9            /* highest collocation degree supported */
 #define ATO_GEOM_WIDTH 16     /* doubles per node in the geometry table */
 
@@ -48,6 +48,7 @@ enum { ATO_ATT_ESP = 0, ATO_ATT_YPR = 1, ATO_ATT_DCM = 2 };  /* quaternion / yaw
 enum { ATO_FRAME_GLOBAL = 0, ATO_FRAME_PARAMETRIC = 1 };
 enum { ATO_TRANS_COLLOCATION = 0, ATO_TRANS_RK4 = 1 };
 enum { ATO_GATE_CIRCLE = 0, ATO_GATE_SQUARE = 1 };
+#define ATO_CPC_MAX 16
 /* Batch layout of w, g, jac, grad_f on the device.
  * INTERLEAVED:      element e of instance b at [e * B + b]  (coalesced; default)
  * INSTANCE_MAJOR:   element e of instance b at [b * n + e]  (n = nw, ng or nnz) */
@@ -104,6 +105,16 @@ typedef struct ato_problem_desc {
     const double* interval_s;  /* [N+1] s at interval starts (parametric) */
     const ato_gate* gates;     /* [n_gates] */
     const double* spheres;     /* [P][3]: dy, dn, available radius (obstacle tube) */
+    /* CPC gate progress (config 5; Foehn et al. 2021 time-optimal planning; build-side, the reference
+     * only displays a CPC trajectory, cpc_utils.py:14-101). cpc_m > 0 (global frame, no gate rows):
+     * per node q three blocks of cpc_m variables after the node variables -- progress lambda, its
+     * decrease mu, tolerance nu -- and the rows, node by node after the obstacle rows:
+     *   mu_j (|p_q - w_j|^2 - nu_j) = 0      (cpc_m complementarity rows)
+     *   lambda_j - lambda_{j+1} <= 0        (cpc_m - 1 order rows)
+     *   lambda_{q+1,j} - lambda_{q,j} + mu_{q,j} = 0   (cpc_m progress rows, not at the last node) */
+    int32_t cpc_m;             /* waypoints (<= ATO_CPC_MAX); 0: no CPC */
+    int32_t pad1;
+    double cpc_wp[ATO_CPC_MAX * 3];   /* waypoint positions w_j */
 } ato_problem_desc;
 
 typedef struct ato_handle ato_handle;

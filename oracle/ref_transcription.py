@@ -46,7 +46,7 @@ class RefNLP:
 
     def __init__(self, line, model, frame, N, K, veh=None, closed=True, fix_gate_center=False,
                  R=1e-7, dR=1e-7, h0=1, v0=1, fixed_gates=None, force_regularity=True,
-                 quat_flip=False, euler_wraps=0.0, spheres=None, rk4=False):
+                 quat_flip=False, euler_wraps=0.0, spheres=None, rk4=False, cpc=None):
         self.line, self.model, self.frame = line, model, frame
         base = dict(DRONE_DEFAULTS if model == 'drone' else POINT_DEFAULTS)
         base.update(veh or {})
@@ -67,6 +67,9 @@ class RefNLP:
         self.h0, self.v0 = h0, v0
         self.fixed_gates, self.force_regularity = fixed_gates, force_regularity
         self.quat_flip, self.euler_wraps, self.spheres = quat_flip, euler_wraps, spheres
+        # CPC gate progress (build-side, parity unpinned: the reference only displays a CPC
+        # trajectory): {'waypoints': (M, 3), 'tol': d_tol}; global frame, no gate rows
+        self.cpc = cpc
         self.Rm = np.eye(self.nu) * R if np.isscalar(R) else np.asarray(R)
         self.dRm = np.eye(self.nu) * dR if np.isscalar(dR) else np.asarray(dR)
         # BaseRaceline._setup_checks (base_raceline.py:226-230), run first by the global override
@@ -89,6 +92,9 @@ class RefNLP:
         else:
             self.tau, self.B, self.C, self.D = coefficients(K)
         self.nw = N + N * (K + 1) * self.nv
+        self.cpc_m = 0 if cpc is None else len(cpc['waypoints'])
+        self.cpc_off = self.nw
+        self.nw += N * (K + 1) * 3 * self.cpc_m
         self._geo_cache = {}
         self.lbg, self.ubg = None, None
         self.w0, self.lbw, self.ubw = self._decision_vector()
@@ -211,6 +217,12 @@ class RefNLP:
                 w0 += self._guess_z(n, k) + [0.] * self.nu + [0.] * self.nu
                 lbw += zl + [v['T_min']] * self.nu + [v['dT_min']] * self.nu
                 ubw += zu + [v['T_max']] * self.nu + [v['dT_max']] * self.nu
+        M = self.cpc_m
+        for q in range(self.N * (self.K + 1)):
+            if M:
+                w0 += [1.] * M + [0.] * M + [0.] * M
+                lbw += [0.] * 3 * M
+                ubw += [1.] * 2 * M + [self.cpc['tol'] ** 2] * M
         return np.array(w0, float), np.array(lbw, float), np.array(ubw, float)
 
     # -------------------------------------------------------------- g(w)
@@ -234,7 +246,7 @@ class RefNLP:
         param = self.frame == 'parametric'
         # BaseGlobalRaceline._enforce_model: equal step sizes within a phase
         if not param:
-            gi = self.gate_n_interval
+            gi = N if self.cpc_m else self.gate_n_interval      # CPC: one total time
             for n in range(0, N, gi):
                 for n2 in range(n + 1, n + gi):
                     add(H[n2] - H[n], 0., 0.)
@@ -373,7 +385,7 @@ class RefNLP:
                 gs = self.geo(s)
                 x_gate = gs['xc'][:, None] + z_gate[1] * gs['ey'][:, None] + z_gate[2] * gs['en'][:, None]
                 self._fix_gate(add, x_gate, s, False)
-        else:
+        elif not self.cpc_m:
             for gate_no, n in enumerate(range(0, N, self.gate_n_interval)):
                 self._fix_gate(add, Z[n][0][:3], gate_no, True)
             if not self.closed:
@@ -386,6 +398,25 @@ class RefNLP:
                     dy, dn, r = self.spheres[n * (K + 1) + k]
                     z = Z[n][k]
                     add((z[1] - dy) ** 2 + (z[2] - dn) ** 2, -inf, max(r, 0) ** 2)
+
+        if self.cpc_m:
+            # CPC gate progress (Foehn et al. 2021), node by node in time order: complementarity
+            # mu_j (|p - w_j|^2 - nu_j) = 0, order lambda_j <= lambda_{j+1}, progress
+            # lambda_{q+1} = lambda_q - mu_q
+            M, P = self.cpc_m, N * (K + 1)
+            wp = np.asarray(self.cpc['waypoints'], float)
+            blk = [w[self.cpc_off + 3 * M * q:self.cpc_off + 3 * M * (q + 1)] for q in range(P)]
+            for q in range(P):
+                z = Z[q // (K + 1)][q % (K + 1)]
+                lam, mu, nu = blk[q][:M], blk[q][M:2 * M], blk[q][2 * M:]
+                for j in range(M):
+                    d2 = (z[0] - wp[j, 0]) ** 2 + (z[1] - wp[j, 1]) ** 2 + (z[2] - wp[j, 2]) ** 2 - nu[j]
+                    add(mu[j] * d2, 0., 0.)
+                for j in range(M - 1):
+                    add(lam[j] - lam[j + 1], -inf, 0.)
+                if q + 1 < P:
+                    for j in range(M):
+                        add(blk[q + 1][j] - lam[j] + mu[j], 0., 0.)
 
         if self.model == 'drone' and self.closed:
             # DroneRaceline._enforce_modified_loop_closure (only for closed lines, drone_raceline.py:153)

@@ -7,8 +7,11 @@ frame, global_r, N = 50, K = 4) in fp32 over a batch of 8192 seeded instances on
     Newton-Schulz continuity operator (csrc/ato_program.hpp AttOp). Its parity with the reference is
     unpinned by construction; it is pinned by equivalence with the ESP path (tests/test_dcm_cpu.py:
     mapped-state ODE rows, warm-start lap time) and here by the 50 x 4 warm-start solve on the device.
-The CPC gate-progress NLP of fig_8_cpc.py exists only as a CSV display in the reference
-(utils/cpc_utils.py:14-101) and is not evaluated here.
+  * the CPC gate-progress formulation (Foehn et al. 2021) with the DCM pose: fig_8_cpc.py shows a CPC
+    trajectory only as a CSV display (utils/cpc_utils.py:14-101), so the NLP is build-side and its
+    parity is UNPINNED (checked against the oracle's restatement, tests/test_cpc_cpu.py). CPC is a
+    global-frame formulation: the fig-8 gates become its 8 waypoints and N rounds up to the gate
+    phases (56 x 4); each instance gets seeded progress / tolerance values and a perturbed path.
 
 Pins: the fp64 kernel on the same batch against the numpy oracle (ESP: the reference-pinned
 restatement; DCM: its restatement, tests/test_programs_cpu.py) on instances spread over the batch
@@ -27,7 +30,20 @@ torch = pytest.importorskip('torch')
 
 B = 8192
 CFG = dict(track='fig8', model='drone', frame='parametric', N=50, K=4, use_quat=True, global_r=True)
-POSES = {'esp': {}, 'dcm': {'use_dcm': True}}
+POSES = {'esp': {}, 'dcm': {'use_dcm': True},
+         'dcm_cpc': {'use_dcm': True, 'frame': 'global', 'cpc': {'waypoints': None, 'tol': 0.3}}}
+
+
+def _cpc_instances(spec, W):
+    ''' seeded progress, decrease and tolerance values and a perturbed path per instance '''
+    rng = np.random.default_rng(11)
+    W = W.copy()
+    M, P = spec.cpc_m, spec.P
+    W[:, spec.cpc_off:] = rng.random((len(W), P * 3 * M)) * np.tile(np.repeat([1.0, 1.0, spec.cpc['tol'] ** 2], M), P)
+    for q in range(P):
+        c = spec.col_z(q // spec.K1, q % spec.K1)
+        W[:, c:c + 3] += rng.normal(0.0, 0.2, (len(W), 3))
+    return W
 
 
 def _close(a, b, scale_tol):
@@ -42,6 +58,9 @@ def batch(request):
     cfg = dict(CFG, **POSES[request.param])
     spec = product_spec(**cfg)
     W, _, _ = seeded_instances(spec, range(B))
+    if spec.cpc is not None:
+        cfg['cpc'] = spec.cpc                     # the waypoints the spec resolved, for the oracle
+        W = _cpc_instances(spec, W)
     out = {}
     for dt in (torch.float64, torch.float32):
         bn = BatchedNLP(spec, B, dtype=dt)

@@ -83,6 +83,10 @@ for s in $STEPS; do
         solvesad) for v in 0 1; do
                    ATO_KKT_SADDLE=$v run solve_sad$v 600 python tools/solve_batched.py --batch 512 --max-iter 1000 --cold --no-host --out "$OUT/solve_sad$v.json"
                done ;;
+        cpc5)  run bench5_cpc_f32 300 python bench.py --track fig8 --pose dcm --cpc --dtype f32 --batch 8192 --no-solve --no-cpu-baseline --eval-steps 50
+               run bench5_cpc_f64 300 python bench.py --track fig8 --pose dcm --cpc --dtype f64 --batch 8192 --no-solve --no-cpu-baseline --eval-steps 50
+               run prof5_cpc 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof5_cpc" -o run -- \
+                   python bench.py --track fig8 --pose dcm --cpc --dtype f32 --batch 8192 --no-solve --no-cpu-baseline --eval-steps 30 ;;
         kktq)  run kkt_b512 200 python tools/bench_kkt.py --batch 512 --out "$OUT/kkt_b512.json"
                run kkt_b1 200 python tools/bench_kkt.py --batch 1 --out "$OUT/kkt_b1.json" ;;
         ipmktests) run pytest_ipmk 300 python -u -m pytest tests/test_gpu_ipm_kernels.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider ;;
