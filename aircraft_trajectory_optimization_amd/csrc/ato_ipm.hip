@@ -562,9 +562,49 @@ __global__ __launch_bounds__(CB) void k_filter_accept(int W, int fmax, const dou
     soc_out[b] = (pd && !ok && first[b] != 0 && tt >= th) ? 1 : 0;
 }
 
+// ------------------------------------------------------------------------------------------
+// KKT diagonals of one inertia-correction pass (batched_ipm.py _kkt_step): dx = Sx + dw,
+// Ds = Ss + dw, dr = -dc on every row and -dc - 1 / Ds on the slack rows; one thread per element
+// of [variables | slack rows | equality rows] x column
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_kkt_diag(Dev d, const double* __restrict__ Sx, const double* __restrict__ Ss,
+                                                  const double* __restrict__ dw, const double* __restrict__ dc,
+                                                  double* __restrict__ dx, double* __restrict__ dr,
+                                                  double* __restrict__ Ds) {
+    const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
+    const long long nW = (long long)d.n * d.W, iW = (long long)d.mi * d.W, eW = (long long)d.meq * d.W;
+    if (t < nW) {
+        const int b = (int)(t % d.W);
+        dx[t] = Sx[t] + dw[b];
+    } else if (t < nW + iW) {
+        const long long u = t - nW;
+        const int r = (int)(u / d.W), b = (int)(u - (long long)r * d.W);
+        const double ds = Ss[u] + dw[b];
+        Ds[u] = ds;
+        dr[at(d, d.iin[r], b)] = -dc[b] - 1.0 / ds;
+    } else if (t < nW + iW + eW) {
+        const long long u = t - nW - iW;
+        const int r = (int)(u / d.W), b = (int)(u - (long long)r * d.W);
+        dr[at(d, d.ieq[r], b)] = -dc[b];
+    }
+}
+
 }  // namespace
 
 extern "C" {
+
+int ato_ipm_kkt_diag(const ato_ipm_dims* d, const double* Sx, const double* Ss, const double* dw, const double* dc,
+                     double* dx, double* dr, double* Ds, void* stream) {
+    if (!d || d->n < 0 || d->mi < 0 || d->meq < 0 || d->mi + d->meq != d->m || d->W <= 0 || !Sx || !dw || !dc ||
+        !dx || !dr || (d->mi && (!Ss || !Ds || !d->iin)) || (d->meq && !d->ieq))
+        return fail(ATO_ERR_ARG, "ato_ipm_kkt_diag: arguments");
+    const Dev v{d->n, d->m, d->mi, d->meq, d->W, d->iin, d->ieq, nullptr, nullptr, nullptr, nullptr};
+    const long long cnt = (long long)(d->n + d->m) * d->W;
+    if (cnt)
+        hipLaunchKernelGGL(k_kkt_diag, dim3(lin_blocks(cnt)), dim3(256), 0, static_cast<hipStream_t>(stream), v, Sx,
+                           Ss, dw, dc, dx, dr, Ds);
+    return check_launch("ato_ipm_kkt_diag");
+}
 
 size_t ato_ipm_work_size(const ato_ipm_dims* d) {
     if (!d || d->W <= 0) return 0;

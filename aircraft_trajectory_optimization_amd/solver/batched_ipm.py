@@ -566,6 +566,16 @@ class BatchedInteriorPoint:
         good = ok & torch.isfinite(y).all(0) & (y.abs().amax(0) <= self.o.constr_mult_init_max)
         return torch.where(good[None, :], y, torch.zeros_like(y))
 
+    def _kkt_diag(self, Sx, Ss, dw, dc):
+        ''' KKT diagonals for per-column perturbations dw, dc: dx = Sx + dw, Ds = Ss + dw, dr = -dc
+        (and -dc - 1 / Ds on the slack rows); one fused kernel on the device '''
+        if self.vk is not None:
+            return self.vk.kkt_diag(Sx, Ss, dw, dc)
+        Ds = Ss + dw
+        dr = (-dc).expand(self.m, self.B).clone()
+        dr[self.iin] -= 1.0 / Ds
+        return Sx + dw, dr, Ds
+
     def _kkt_step(self, W, Js, Sx, Ss, rhs_x, rhs_s, rhs_y, mu, dwl, act, start_dw=None, start_dc=None):
         '''
         Newton step with IPOPT's inertia correction, per instance. Returns
@@ -589,9 +599,6 @@ class BatchedInteriorPoint:
         pend = act.clone()
         ok_all = torch.zeros(B, dtype=torch.bool, device=self.dev)
         sol = torch.zeros((n + m, B), dtype=torch.float64, device=self.dev)
-        Ds_used = torch.ones_like(Ss)
-        dx_used = torch.zeros((n, B), dtype=torch.float64, device=self.dev)
-        dr_used = torch.zeros((m, B), dtype=torch.float64, device=self.dev)
         dw_out = zeros.clone()
         dc_out = zeros.clone()
         pidx = _idx(pend)
@@ -619,10 +626,7 @@ class BatchedInteriorPoint:
         # as before; only the order between instances changes.
         while True:
             while len(pidx):
-                Ds_tot = Ss + delta_w
-                dr = (-delta_c).expand(m, B).clone()
-                dr[self.iin] -= 1.0 / Ds_tot
-                dx = Sx + delta_w
+                dx, dr, _ = self._kkt_diag(Sx, Ss, delta_w, delta_c)
                 self.laps.lap('kkt_other')
                 inertia = self.kkt.factor(W, Js, dx, dr, pidx)
                 # first pass (delta_w = 0) vs the inertia-correction retries, timed apart
@@ -636,10 +640,6 @@ class BatchedInteriorPoint:
                 ok = (inertia[:, 0] == n) & (inertia[:, 1] == m) & (inertia[:, 2] == 0)
                 sing = inertia[:, 2] > 0
                 good = pend & ok & ~sing
-                g2 = good[None, :]
-                Ds_used = torch.where(g2, Ds_tot, Ds_used)
-                dx_used = torch.where(g2, dx, dx_used)
-                dr_used = torch.where(g2, dr, dr_used)
                 dw_out = torch.where(good, delta_w, dw_out)
                 dc_out = torch.where(good, delta_c, dc_out)
                 tosolve = tosolve | good
@@ -648,6 +648,8 @@ class BatchedInteriorPoint:
             sidx = _idx(tosolve)
             if not len(sidx):
                 break
+            # the diagonals of every instance's accepted pass (bitwise those it was factorised with)
+            dx_used, dr_used, Ds_used = self._kkt_diag(Sx, Ss, dw_out, dc_out)
             ry = rhs_y.clone()
             ry[self.iin] += rhs_s / Ds_used
             xs = self._solve(torch.cat([rhs_x, ry]), tosolve, W, Js, dx_used, dr_used, idx=sidx)
@@ -661,6 +663,7 @@ class BatchedInteriorPoint:
             pidx = _idx(pend)
             if not len(pidx):
                 break
+        dx_used, dr_used, Ds_used = self._kkt_diag(Sx, Ss, dw_out, dc_out)
         dxs, dy = sol[:n], sol[n:]
         ds = (rhs_s + dy[self.iin]) / Ds_used
         ctx = (W, Js, dx_used, dr_used, Ds_used)

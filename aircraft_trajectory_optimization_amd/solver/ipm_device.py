@@ -139,6 +139,19 @@ class DeviceIPMKernels:
                     'ato_ipm_multipliers')
         return tuple(z)
 
+    def kkt_diag(self, Sx, Ss, dw, dc):
+        ''' (dx [n, W], dr [m, W], Ds [mi, W]) of one inertia-correction pass: new tensors '''
+        W = Sx.shape[1]
+        n, m, mi = self.n, self.m, self.mi
+        d, _ = self.dims(W)
+        dx = torch.empty((n, W), dtype=torch.float64, device=self.device)
+        dr = torch.empty((m, W), dtype=torch.float64, device=self.device)
+        Ds = torch.empty((mi, W), dtype=torch.float64, device=self.device)
+        self._check(self.lib.ato_ipm_kkt_diag(d, _p(self._v(Sx, n, W)), _p(self._v(Ss, mi, W)), _p(self._c(dw, W)),
+                                              _p(self._c(dc, W)), _p(dx), _p(dr), _p(Ds), self._stream()),
+                    'ato_ipm_kkt_diag')
+        return dx, dr, Ds
+
     def filter_accept(self, theta, phi, gphi_d, alpha, tht, pht, F, nf, theta_max, theta_min, pend, first, o):
         ''' (ok, arm, soc) bool [W]: the filter test of a trial point for the searching columns
         (batched_ipm.py _accept, `& pend`) and the columns that try a second-order correction '''

@@ -43,6 +43,12 @@ typedef struct ato_ipm_bounds {
     const double* dU;
 } ato_ipm_bounds;
 
+/* KKT diagonals of one inertia-correction pass (batched_ipm.py _kkt_step, IPOPT's perturbed
+ * augmented system): dx = Sx + dw [n][W], Ds = Ss + dw [mi][W], dr [m][W] = -dc on equality rows and
+ * -dc - 1 / Ds on slack rows; dw, dc [W] the per-column delta_w / delta_c. */
+int ato_ipm_kkt_diag(const ato_ipm_dims* d, const double* Sx, const double* Ss, const double* dw, const double* dc,
+                     double* dx, double* dr, double* Ds, void* stream);
+
 /* doubles of workspace the reductions below need for these dimensions */
 size_t ato_ipm_work_size(const ato_ipm_dims* d);
 
