@@ -117,6 +117,8 @@ for s in $STEPS; do
                done ;;
         listpmc) run listpmc 120 rocprofv3 -L ;;
         mb)    run mb_store 120 ./tools/mb_store ;;
+        mbscale) run mb_store_scale 120 ./tools/mb_store_scale
+               run bench_b4096 300 python bench.py --steps 20 --warmup 5 --batch 4096 --no-cpu-baseline --no-solve --eval-steps 30 ;;
         mbpmc) run mb_fetch 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/mb_fetch" -o run -- ./tools/mb_store
                run mb_write 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/mb_write" -o run -- ./tools/mb_store ;;
         units) for k in 0 1 2 3 4 12 34; do
