@@ -47,7 +47,8 @@ static void release(ato_handle* h) {
     (void)hipFree(h->d_units);
     (void)hipFree(h->d_units_lf);
     (void)hipFree(h->d_fpart);
-    for (int32_t* d : {h->d_color, h->d_take_e, h->d_take_r, h->d_csc_ptr, h->d_csc_ent, h->d_csc_row}) (void)hipFree(d);
+    for (int32_t* d : {h->d_color, h->d_take_e, h->d_take_r, h->d_tk_ptr, h->d_tk_ent, h->d_tk_row}) (void)hipFree(d);
+    (void)hipFree(h->d_amask);
     (void)hipFree(h->d_dJ);
     (void)hipFree(h->d_dgf);
     for (hipEvent_t e : h->events) (void)hipEventDestroy(e);
@@ -119,6 +120,8 @@ int ato_create(const ato_problem_desc* desc, ato_handle** out) {
     h->pd_lf = h->pd;
     h->pd_lf.units = h->d_units_lf;
     if (const char* e = std::getenv("ATO_LONGFIRST_MAX_B")) h->lf_max_batch = std::atoi(e);
+    if (const char* e = std::getenv("ATO_EVAL_TILE")) h->eval_tile = std::atoi(e);
+    if (const char* e = std::getenv("ATO_EVAL_TILE_LF")) h->tile_lf = std::atoi(e) != 0;
     *out = h;
     return ATO_OK;
 }
@@ -214,8 +217,10 @@ static int eval_impl(ato_handle* h, int32_t batch, int32_t layout, const T* w, T
         int rc = ato_reserve(h, batch);
         if (rc) return rc;
     }
-    // small batches run the long-first unit order (see Layout::build_units)
-    const ato::ProbD& p = batch <= h->lf_max_batch ? h->pd_lf : h->pd;
+    // small batches run the long-first unit order (see Layout::build_units); larger ones run in
+    // instance tiles of eval_tile chunks (long-first inside a tile when tile_lf)
+    const bool tiled = batch > h->lf_max_batch && h->eval_tile > 0;
+    const ato::ProbD& p = batch <= h->lf_max_batch || (tiled && h->tile_lf) ? h->pd_lf : h->pd;
     hipError_t e = hipSuccess;
     ato::with_model(p, [&]<class M>() {
         hipEvent_t* ev = nullptr;
@@ -224,7 +229,7 @@ static int eval_impl(ato_handle* h, int32_t batch, int32_t layout, const T* w, T
         if (sample && (size_t)(h->timed_calls + 1) * 3 <= h->events.size())
             ev = &h->events[(size_t)h->timed_calls++ * 3];
         e = ato::launch_eval<M, T>(p, batch, layout, w, g, jac, grad_f, f, (T*)h->d_fpart, (hipStream_t)stream,
-                                   ev);
+                                   ev, tiled ? h->eval_tile : 0);
     });
     if (e != hipSuccess) return fail(ATO_ERR_HIP, std::string("kernel launch: ") + hipGetErrorString(e));
     return ATO_OK;
@@ -279,8 +284,9 @@ static int ensure_hess(ato_handle* h) {
     if (!err.empty()) return fail(ATO_ERR_UNSUPPORTED, err);
     int rc;
     if ((rc = upload(h->HL.color, &h->d_color)) || (rc = upload(h->HL.take_e, &h->d_take_e)) ||
-        (rc = upload(h->HL.take_r, &h->d_take_r)) || (rc = upload(h->HL.csc_ptr, &h->d_csc_ptr)) ||
-        (rc = upload(h->HL.csc_ent, &h->d_csc_ent)) || (rc = upload(h->HL.csc_row, &h->d_csc_row)))
+        (rc = upload(h->HL.take_r, &h->d_take_r)) || (rc = upload(h->HL.tk_ptr, &h->d_tk_ptr)) ||
+        (rc = upload(h->HL.tk_ent, &h->d_tk_ent)) || (rc = upload(h->HL.tk_row, &h->d_tk_row)) ||
+        (rc = upload(h->HL.amask, &h->d_amask)))
         return rc;
     h->hess_ready = true;
     return ATO_OK;
@@ -308,7 +314,8 @@ extern "C" int ato_hess_eval(ato_handle* h, int32_t batch, int32_t layout, const
     int rc = ensure_hess(h);
     if (rc) return rc;
     if ((rc = hess_reserve(h, batch))) return rc;
-    const ato::HessDev hd{h->d_color, h->d_take_e, h->d_take_r, h->d_csc_ptr, h->d_csc_ent, h->d_csc_row,
+    const ato::HessDev hd{h->d_color, h->d_take_e, h->d_take_r, h->d_tk_ptr, h->d_tk_ent, h->d_tk_row,
+                          h->d_amask, h->HL.mask_words,
                           h->HL.take_off.data(), h->HL.n_colors, h->HL.nnz()};
     hipError_t e = hipSuccess;
     const ato::ProbD& p = batch <= h->lf_max_batch ? h->pd_lf : h->pd;   // unit order as in ato_eval

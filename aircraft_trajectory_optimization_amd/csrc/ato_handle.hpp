@@ -10,6 +10,11 @@ struct ato_handle {
     ato::ProbD pd{};            // device-pointer copy of L.p (interval-major unit table)
     ato::ProbD pd_lf{};         // the same with the long-first unit table (batches <= lf_max_batch)
     int32_t lf_max_batch = 2048;
+    // batches above lf_max_batch: the workgroup order runs eval_tile 64-instance chunks through every
+    // unit before the next chunks start (0 = one pass per unit over the whole batch); tile_lf picks
+    // the long-first unit table inside the tiles
+    int32_t eval_tile = 8;
+    bool tile_lf = true;
     double* d_geom = nullptr;
     double* d_node_s = nullptr;
     double* d_interval_s = nullptr;
@@ -30,7 +35,8 @@ struct ato_handle {
     bool hess_ready = false;
     ato::HessLayout HL;
     int32_t *d_color = nullptr, *d_take_e = nullptr, *d_take_r = nullptr;
-    int32_t *d_csc_ptr = nullptr, *d_csc_ent = nullptr, *d_csc_row = nullptr;
+    int32_t *d_tk_ptr = nullptr, *d_tk_ent = nullptr, *d_tk_row = nullptr;
+    uint32_t* d_amask = nullptr;
     double* d_dJ = nullptr;     // [nnz][hess_reserved] Jacobian tangents of one colour
     double* d_dgf = nullptr;    // [nw][hess_reserved] grad f tangents of one colour
     int32_t hess_reserved = 0;

@@ -80,15 +80,24 @@ struct DepW {
     double par(long) const { return 0.0; }     // per-instance constants depend on nothing
 };
 
-// records (column of the entry, variable its value depends on) pairs
+// records (column of the entry, variable its value depends on) pairs, and per Jacobian entry (in
+// the sinks' entry order) its column and dependency set
 struct DepSink {
     std::vector<std::pair<int32_t, int32_t>>* pairs;
-    void begin(int, int) {}
+    std::vector<std::vector<int32_t>>* ent_dep = nullptr;
+    std::vector<int32_t>* ent_col = nullptr;
+    int cur = 0;
+    void begin(int, int nnz0) { cur = nnz0; }
     void jac(int col, const Dep& v) {
         for (int32_t k : v.s) pairs->push_back({col, k});
+        if (ent_dep) {
+            (*ent_dep)[cur] = v.s;
+            (*ent_col)[cur] = col;
+        }
+        ++cur;
     }
     void row(const Dep&, double, double) {}
-    void skip() {}
+    void skip() { ++cur; }
     void row_skip() {}
     void finish() {}
 };
@@ -111,6 +120,13 @@ struct HessLayout {
     std::vector<int32_t> take_e, take_r;
     // CSC of the Jacobian: column r -> (J entry index, J row)
     std::vector<int32_t> csc_ptr, csc_ent, csc_row;
+    // Colour c's seeded pass changes only the Jacobian entries that depend on a variable of colour c
+    // (the tangent of every other entry is exactly 0): amask[c * mask_words + e / 32] bit e % 32 marks
+    // them -- the only tangents the device pass stores -- and take t sums over just those entries of
+    // its column: (J entry, J row) = (tk_ent, tk_row)[tk_ptr[t] .. tk_ptr[t + 1])
+    std::vector<uint32_t> amask;
+    int mask_words = 0;
+    std::vector<int32_t> tk_ptr, tk_ent, tk_row;
     int nnz() const { return (int)col.size(); }
 
     // structure analysis + colouring (host only; defined in ato_hstruct.cpp, compiled by the host
@@ -139,8 +155,11 @@ std::string HessLayout::build(const Layout& L) {
     const ProbD& p = L.p;
     const int nw = p.nw;
     std::vector<std::pair<int32_t, int32_t>> pairs;
+    const int nnzJ = (int)L.col.size();
+    std::vector<std::vector<int32_t>> ent_dep(nnzJ);
+    std::vector<int32_t> ent_col(nnzJ, -1);
     const bool ok = with_model(p, [&]<class M>() {
-        DepSink s{&pairs};
+        DepSink s{&pairs, &ent_dep, &ent_col};
         DepGrad go{&pairs};
         for (int u = 0; u < p.n_units; ++u) {
             const int32_t* ut = p.units + 4 * u;
@@ -229,7 +248,8 @@ std::string HessLayout::build(const Layout& L) {
     std::string err = verify(adj, is_hub);
     if (!err.empty()) return err;
     // CSC of J
-    const int nnzJ = (int)L.col.size();
+    for (int e = 0; e < nnzJ; ++e)
+        if (ent_col[e] != L.col[e]) return "hessian: seeded-pass entry order differs from the Jacobian pattern";
     csc_ptr.assign(nw + 1, 0);
     for (int e = 0; e < nnzJ; ++e) ++csc_ptr[L.col[e] + 1];
     for (int r = 0; r < nw; ++r) csc_ptr[r + 1] += csc_ptr[r];
@@ -242,17 +262,41 @@ std::string HessLayout::build(const Layout& L) {
             csc_ent[t] = e;
             csc_row[t] = i;
         }
+    // per-colour active entries and the take lists over them
+    mask_words = (nnzJ + 31) / 32;
+    amask.assign((size_t)n_colors * mask_words, 0u);
+    for (int e = 0; e < nnzJ; ++e)
+        for (int32_t k : ent_dep[e]) {
+            const int c = color[k];
+            amask[(size_t)c * mask_words + e / 32] |= 1u << (e % 32);
+        }
+    tk_ptr.assign(take_r.size() + 1, 0);
+    tk_ent.clear();
+    tk_row.clear();
+    for (int c = 0; c < n_colors; ++c)
+        for (int t = take_off[c]; t < take_off[c + 1]; ++t) {
+            const int r = take_r[t];
+            for (int q = csc_ptr[r]; q < csc_ptr[r + 1]; ++q) {
+                const int e = csc_ent[q];
+                if (amask[(size_t)c * mask_words + e / 32] >> (e % 32) & 1u) {
+                    tk_ent.push_back(e);
+                    tk_row.push_back(csc_row[q]);
+                }
+            }
+            tk_ptr[t + 1] = (int32_t)tk_ent.size();
+        }
     return "";
 }
 #endif
 
-// (H v_c)_r for one take: sigma dgf[r] + sum over Jacobian column r of lambda_i dJ_e
-// (element strides: lam / dJ / dgf by their own stride; the caller offsets to the instance)
+// (H v_c)_r for take t (row r): sigma dgf[r] + sum over the entries of Jacobian column r that colour c
+// changes of lambda_i dJ_e (the others add exact zeros); element strides: lam / dJ / dgf by their own
+// stride, the caller offsets to the instance
 template <class T>
-ATO_HD T hess_take(const int32_t* csc_ptr, const int32_t* csc_ent, const int32_t* csc_row, int r, T sigma,
+ATO_HD T hess_take(const int32_t* tk_ptr, const int32_t* tk_ent, const int32_t* tk_row, int t, int r, T sigma,
                    const T* lam, long ls, const T* dJ, long js, const T* dgf, long gs) {
     T acc = sigma * dgf[(long)r * gs];
-    for (int t = csc_ptr[r]; t < csc_ptr[r + 1]; ++t) acc += lam[(long)csc_row[t] * ls] * dJ[(long)csc_ent[t] * js];
+    for (int q = tk_ptr[t]; q < tk_ptr[t + 1]; ++q) acc += lam[(long)tk_row[q] * ls] * dJ[(long)tk_ent[q] * js];
     return acc;
 }
 

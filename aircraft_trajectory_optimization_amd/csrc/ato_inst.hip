@@ -34,9 +34,9 @@ using Model = DroneModel<DCM, PARAM_GR>;
 using Model = DroneModel<DCM, PARAM_REL>;
 #endif
 template hipError_t launch_eval<Model, double>(const ProbD&, int, int, const double*, double*, double*, double*,
-                                              double*, double*, hipStream_t, hipEvent_t*);
+                                              double*, double*, hipStream_t, hipEvent_t*, int);
 template hipError_t launch_hess<Model>(const ProbD&, const HessDev&, int, int, const double*, const double*,
                                        const double*, double*, double*, double*, hipStream_t);
 template hipError_t launch_eval<Model, float>(const ProbD&, int, int, const float*, float*, float*, float*,
-                                             float*, float*, hipStream_t, hipEvent_t*);
+                                             float*, float*, hipStream_t, hipEvent_t*, int);
 }  // namespace ato

@@ -253,7 +253,7 @@ template <class M, class T, int KS, bool WJ, bool WG, bool WF, int UMASK>
 __global__ __launch_bounds__(WAVE) void k_eval(ProbD p, int B, int layout, const T* __restrict__ w,
                                                T* __restrict__ g, T* __restrict__ J,
                                                T* __restrict__ gf, T* __restrict__ fpart) {
-    const int b = blockIdx.x * WAVE + threadIdx.x;
+    const int b = (blockIdx.z * gridDim.x + blockIdx.x) * WAVE + threadIdx.x;   // z: instance tile (launch_eval)
     if (b >= B) return;
     const int32_t* ut = p.units + 4 * blockIdx.y;      // wave-uniform: scalar loads
     long st;
@@ -321,7 +321,8 @@ __global__ __launch_bounds__(WAVE) ATO_EVAL_ATTR void k_eval_paired(ProbD p, int
                                                       T* __restrict__ gf, T* __restrict__ fpart) {
     constexpr bool QUAD = FULL && ATO_EVAL_F32_QUAD && std::is_same_v<T, float>;
     const int l = threadIdx.x;
-    const int chunk = blockIdx.x * WAVE;
+    const int chunk = (blockIdx.z * gridDim.x + blockIdx.x) * WAVE;   // z: instance tile (launch_eval)
+    if (chunk >= B) return;                                            // past the end of the last tile
     // instance of this lane inside the chunk
     const int own = QUAD ? 4 * (l & 15) + (l >> 4) : 2 * (l & 31) + (l >> 5);
     const int b = chunk + own;
@@ -372,17 +373,28 @@ __global__ __launch_bounds__(256) void k_cost_reduce(int N, int B, const T* __re
 
 // ------------------------------------------------------------------ Hessian of the Lagrangian
 // Tangents of the Jacobian entries of a seeded pass (see ato_hessian.hpp); g rows are ignored.
+// Only the entries that the colour changes are stored (HessLayout::amask, this colour's row): the
+// take lists read no others, and the rest of the tangents are exact zeros.
 template <class T>
 struct DevTangentSink {
     T* J;
     long je, e;
-    __device__ __forceinline__ void begin(int, int nnz0) { e = (long)nnz0 * je; }
+    const uint32_t* mask;
+    int ei;                                   // entry index (wave-uniform)
+    __device__ __forceinline__ void begin(int, int nnz0) {
+        e = (long)nnz0 * je;
+        ei = nnz0;
+    }
     __device__ __forceinline__ void jac(int, const Dual<T, 1>& v) {
-        J[e] = v.d[0];
+        if (mask[ei >> 5] >> (ei & 31) & 1u) J[e] = v.d[0];
         e += je;
+        ++ei;
     }
     __device__ __forceinline__ void row(const Dual<T, 1>&, double, double) {}
-    __device__ __forceinline__ void skip() { e += je; }
+    __device__ __forceinline__ void skip() {
+        e += je;
+        ++ei;
+    }
     __device__ __forceinline__ void row_skip() {}
     __device__ __forceinline__ void finish() {}
 };
@@ -392,6 +404,7 @@ struct DevTangentSink {
 template <class M, int UMASK>
 __global__ __launch_bounds__(WAVE) void k_hess_dual(ProbD p, int B, int layout, const double* __restrict__ w,
                                                    const int32_t* __restrict__ color, int c,
+                                                   const uint32_t* __restrict__ amask,
                                                    double* __restrict__ dJ, double* __restrict__ dgf) {
     const int b = blockIdx.x * WAVE + threadIdx.x;
     if (b >= B) return;
@@ -400,7 +413,7 @@ __global__ __launch_bounds__(WAVE) void k_hess_dual(ProbD p, int B, int layout, 
     const ColorW<double, DevW<double>> W{DevW<double>{il ? w + b : w + (long)b * p.nw, il ? (long)B : 1L,
                                                       p.isph ? p.isph + b : nullptr, (long)p.isph_stride},
                                          color, c};
-    DevTangentSink<double> s{dJ + b, (long)B, 0};
+    DevTangentSink<double> s{dJ + b, (long)B, 0, amask, 0};
     const TangentGrad<double> go{dgf + b, (long)B};
     run_unit<M, Dual<double, 1>, 0, true, true, UMASK>(p, ut[0], ut[1], ut[2], W, s, go);
 }
@@ -411,9 +424,9 @@ template <int UNUSED = 0>
 __global__ __launch_bounds__(WAVE) void k_hess_take(int B, int layout, int ng, int nnzh, int t0,
                                                    const int32_t* __restrict__ take_e,
                                                    const int32_t* __restrict__ take_r,
-                                                   const int32_t* __restrict__ csc_ptr,
-                                                   const int32_t* __restrict__ csc_ent,
-                                                   const int32_t* __restrict__ csc_row,
+                                                   const int32_t* __restrict__ tk_ptr,
+                                                   const int32_t* __restrict__ tk_ent,
+                                                   const int32_t* __restrict__ tk_row,
                                                    const double* __restrict__ lam, const double* __restrict__ sigma,
                                                    const double* __restrict__ dJ, const double* __restrict__ dgf,
                                                    double* __restrict__ H) {
@@ -424,14 +437,16 @@ __global__ __launch_bounds__(WAVE) void k_hess_take(int B, int layout, int ng, i
     const bool il = layout == ATO_LAYOUT_INTERLEAVED;
     const double* lb = il ? lam + b : lam + (long)b * ng;
     const long ls = il ? (long)B : 1L;
-    const double v = hess_take(csc_ptr, csc_ent, csc_row, r, sigma[b], lb, ls, dJ + b, (long)B, dgf + b, (long)B);
+    const double v = hess_take(tk_ptr, tk_ent, tk_row, t, r, sigma[b], lb, ls, dJ + b, (long)B, dgf + b, (long)B);
     if (il) H[(long)e * B + b] = v;
     else H[(long)b * nnzh + e] = v;
 }
 
 // device copies of the HessLayout tables
 struct HessDev {
-    const int32_t *color, *take_e, *take_r, *csc_ptr, *csc_ent, *csc_row;
+    const int32_t *color, *take_e, *take_r, *tk_ptr, *tk_ent, *tk_row;
+    const uint32_t* amask;          // [n_colors][mask_words]
+    int mask_words;
     const int32_t* take_off_host;   // host array [n_colors + 1]
     int n_colors, nnzh;
 };
@@ -443,14 +458,16 @@ hipError_t launch_hess(const ProbD& p, const HessDev& hd, int B, int layout, con
 // Host-side launcher, explicitly instantiated per model in ato_inst.hip (one translation unit
 // per model variant so the library builds in parallel).
 // ev (optional): events recorded before / after the g, J kernels and after the cost reduction
+// tile > 0: instance-tiled workgroup order -- grid (tile, units, tiles), so the dispatcher (x fastest,
+// z slowest) runs tile 64-instance chunks through every unit before the next tile starts
 template <class M, class T>
 hipError_t launch_eval(const ProbD& p, int B, int layout, const T* w, T* g, T* J, T* gf, T* f, T* fpart,
-                       hipStream_t st, hipEvent_t* ev);
+                       hipStream_t st, hipEvent_t* ev, int tile = 0);
 
 #ifdef ATO_DEFINE_LAUNCHERS
 template <class M, class T>
 hipError_t launch_eval(const ProbD& p, int B, int layout, const T* w, T* g, T* J, T* gf, T* f, T* fpart,
-                       hipStream_t st, hipEvent_t* ev) {
+                       hipStream_t st, hipEvent_t* ev, int tile) {
     const dim3 block(WAVE);
     const int chunks = (B + WAVE - 1) / WAVE;
     const bool wj = J != nullptr, wg = g != nullptr, wf = gf != nullptr;
@@ -467,7 +484,8 @@ hipError_t launch_eval(const ProbD& p, int B, int layout, const T* w, T* g, T* J
     // Collocation and RK4 problems get separate instantiations so neither pays the other's
     // register allocation (the RK4 dual-number step vs the collocation ODE units).
     auto launch = [&]<int UM>() {
-        const dim3 grid(chunks, p.n_units);
+        const bool tiled = tile > 0 && chunks > tile;
+        const dim3 grid = tiled ? dim3(tile, p.n_units, (chunks + tile - 1) / tile) : dim3(chunks, p.n_units);
         if (paired) {
             if (wj && wg && wf)
                 hipExtLaunchKernelGGL((k_eval_paired<M, T, 0, true, true, true, true, UM>), grid, block, 0, st, e0, e1, 0, p, B, 0, w, g, J, gf, fpart);
@@ -511,14 +529,14 @@ hipError_t launch_hess(const ProbD& p, const HessDev& hd, int B, int layout, con
     for (int c = 0; c < hd.n_colors; ++c) {
         if (p.trans == ATO_TRANS_RK4)
             hipLaunchKernelGGL((k_hess_dual<M, UMASK_RK4>), dim3(chunks, p.n_units), dim3(WAVE), 0, st, p, B, layout,
-                               w, hd.color, c, dJ, dgf);
+                               w, hd.color, c, hd.amask + (long)c * hd.mask_words, dJ, dgf);
         else
             hipLaunchKernelGGL((k_hess_dual<M, UMASK_COLLOC>), dim3(chunks, p.n_units), dim3(WAVE), 0, st, p, B,
-                               layout, w, hd.color, c, dJ, dgf);
+                               layout, w, hd.color, c, hd.amask + (long)c * hd.mask_words, dJ, dgf);
         const int t0 = hd.take_off_host[c], nt = hd.take_off_host[c + 1] - t0;
         if (nt > 0)
             hipLaunchKernelGGL(k_hess_take<0>, dim3(chunks, nt), dim3(WAVE), 0, st, B, layout, p.ng, hd.nnzh, t0,
-                               hd.take_e, hd.take_r, hd.csc_ptr, hd.csc_ent, hd.csc_row, lam, sigma,
+                               hd.take_e, hd.take_r, hd.tk_ptr, hd.tk_ent, hd.tk_row, lam, sigma,
                                (const double*)dJ, (const double*)dgf, H);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;

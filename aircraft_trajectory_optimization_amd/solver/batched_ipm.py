@@ -259,6 +259,15 @@ class _Laps:
         self.last = now
 
 
+# speculative inertia-correction passes (BatchedInteriorPoint._speculate): spare factor slots, and
+# the most members of one instance's delta_w sequence tried in one call
+SPEC_SLOTS = 64
+SPEC_MAX_DEPTH = 16
+# from this pass on (passes 0 / 1 branch on the first failure's singularity; most instances that
+# reach pass 2 succeed there, where a speculative call plus its confirmation would cost two calls)
+SPEC_FROM_PASS = 3
+
+
 def _idx(mask: torch.Tensor) -> np.ndarray:
     return torch.nonzero(mask).reshape(-1).cpu().numpy().astype(np.int32)
 
@@ -576,6 +585,75 @@ class BatchedInteriorPoint:
         dr[self.iin] -= 1.0 / Ds
         return Sx + dw, dr, Ds
 
+    def _spec_kkt(self):
+        ''' the spare factorisation of the speculative inertia-correction passes (device KKT only;
+        one per factor storage, so views share their base's and forks get their own) '''
+        if os.environ.get('ATO_KKT_SPECULATE', '1') == '0' or self.vk is None:
+            return None
+        from aircraft_trajectory_optimization_amd.solver.kkt_device import DeviceKKT
+        base = getattr(self.kkt, 'base', self.kkt)
+        if not isinstance(base, DeviceKKT):
+            return None
+        spec = getattr(base, '_spec', None)
+        if spec is None:
+            spec = base._spec = DeviceKKT(base.plan, SPEC_SLOTS, base.device)
+        return spec
+
+    def _speculate(self, W, Js, Sx, Ss, delta_w, delta_c, dwl, pend, pidx):
+        '''
+        IPOPT's inertia-correction retries for the pending instances, several at once. Past the
+        first retry an instance's sequence no longer branches: delta_c is fixed and delta_w grows by
+        kappa_w_plus (kappa_w_plus_bar when the last iteration's delta_w was 0) per failed attempt until
+        it exceeds delta_w_max. The next K members of each sequence (the products formed in the same
+        order as next_pass, so bitwise its values) are factorised side by side in the spare storage;
+        each instance's delta_w moves to its first member with the right inertia -- the pass that
+        follows re-factorises exactly that matrix in the instance's own slot (the factorisation of a
+        column does not depend on the rest of the batch: tests/test_gpu_kkt.py wide-vs-narrow) -- or
+        to the member after the K tried, and instances whose sequence passed delta_w_max without a
+        success drop out as the serial passes would have dropped them. The serial loop needs one
+        factorisation call per attempt; a handful of hard instances used to cost ~7 calls per
+        iteration (bench solver_stats factor_passes 2..38).
+        '''
+        o = self.o
+        spec = self._spec_kkt()
+        P = len(pidx)
+        K = min(SPEC_SLOTS // P, SPEC_MAX_DEPTH)
+        it = torch.as_tensor(pidx, dtype=torch.long, device=self.dev)
+        dw0 = delta_w[it].cpu().numpy()
+        grow = np.where(dwl[it].cpu().numpy() == 0, o.kappa_w_plus_bar, o.kappa_w_plus)
+        cand = np.empty((P, K))
+        cand[:, 0] = dw0
+        for j in range(1, K):
+            cand[:, j] = cand[:, j - 1] * grow
+        valid = cand <= o.delta_w_max           # cand[:, 0] passed next_pass's test already
+        pp, jj = np.nonzero(valid)
+        ns = len(pp)
+        cols = np.full(SPEC_SLOTS, pidx[0], dtype=np.int64)
+        cols[:ns] = pidx[pp]
+        ct = torch.as_tensor(cols, device=self.dev)
+        dws = np.full(SPEC_SLOTS, cand[0, 0])
+        dws[:ns] = cand[pp, jj]
+        dx, dr, _ = self._kkt_diag(Sx[:, ct], Ss[:, ct], torch.as_tensor(dws, device=self.dev), delta_c[ct])
+        inertia = spec.factor(W[:, ct] if W is not None else None, Js[:, ct], dx, dr, np.arange(ns, dtype=np.int32))
+        inr = inertia[:ns].cpu().numpy()
+        self.laps.lap('kkt_factor_retry')
+        self.stats['factorizations'] += 1
+        sp = self.stats.setdefault('speculative', [0, 0])      # [calls, candidate slots]
+        sp[0] += 1
+        sp[1] += ns
+        okv = np.zeros((P, K), dtype=bool)
+        okv[pp, jj] = (inr[:, 0] == self.n) & (inr[:, 1] == self.m) & (inr[:, 2] == 0)
+        hit = okv.any(1)
+        first_ok = okv.argmax(1)
+        new_dw = np.where(hit, cand[np.arange(P), first_ok], cand[:, -1] * grow)
+        dead = ~hit & ((~valid).any(1) | (new_dw > o.delta_w_max))
+        delta_w = delta_w.clone()
+        delta_w[it] = torch.as_tensor(new_dw, device=self.dev)
+        if dead.any():
+            pend = pend.clone()
+            pend[it[torch.as_tensor(dead, device=self.dev)]] = False
+        return delta_w, pend
+
     def _kkt_step(self, W, Js, Sx, Ss, rhs_x, rhs_s, rhs_y, mu, dwl, act, start_dw=None, start_dc=None):
         '''
         Newton step with IPOPT's inertia correction, per instance. Returns
@@ -626,6 +704,11 @@ class BatchedInteriorPoint:
         # as before; only the order between instances changes.
         while True:
             while len(pidx):
+                if npass >= SPEC_FROM_PASS and len(pidx) <= SPEC_SLOTS // 2 and self._spec_kkt() is not None:
+                    delta_w, pend = self._speculate(W, Js, Sx, Ss, delta_w, delta_c, dwl, pend, pidx)
+                    pidx = _idx(pend)
+                    if not len(pidx):
+                        break
                 dx, dr, _ = self._kkt_diag(Sx, Ss, delta_w, delta_c)
                 self.laps.lap('kkt_other')
                 inertia = self.kkt.factor(W, Js, dx, dr, pidx)

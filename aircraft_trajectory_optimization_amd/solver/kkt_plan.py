@@ -29,8 +29,10 @@ diagonal by interval, almost every row touches one interval or two neighbouring 
            inside a leaf, so the collocation defects there determine the later nodes and the
            leaf blocks stay non-singular (interior rows that touch only anchors join the
            separator). Separators are joined by recursive bisection, the
-           border rows (loop closure, equal step sizes: rows spanning non-neighbouring
-           intervals) form the root. The critical path of one factorisation is one leaf plus
+           border rows (loop closure: rows spanning non-neighbouring intervals) form the root;
+           HUB variables (a global gate phase's first step size, tied to every step of the phase
+           by the equal-step rows) are eliminated at the root and left out of the row spans, so
+           those rows stay inside their intervals. The critical path of one factorisation is one leaf plus
            log2(N) separators instead of the whole chain. Variable / row pairs isolated inside an
            interval (the input rates and their defect rows) form a child front of the leaf
            (split_pairs), which shrinks the leaf block. With `saddle` pairs (collocation_saddle:
@@ -197,17 +199,43 @@ def collocation_saddle(N, K1, nv, nz, m, j_row_ptr, j_col):
     return np.asarray(cols, np.int64), np.asarray(rows, np.int64)
 
 
+HUB_MIN_ROWS = 3           # border rows of a hub reach this many distinct intervals (eliminated at the root)
+
+
 def _fronts_nd(n, var_stage, lo, hi, j_row_ptr, j_col, split_pairs=True, saddle=None):
     S = int(var_stage.max()) + 1
     m = len(lo)
+    jr = np.repeat(np.arange(m), np.diff(np.asarray(j_row_ptr)))
+    jc = np.asarray(j_col)
+    # hubs: variables on many rows that span more than two intervals -- the first step size h_n0 of a
+    # global raceline's gate phase, which the equal-step rows h_n2 - h_n0 = 0 tie to every step of the
+    # phase (base_raceline.py:897-905). As border rows those would all sit in the root front (514
+    # positions for race.py's 490 RK4 steps, over the device's 256). Instead a hub is eliminated at the
+    # root like the root anchors below, and the rows' spans are taken without it: h_n2 - h_n0 becomes
+    # an interior row of interval n2, whose leaf hands h_n0 up as one trailing position.
+    # (a hub's border rows reach at least HUB_MIN_ROWS distinct far intervals; a closed line's closure
+    # rows all reach interval 0 and stay with the root anchors)
+    bsel = (hi - lo > 1)[jr]
+    bv, br = jc[bsel], jr[bsel]
+    far = np.where(var_stage[bv] == lo[br], hi[br], lo[br])
+    pairs = np.unique(np.stack([bv, far]), axis=1)
+    hub = np.bincount(pairs[0], minlength=n) >= HUB_MIN_ROWS
+    if hub.any():
+        kept = ~hub[jc]
+        st = var_stage[jc]
+        lo2 = np.full(m, np.iinfo(np.int64).max)
+        hi2 = np.full(m, -1)
+        np.minimum.at(lo2, jr[kept], st[kept])
+        np.maximum.at(hi2, jr[kept], st[kept])
+        some = hi2 >= 0                          # rows with a non-hub entry take the reduced span
+        lo, hi = np.where(some, lo2, lo), np.where(some, hi2, hi)
     link = hi - lo == 1
     interior = hi == lo
     # anchors of boundary j: the variables of interval j touched by its link rows
     anchor = np.zeros(n, bool)
-    jr = np.repeat(np.arange(m), np.diff(np.asarray(j_row_ptr)))
-    jc = np.asarray(j_col)
     sel = link[jr] & (var_stage[jc] == hi[jr])
     anchor[jc[sel]] = True
+    anchor &= ~hub
     # root anchors: the interval-0 variables that border rows touch (a closed line's closure rows
     # tie node 0 to the last node). They are eliminated in the border front, so the closure rows
     # no longer couple to leaf 0 -- its block shrinks from 182 to 166 positions on the racetrack,
@@ -218,6 +246,7 @@ def _fronts_nd(n, var_stage, lo, hi, j_row_ptr, j_col, split_pairs=True, saddle=
     rsel = border_row[jr] & (var_stage[jc] == 0)
     root_anchor[jc[rsel]] = True
     root_anchor &= ~anchor
+    root_anchor |= hub
     # interior rows whose every entry sits on anchors (e.g. a global-frame gate row on Z[n,0][:3],
     # whose position the continuity rows make anchors) have no variable inside the leaf: in the
     # leaf their own column would hold only the row diagonal (a zero pivot for an equality row,

@@ -216,7 +216,7 @@ int atoh_hess_eval(atoh_handle* h, int B, const double* w, const double* lam, co
                 }
                 for (int t = HL.take_off[c]; t < HL.take_off[c + 1]; ++t)
                     H[(long)b * nnzh + HL.take_e[t]] =
-                        ato::hess_take(HL.csc_ptr.data(), HL.csc_ent.data(), HL.csc_row.data(), HL.take_r[t],
+                        ato::hess_take(HL.tk_ptr.data(), HL.tk_ent.data(), HL.tk_row.data(), t, HL.take_r[t],
                                        sigma[b], lam + (long)b * p.ng, 1L, dJ.data(), 1L, dgf.data(), 1L);
             }
         }
@@ -226,6 +226,36 @@ int atoh_hess_eval(atoh_handle* h, int B, const double* w, const double* lam, co
         return -1;
     }
     return 0;
+}
+
+// diagnostic: over every colour's seeded pass at one point w, the Jacobian tangents that the device
+// pass does not store (HessLayout::amask bit clear) must be exact zeros; returns how many are not
+// (and their largest magnitude in *max_abs)
+int atoh_hess_mask_check(atoh_handle* h, const double* w, double* max_abs) {
+    int32_t nnzh, nc;
+    if (atoh_hess_sparsity(h, &nnzh, &nc)) return -1;
+    const ato::ProbD& p = h->L.p;
+    const ato::HessLayout& HL = h->HL;
+    std::vector<double> dJ(p.nnz), dgf(p.nw);
+    int bad = 0;
+    *max_abs = 0.0;
+    ato::with_model(p, [&]<class M>() {
+        for (int c = 0; c < HL.n_colors; ++c) {
+            ato::ColorW<double, HostW<double>> W{HostW<double>{w, 1, p.isph, (long)p.isph_stride}, HL.color.data(), c};
+            HostTangentSink<double> s{dJ.data(), 0};
+            const ato::TangentGrad<double> go{dgf.data(), 1};
+            for (int u = 0; u < p.n_units; ++u) {
+                const int32_t* ut = p.units + 4 * u;
+                ato::run_unit<M, ato::Dual<double, 1>, 0, true, true>(p, ut[0], ut[1], ut[2], W, s, go);
+            }
+            for (int e = 0; e < p.nnz; ++e)
+                if (!(HL.amask[(size_t)c * HL.mask_words + e / 32] >> (e % 32) & 1u) && dJ[e] != 0.0) {
+                    ++bad;
+                    *max_abs = std::max(*max_abs, std::abs(dJ[e]));
+                }
+        }
+    });
+    return bad;
 }
 
 }  // extern "C"

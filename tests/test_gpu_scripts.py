@@ -1,0 +1,104 @@
+'''
+Script-level solves on the device (SURVEY 8(a) rows A3/A17 as the reference's scripts run them):
+
+  * scripts/race.py:29-49 -- solve_util(use_rk4=True, N=70, use_ws=True, use_quaternion=True) in the
+    global and the parametric frame: _setup_checks turns N = 70 with the default K = 7 into 490 RK4
+    steps (base_raceline.py:226-230); the drone solve starts from the point-mass raceline;
+  * scripts/obstacles.py:27-40 -- ParametricObstacleDroneRaceline with N = 100 (K = 7 collocation),
+    r_c = 0.4, no gates, the tube from the mesh, warm-started from the point-mass obstacle raceline.
+
+Each goes through the reference's API (solve() runs the batched device solver at B = 1) and must
+(1) report a feasible raceline, (2) reach the local optimum that the host-KKT single-instance solver
+reaches from the same guess (lap times measured on CPU with the CPU build of the same programs,
+tests/script_solves_host.py; tolerance 1e-5 s: the two factorisations round differently, so the
+iterates part ways after a few hundred iterations but settle on the same KKT point), and (3) be a
+KKT point of the oracle's NLP (tests/helpers.kkt_certificate; IPOPT's scaled stopping test in
+unscaled units, as in test_config3_full_size_cold_start_batch).
+'''
+import time
+
+import numpy as np
+import pytest
+
+from tests.helpers import kkt_certificate, oracle_line
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip('torch')
+
+# host-KKT solver (solver/ipm.py over the CPU build of the programs), tests/script_solves_host.py
+HOST_LAP = {'race_rk4_parametric': 5.813425461388203,
+            'race_rk4_global': 5.647455768513202,
+            'obstacles_N100': 7.434782275545377}
+
+
+def _certify(solver, nlp, tol_primal=5e-4):
+    res = solver.result
+    x = res.x[:, 0].cpu().numpy()
+    c = kkt_certificate(nlp, x, res.lam_g[:, 0].cpu().numpy(), res.lam_x[:, 0].cpu().numpy(),
+                        solver.spec.lbw, solver.spec.ubw)
+    assert c['primal'] <= tol_primal and c['dual'] <= 1e-5 and c['compl'] <= 1e-6, c
+    return c
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize('frame', ['parametric', 'global'])
+def test_race_script_rk4_drone_solve(frame):
+    from aircraft_trajectory_optimization_amd.tracks import make_line
+    from aircraft_trajectory_optimization_amd.utils.solve_util import solve_util
+    from oracle.ref_transcription import RefNLP
+    line = make_line('race')
+    t0 = time.time()
+    solver, res = solve_util(line=line, global_frame=frame == 'global', drone=True, use_ws=True,
+                             use_quaternion=True, use_rk4=True, N=70, verbose=False)
+    wall = time.time() - t0
+    sp = solver.spec
+    assert sp.rk4 and sp.N == 490, (sp.rk4, sp.N)
+    print(f'race.py {frame} RK4: point-mass {solver.ws_raceline.time:.6f} s lap ({solver.ws_raceline.solve_time:.2f} s), '
+          f'drone {res.time:.9f} s lap, solve {res.solve_time:.2f} s (feval {res.feval_time:.2f} s), '
+          f'wall {wall:.1f} s, status {solver.result.status[0]}, iterations {int(solver.result.iters[0])}')
+    assert res.feasible and solver.ws_raceline.feasible
+    ref = HOST_LAP[f'race_rk4_{frame}']
+    if ref is not None:
+        assert abs(res.time - ref) <= 1e-5, (res.time, ref)
+    nlp = RefNLP(oracle_line('race', True), 'drone', frame, 70, 7,
+                 veh={'use_quat': True, 'global_r': True, 'use_dcm': False},
+                 fixed_gates=(line.config.s[:-1] if frame == 'parametric' else None),
+                 quat_flip=sp.quat_flip, euler_wraps=sp.euler_wraps, rk4=True, closed=True)
+    assert (nlp.nw, nlp.ng) == (sp.nw, len(solver.evaluator.lbg))
+    _certify(solver, nlp)
+
+
+@pytest.mark.timeout(900)
+def test_obstacles_script_drone_solve():
+    from aircraft_trajectory_optimization_amd.obstacles.mesh_obstacle import MeshObstacle
+    from aircraft_trajectory_optimization_amd.pytypes import DroneConfig
+    from aircraft_trajectory_optimization_amd.raceline.config import ParametricRacelineConfig
+    from aircraft_trajectory_optimization_amd.raceline.solvers import ParametricObstacleDroneRaceline
+    from aircraft_trajectory_optimization_amd.tracks import make_line
+    from oracle.ref_transcription import RefNLP
+    line = make_line('obstacles')
+    line.config.gate_s = None                          # obstacles.py:21-24
+    config = ParametricRacelineConfig(verbose=False, N=100)
+    config.closed = True
+    mesh = MeshObstacle()
+    t0 = time.time()
+    solver = ParametricObstacleDroneRaceline(line, config, DroneConfig(global_r=True, use_quat=True,
+                                                                       collision_radius=0.4), mesh, generate_ws=True)
+    res = solver.solve()
+    wall = time.time() - t0
+    sp = solver.spec
+    assert (sp.N, sp.K) == (100, 7)
+    d = np.array([st.d for st in res.states])
+    print(f'obstacles.py N=100 K=7: point-mass {solver.ws_raceline.time:.6f} s lap, drone {res.time:.9f} s lap, '
+          f'solve {res.solve_time:.2f} s (feval {res.feval_time:.2f} s), wall {wall:.1f} s, '
+          f'status {solver.result.status[0]}, iterations {int(solver.result.iters[0])}, '
+          f'min obstacle distance {d.min():.4f} m')
+    assert res.feasible and solver.ws_raceline.feasible
+    ref = HOST_LAP['obstacles_N100']
+    if ref is not None:
+        assert abs(res.time - ref) <= 1e-5, (res.time, ref)
+    nlp = RefNLP(oracle_line('obstacles', True), 'drone', 'parametric', 100, 7,
+                 veh={'use_quat': True, 'global_r': True, 'collision_radius': 0.4}, fixed_gates=[],
+                 spheres=solver.sphere_table, quat_flip=sp.quat_flip, euler_wraps=sp.euler_wraps)
+    assert (nlp.nw, nlp.ng) == (sp.nw, len(solver.evaluator.lbg))
+    _certify(solver, nlp)

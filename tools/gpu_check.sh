@@ -117,6 +117,21 @@ for s in $STEPS; do
                done ;;
         listpmc) run listpmc 120 rocprofv3 -L ;;
         mb)    run mb_store 120 ./tools/mb_store ;;
+        tileab) for t in 0 8 16 4; do
+                    ATO_EVAL_TILE=$t run eval_tile${t}_b4096 300 python bench.py --steps 20 --warmup 5 --batch 4096 --no-cpu-baseline --no-solve --eval-steps 30
+                done
+                ATO_EVAL_TILE=8 ATO_EVAL_TILE_LF=0 run eval_tile8im_b4096 300 python bench.py --steps 20 --warmup 5 --batch 4096 --no-cpu-baseline --no-solve --eval-steps 30
+                for t in 0 8; do
+                    ATO_EVAL_TILE=$t run eval_tile${t}_f32_b8192 300 python bench.py --track fig8 --pose dcm --dtype f32 --batch 8192 --no-solve --no-cpu-baseline --eval-steps 50
+                done ;;
+        specab) for v in 0 1; do
+                    ATO_KKT_SPECULATE=$v run solve_spec$v 600 python tools/solve_batched.py --batch 512 --max-iter 200 --cold --no-host --out "$OUT/solve_spec$v.json"
+                done ;;
+        specfull) for v in 0 1; do
+                    ATO_KKT_SPECULATE=$v run solvefull_spec$v 600 python tools/solve_batched.py --batch 512 --max-iter 1000 --cold --no-host --out "$OUT/solvefull_spec$v.json"
+                done ;;
+        spectests) run pytest_spec 300 python -u -m pytest tests/test_gpu_batched_ipm.py -x -v -s --timeout 200 --timeout-method thread -p no:cacheprovider -k "speculative or deterministic or restoration" ;;
+        scripts) run pytest_scripts 900 python -u -m pytest tests/test_gpu_scripts.py -x -v -s --timeout 800 --timeout-method thread -p no:cacheprovider ;;
         mbscale) run mb_store_scale 120 ./tools/mb_store_scale
                run bench_b4096 300 python bench.py --steps 20 --warmup 5 --batch 4096 --no-cpu-baseline --no-solve --eval-steps 30 ;;
         mbpmc) run mb_fetch 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/mb_fetch" -o run -- ./tools/mb_store
