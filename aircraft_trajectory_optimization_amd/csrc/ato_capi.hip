@@ -47,7 +47,9 @@ static void release(ato_handle* h) {
     (void)hipFree(h->d_units);
     (void)hipFree(h->d_units_lf);
     (void)hipFree(h->d_fpart);
-    for (int32_t* d : {h->d_color, h->d_take_e, h->d_take_r, h->d_tk_ptr, h->d_tk_ent, h->d_tk_row}) (void)hipFree(d);
+    for (int32_t* d : {h->d_color, h->d_take_e, h->d_take_r, h->d_tk_ptr, h->d_tk_ent, h->d_tk_row, h->d_tkf_ptr,
+                       h->d_tkf_ent, h->d_tkf_row})
+        (void)hipFree(d);
     (void)hipFree(h->d_amask);
     (void)hipFree(h->d_dJ);
     (void)hipFree(h->d_dgf);
@@ -122,6 +124,7 @@ int ato_create(const ato_problem_desc* desc, ato_handle** out) {
     if (const char* e = std::getenv("ATO_LONGFIRST_MAX_B")) h->lf_max_batch = std::atoi(e);
     if (const char* e = std::getenv("ATO_EVAL_TILE")) h->eval_tile = std::atoi(e);
     if (const char* e = std::getenv("ATO_EVAL_TILE_LF")) h->tile_lf = std::atoi(e) != 0;
+    if (const char* e = std::getenv("ATO_HESS_MASK")) h->hess_mask = std::atoi(e) != 0;
     *out = h;
     return ATO_OK;
 }
@@ -286,7 +289,8 @@ static int ensure_hess(ato_handle* h) {
     if ((rc = upload(h->HL.color, &h->d_color)) || (rc = upload(h->HL.take_e, &h->d_take_e)) ||
         (rc = upload(h->HL.take_r, &h->d_take_r)) || (rc = upload(h->HL.tk_ptr, &h->d_tk_ptr)) ||
         (rc = upload(h->HL.tk_ent, &h->d_tk_ent)) || (rc = upload(h->HL.tk_row, &h->d_tk_row)) ||
-        (rc = upload(h->HL.amask, &h->d_amask)))
+        (rc = upload(h->HL.tkf_ptr, &h->d_tkf_ptr)) || (rc = upload(h->HL.tkf_ent, &h->d_tkf_ent)) ||
+        (rc = upload(h->HL.tkf_row, &h->d_tkf_row)) || (rc = upload(h->HL.amask, &h->d_amask)))
         return rc;
     h->hess_ready = true;
     return ATO_OK;
@@ -314,8 +318,10 @@ extern "C" int ato_hess_eval(ato_handle* h, int32_t batch, int32_t layout, const
     int rc = ensure_hess(h);
     if (rc) return rc;
     if ((rc = hess_reserve(h, batch))) return rc;
-    const ato::HessDev hd{h->d_color, h->d_take_e, h->d_take_r, h->d_tk_ptr, h->d_tk_ent, h->d_tk_row,
-                          h->d_amask, h->HL.mask_words,
+    const bool mk = h->hess_mask;
+    const ato::HessDev hd{h->d_color, h->d_take_e, h->d_take_r, mk ? h->d_tk_ptr : h->d_tkf_ptr,
+                          mk ? h->d_tk_ent : h->d_tkf_ent, mk ? h->d_tk_row : h->d_tkf_row,
+                          mk ? h->d_amask : nullptr, h->HL.mask_words,
                           h->HL.take_off.data(), h->HL.n_colors, h->HL.nnz()};
     hipError_t e = hipSuccess;
     const ato::ProbD& p = batch <= h->lf_max_batch ? h->pd_lf : h->pd;   // unit order as in ato_eval

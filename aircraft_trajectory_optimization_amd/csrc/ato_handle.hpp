@@ -36,7 +36,9 @@ struct ato_handle {
     ato::HessLayout HL;
     int32_t *d_color = nullptr, *d_take_e = nullptr, *d_take_r = nullptr;
     int32_t *d_tk_ptr = nullptr, *d_tk_ent = nullptr, *d_tk_row = nullptr;
+    int32_t *d_tkf_ptr = nullptr, *d_tkf_ent = nullptr, *d_tkf_row = nullptr;
     uint32_t* d_amask = nullptr;
+    bool hess_mask = false;           // ATO_HESS_MASK=1: the masked colour passes (HessLayout::amask)
     double* d_dJ = nullptr;     // [nnz][hess_reserved] Jacobian tangents of one colour
     double* d_dgf = nullptr;    // [nw][hess_reserved] grad f tangents of one colour
     int32_t hess_reserved = 0;

@@ -127,6 +127,8 @@ struct HessLayout {
     std::vector<uint32_t> amask;
     int mask_words = 0;
     std::vector<int32_t> tk_ptr, tk_ent, tk_row;
+    // the same take lists over the whole column (the default device pass, which stores every tangent)
+    std::vector<int32_t> tkf_ptr, tkf_ent, tkf_row;
     int nnz() const { return (int)col.size(); }
 
     // structure analysis + colouring (host only; defined in ato_hstruct.cpp, compiled by the host
@@ -273,17 +275,23 @@ std::string HessLayout::build(const Layout& L) {
     tk_ptr.assign(take_r.size() + 1, 0);
     tk_ent.clear();
     tk_row.clear();
+    tkf_ptr.assign(take_r.size() + 1, 0);
+    tkf_ent.clear();
+    tkf_row.clear();
     for (int c = 0; c < n_colors; ++c)
         for (int t = take_off[c]; t < take_off[c + 1]; ++t) {
             const int r = take_r[t];
             for (int q = csc_ptr[r]; q < csc_ptr[r + 1]; ++q) {
                 const int e = csc_ent[q];
+                tkf_ent.push_back(e);
+                tkf_row.push_back(csc_row[q]);
                 if (amask[(size_t)c * mask_words + e / 32] >> (e % 32) & 1u) {
                     tk_ent.push_back(e);
                     tk_row.push_back(csc_row[q]);
                 }
             }
             tk_ptr[t + 1] = (int32_t)tk_ent.size();
+            tkf_ptr[t + 1] = (int32_t)tkf_ent.size();
         }
     return "";
 }

@@ -253,7 +253,7 @@ template <class M, class T, int KS, bool WJ, bool WG, bool WF, int UMASK>
 __global__ __launch_bounds__(WAVE) void k_eval(ProbD p, int B, int layout, const T* __restrict__ w,
                                                T* __restrict__ g, T* __restrict__ J,
                                                T* __restrict__ gf, T* __restrict__ fpart) {
-    const int b = (blockIdx.z * gridDim.x + blockIdx.x) * WAVE + threadIdx.x;   // z: instance tile (launch_eval)
+    const int b = blockIdx.x * WAVE + threadIdx.x;
     if (b >= B) return;
     const int32_t* ut = p.units + 4 * blockIdx.y;      // wave-uniform: scalar loads
     long st;
@@ -315,14 +315,16 @@ __device__ __forceinline__ void eval_unit(const ProbD& p, const int32_t* ut, con
 #else
 #define ATO_EVAL_ATTR
 #endif
-template <class M, class T, int KS, bool WJ, bool WG, bool WF, bool FULL, int UMASK>
+// TILED: grid (tile, units, tiles) of launch_eval's instance tiles (a separate instantiation, so that
+// the untiled kernel's code -- and its floating-point contraction -- is not touched by the tiling)
+template <class M, class T, int KS, bool WJ, bool WG, bool WF, bool FULL, int UMASK, bool TILED = false>
 __global__ __launch_bounds__(WAVE) ATO_EVAL_ATTR void k_eval_paired(ProbD p, int B, int unit0, const T* __restrict__ w,
                                                       T* __restrict__ g, T* __restrict__ J,
                                                       T* __restrict__ gf, T* __restrict__ fpart) {
     constexpr bool QUAD = FULL && ATO_EVAL_F32_QUAD && std::is_same_v<T, float>;
     const int l = threadIdx.x;
-    const int chunk = (blockIdx.z * gridDim.x + blockIdx.x) * WAVE;   // z: instance tile (launch_eval)
-    if (chunk >= B) return;                                            // past the end of the last tile
+    const int chunk = TILED ? (blockIdx.z * gridDim.x + blockIdx.x) * WAVE : blockIdx.x * WAVE;
+    if (TILED && chunk >= B) return;                                   // past the end of the last tile
     // instance of this lane inside the chunk
     const int own = QUAD ? 4 * (l & 15) + (l >> 4) : 2 * (l & 31) + (l >> 5);
     const int b = chunk + own;
@@ -373,10 +375,28 @@ __global__ __launch_bounds__(256) void k_cost_reduce(int N, int B, const T* __re
 
 // ------------------------------------------------------------------ Hessian of the Lagrangian
 // Tangents of the Jacobian entries of a seeded pass (see ato_hessian.hpp); g rows are ignored.
-// Only the entries that the colour changes are stored (HessLayout::amask, this colour's row): the
-// take lists read no others, and the rest of the tangents are exact zeros.
 template <class T>
 struct DevTangentSink {
+    T* J;
+    long je, e;
+    __device__ __forceinline__ void begin(int, int nnz0) { e = (long)nnz0 * je; }
+    __device__ __forceinline__ void jac(int, const Dual<T, 1>& v) {
+        J[e] = v.d[0];
+        e += je;
+    }
+    __device__ __forceinline__ void row(const Dual<T, 1>&, double, double) {}
+    __device__ __forceinline__ void skip() { e += je; }
+    __device__ __forceinline__ void row_skip() {}
+    __device__ __forceinline__ void finish() {}
+};
+
+// Masked pass (ATO_HESS_MASK=1): only the entries that the colour changes are stored
+// (HessLayout::amask, this colour's row); the masked take lists read no others, and the rest of the
+// tangents are exact zeros. Same H, 22 % less time at B = 512 -- but the conditional store changes
+// how the compiler contracts the tangent arithmetic into FMAs, so H rounds differently from the
+// default pass (Hessian).
+template <class T>
+struct DevTangentSinkMasked {
     T* J;
     long je, e;
     const uint32_t* mask;
@@ -401,7 +421,7 @@ struct DevTangentSink {
 
 // one seeded pass for colour c: dJ = d J / d eps, dgf = d grad f / d eps along v_c
 // (outputs interleaved [entry][B]; w in either layout)
-template <class M, int UMASK>
+template <class M, int UMASK, bool MASKED = false>
 __global__ __launch_bounds__(WAVE) void k_hess_dual(ProbD p, int B, int layout, const double* __restrict__ w,
                                                    const int32_t* __restrict__ color, int c,
                                                    const uint32_t* __restrict__ amask,
@@ -413,9 +433,14 @@ __global__ __launch_bounds__(WAVE) void k_hess_dual(ProbD p, int B, int layout, 
     const ColorW<double, DevW<double>> W{DevW<double>{il ? w + b : w + (long)b * p.nw, il ? (long)B : 1L,
                                                       p.isph ? p.isph + b : nullptr, (long)p.isph_stride},
                                          color, c};
-    DevTangentSink<double> s{dJ + b, (long)B, 0, amask, 0};
     const TangentGrad<double> go{dgf + b, (long)B};
-    run_unit<M, Dual<double, 1>, 0, true, true, UMASK>(p, ut[0], ut[1], ut[2], W, s, go);
+    if constexpr (MASKED) {
+        DevTangentSinkMasked<double> s{dJ + b, (long)B, 0, amask, 0};
+        run_unit<M, Dual<double, 1>, 0, true, true, UMASK>(p, ut[0], ut[1], ut[2], W, s, go);
+    } else {
+        DevTangentSink<double> s{dJ + b, (long)B, 0};
+        run_unit<M, Dual<double, 1>, 0, true, true, UMASK>(p, ut[0], ut[1], ut[2], W, s, go);
+    }
 }
 
 // Hessian entries recovered from colour c: one wave = one take for 64 instances
@@ -444,8 +469,8 @@ __global__ __launch_bounds__(WAVE) void k_hess_take(int B, int layout, int ng, i
 
 // device copies of the HessLayout tables
 struct HessDev {
-    const int32_t *color, *take_e, *take_r, *tk_ptr, *tk_ent, *tk_row;
-    const uint32_t* amask;          // [n_colors][mask_words]
+    const int32_t *color, *take_e, *take_r, *tk_ptr, *tk_ent, *tk_row;   // take lists (masked or full)
+    const uint32_t* amask;          // [n_colors][mask_words]; NULL: the full (default) pass
     int mask_words;
     const int32_t* take_off_host;   // host array [n_colors + 1]
     int n_colors, nnzh;
@@ -484,9 +509,16 @@ hipError_t launch_eval(const ProbD& p, int B, int layout, const T* w, T* g, T* J
     // Collocation and RK4 problems get separate instantiations so neither pays the other's
     // register allocation (the RK4 dual-number step vs the collocation ODE units).
     auto launch = [&]<int UM>() {
-        const bool tiled = tile > 0 && chunks > tile;
-        const dim3 grid = tiled ? dim3(tile, p.n_units, (chunks + tile - 1) / tile) : dim3(chunks, p.n_units);
+        const dim3 grid(chunks, p.n_units);
         if (paired) {
+            if (tile > 0 && chunks > tile && wj && wg) {     // instance tiles (the J-producing passes)
+                const dim3 tgrid(tile, p.n_units, (chunks + tile - 1) / tile);
+                if (wf)
+                    hipExtLaunchKernelGGL((k_eval_paired<M, T, 0, true, true, true, true, UM, true>), tgrid, block, 0, st, e0, e1, 0, p, B, 0, w, g, J, gf, fpart);
+                else
+                    hipExtLaunchKernelGGL((k_eval_paired<M, T, 0, true, true, false, true, UM, true>), tgrid, block, 0, st, e0, e1, 0, p, B, 0, w, g, J, gf, fpart);
+                return;
+            }
             if (wj && wg && wf)
                 hipExtLaunchKernelGGL((k_eval_paired<M, T, 0, true, true, true, true, UM>), grid, block, 0, st, e0, e1, 0, p, B, 0, w, g, J, gf, fpart);
             else if (wj && wg)
@@ -527,12 +559,17 @@ hipError_t launch_hess(const ProbD& p, const HessDev& hd, int B, int layout, con
                        const double* sigma, double* H, double* dJ, double* dgf, hipStream_t st) {
     const int chunks = (B + WAVE - 1) / WAVE;
     for (int c = 0; c < hd.n_colors; ++c) {
-        if (p.trans == ATO_TRANS_RK4)
-            hipLaunchKernelGGL((k_hess_dual<M, UMASK_RK4>), dim3(chunks, p.n_units), dim3(WAVE), 0, st, p, B, layout,
-                               w, hd.color, c, hd.amask + (long)c * hd.mask_words, dJ, dgf);
-        else
-            hipLaunchKernelGGL((k_hess_dual<M, UMASK_COLLOC>), dim3(chunks, p.n_units), dim3(WAVE), 0, st, p, B,
-                               layout, w, hd.color, c, hd.amask + (long)c * hd.mask_words, dJ, dgf);
+        {
+            const uint32_t* am = hd.amask ? hd.amask + (long)c * hd.mask_words : nullptr;
+            const dim3 grid(chunks, p.n_units);
+            if (p.trans == ATO_TRANS_RK4) {
+                if (am) hipLaunchKernelGGL((k_hess_dual<M, UMASK_RK4, true>), grid, dim3(WAVE), 0, st, p, B, layout, w, hd.color, c, am, dJ, dgf);
+                else hipLaunchKernelGGL((k_hess_dual<M, UMASK_RK4>), grid, dim3(WAVE), 0, st, p, B, layout, w, hd.color, c, am, dJ, dgf);
+            } else {
+                if (am) hipLaunchKernelGGL((k_hess_dual<M, UMASK_COLLOC, true>), grid, dim3(WAVE), 0, st, p, B, layout, w, hd.color, c, am, dJ, dgf);
+                else hipLaunchKernelGGL((k_hess_dual<M, UMASK_COLLOC>), grid, dim3(WAVE), 0, st, p, B, layout, w, hd.color, c, am, dJ, dgf);
+            }
+        }
         const int t0 = hd.take_off_host[c], nt = hd.take_off_host[c + 1] - t0;
         if (nt > 0)
             hipLaunchKernelGGL(k_hess_take<0>, dim3(chunks, nt), dim3(WAVE), 0, st, B, layout, p.ng, hd.nnzh, t0,

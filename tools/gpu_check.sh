@@ -130,6 +130,18 @@ for s in $STEPS; do
         specfull) for v in 0 1; do
                     ATO_KKT_SPECULATE=$v run solvefull_spec$v 600 python tools/solve_batched.py --batch 512 --max-iter 1000 --cold --no-host --out "$OUT/solvefull_spec$v.json"
                 done ;;
+        c3ab)  for v in base cur; do
+                   if [ $v = base ]; then lp=$PWD/tools/diag/_lib/libato_base.so; else lp=; fi
+                   ATO_LIB_PATH=$lp ATO_KKT_SPECULATE=0 run pytest_c3_$v 300 python -u -m pytest tests/test_gpu_batched_ipm.py -x -v -s --timeout 200 --timeout-method thread -p no:cacheprovider -k config3_full
+               done ;;
+        hessab) ATO_LIB_PATH=$PWD/tools/diag/_lib/libato_base.so run hess_base 200 python tools/diag/hess_ab.py "$OUT/hess_base.npz"
+                run hess_cur 200 python tools/diag/hess_ab.py "$OUT/hess_cur.npz"
+                ATO_HESS_MASK=1 run hess_mask 200 python tools/diag/hess_ab.py "$OUT/hess_mask.npz" ;;
+        c3b128) run solve_c3_b128 300 python tools/solve_batched.py --batch 128 --max-iter 1000 --cold --no-host --out "$OUT/solve_c3_b128.json" ;;
+        nanab) for v in base cur; do
+                   if [ $v = base ]; then lp=$PWD/tools/diag/_lib/libato_base.so; else lp=; fi
+                   ATO_LIB_PATH=$lp ATO_DEBUG_HESS_NONFINITE=1 run solve_nan_$v 300 python tools/solve_batched.py --batch 64 --max-iter 1000 --cold --no-host --out "$OUT/solve_nan_$v.json"
+               done ;;
         spectests) run pytest_spec 300 python -u -m pytest tests/test_gpu_batched_ipm.py -x -v -s --timeout 200 --timeout-method thread -p no:cacheprovider -k "speculative or deterministic or restoration" ;;
         scripts) run pytest_scripts 900 python -u -m pytest tests/test_gpu_scripts.py -x -v -s --timeout 800 --timeout-method thread -p no:cacheprovider ;;
         mbscale) run mb_store_scale 120 ./tools/mb_store_scale

@@ -54,6 +54,7 @@ def run(B, max_iter, N=50, K=4, track='race', host_ref=True, cold=False):
            'instance_iterations': int(res.iters.sum()), 'lockstep_iterations': int(len(solver.history)),
            'iterations_per_s': float(res.iters.sum() / t_solve),
            'converged': int(ok.sum()), 'statuses': {s: res.status.count(s) for s in set(res.status)},
+           'status_list': list(res.status), 'iters_list': [int(i) for i in res.iters],
            'lap_time_instance0_s': float(laps[0]),
            'lap_time_converged': {'min': float(laps[ok].min()) if ok.any() else None,
                                   'median': float(np.median(laps[ok])) if ok.any() else None,
