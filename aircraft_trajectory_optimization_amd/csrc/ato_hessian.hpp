@@ -88,11 +88,16 @@ struct DepSink {
     std::vector<int32_t>* ent_col = nullptr;
     int cur = 0;
     void begin(int, int nnz0) { cur = nnz0; }
+    int overrun = 0;                           // entries past the Jacobian pattern (a program bug)
     void jac(int col, const Dep& v) {
         for (int32_t k : v.s) pairs->push_back({col, k});
         if (ent_dep) {
-            (*ent_dep)[cur] = v.s;
-            (*ent_col)[cur] = col;
+            if (cur >= 0 && cur < (int)ent_dep->size()) {
+                (*ent_dep)[cur] = v.s;
+                (*ent_col)[cur] = col;
+            } else {
+                ++overrun;
+            }
         }
         ++cur;
     }
@@ -160,6 +165,7 @@ std::string HessLayout::build(const Layout& L) {
     const int nnzJ = (int)L.col.size();
     std::vector<std::vector<int32_t>> ent_dep(nnzJ);
     std::vector<int32_t> ent_col(nnzJ, -1);
+    int overrun = 0;
     const bool ok = with_model(p, [&]<class M>() {
         DepSink s{&pairs, &ent_dep, &ent_col};
         DepGrad go{&pairs};
@@ -167,6 +173,7 @@ std::string HessLayout::build(const Layout& L) {
             const int32_t* ut = p.units + 4 * u;
             run_unit<M, Dep, 0, true, true, UMASK_ALL>(p, ut[0], ut[1], ut[2], DepW{}, s, go);
         }
+        overrun = s.overrun;
     });
     if (!ok) return "hessian: unsupported model";
     // symmetric lower-triangular structure
@@ -250,6 +257,7 @@ std::string HessLayout::build(const Layout& L) {
     std::string err = verify(adj, is_hub);
     if (!err.empty()) return err;
     // CSC of J
+    if (overrun) return "hessian: a seeded pass writes " + std::to_string(overrun) + " entries past the Jacobian";
     for (int e = 0; e < nnzJ; ++e)
         if (ent_col[e] != L.col[e]) return "hessian: seeded-pass entry order differs from the Jacobian pattern";
     csc_ptr.assign(nw + 1, 0);
