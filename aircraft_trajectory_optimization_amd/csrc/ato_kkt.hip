@@ -111,7 +111,8 @@ constexpr int CH = ATO_KKT_CH;            // doubles per ring chunk of the solve
 constexpr int CPT = CH / ST;              // chunk doubles per thread
 // a factor column (two for a 2x2 pivot: 2 x 32 T doubles) must fit in the two resident chunks
 static_assert(CH >= 2 * 32 * 8, "solve ring chunk smaller than the largest column pair");
-constexpr int MAXT = 8;                   // strips per front in ent_ptr
+constexpr int MAX_FRONT_TILES = 9;        // fronts up to 288 positions
+constexpr int MAXT = MAX_FRONT_TILES;     // strips per front in ent_ptr
 constexpr double BK_ALPHA = 0.64038820320220756872767623199676;   // (1 + sqrt(17)) / 8
 constexpr int SRC_SHIFT = 29;
 constexpr int SAD_DONE = -1;              // sinfo.x of a saddle front factorised by k_front_saddle
@@ -1341,24 +1342,33 @@ __device__ void saddle_bwd(const Plan& P, int f, int b, const double* Lb, double
 // ------------------------------------------------------------------------------------------
 // Stream of the front's factor columns through a two-slot LDS ring. Forward: chunks 0, 1, 2,
 // ... of [0, total); backward: the same chunks in reverse. Chunk c lives in slot c & 1.
+// C: doubles per chunk (a power of two holding the front's largest column pair: CH up to eight tiles,
+// 2 CH for nine, ring_chunk<T>)
+template <int T>
+constexpr int ring_chunk() { return T > 8 ? 2 * CH : CH; }
+static_assert(2 * CH >= 2 * 32 * MAX_FRONT_TILES, "solve ring chunk smaller than the largest column pair");
+
+template <int C>
 struct Ring {
-    double* buf;           // [2][CH]
-    __device__ __forceinline__ double at(long long off) const { return buf[off & (2 * CH - 1)]; }
+    double* buf;           // [2][C]
+    __device__ __forceinline__ double at(long long off) const { return buf[off & (2 * C - 1)]; }
 };
 
+template <int C>
 __device__ __forceinline__ void ring_load(const double* __restrict__ src, long long total, long long c,
-                                          double (&r)[CPT], int tid) {
+                                          double (&r)[C / ST], int tid) {
 #pragma unroll
-    for (int q = 0; q < CPT; ++q) {
-        const long long o = c * CH + q * ST + tid;
+    for (int q = 0; q < C / ST; ++q) {
+        const long long o = c * C + q * ST + tid;
         r[q] = (c >= 0 && o < total) ? src[o] : 0.0;
     }
 }
 
-__device__ __forceinline__ void ring_store(double* buf, long long c, const double (&r)[CPT], int tid) {
-    double* dst = buf + (c & 1) * CH;
+template <int C>
+__device__ __forceinline__ void ring_store(double* buf, long long c, const double (&r)[C / ST], int tid) {
+    double* dst = buf + (c & 1) * C;
 #pragma unroll
-    for (int q = 0; q < CPT; ++q) dst[q * ST + tid] = r[q];
+    for (int q = 0; q < C / ST; ++q) dst[q * ST + tid] = r[q];
 }
 
 template <int NQ>
@@ -1424,7 +1434,8 @@ __global__ __launch_bounds__(ST) void k_front_fwd(Plan P, int f0, int batch, con
                                                   long long sb) {
     constexpr int NP = 32 * T;
     constexpr int NQ = (NP + 63) / 64;
-    __shared__ double ring_buf[2 * CH];
+    constexpr int CHT = ring_chunk<T>();
+    __shared__ double ring_buf[2 * CHT];
     __shared__ double cvec[NP];
     __shared__ int2 s_piv[NP];
     __shared__ double s_dinv[3 * NP];
@@ -1441,16 +1452,16 @@ __global__ __launch_bounds__(ST) void k_front_fwd(Plan P, int f0, int batch, con
     }
     const int lane = tid & 63;
     const bool w0 = tid < 64;
-    Ring ring{ring_buf};
-    double stage_r[CPT];
+    Ring<CHT> ring{ring_buf};
+    double stage_r[CHT / ST];
 
     // ---- right-hand side: own entries of b, zero trailing, plus the children's contributions
     for (int i = tid; i < NP; i += ST) cvec[i] = i < F.own ? F.xb[(long long)P.pos_index[F.p0 + i] * se] : 0.0;
     stage_records(F.pv, F.dvp, F.steps, tid, s_piv, s_dinv);
-    ring_load(F.Lb, F.total, 0, stage_r, tid);
-    ring_store(ring.buf, 0, stage_r, tid);
-    ring_load(F.Lb, F.total, 1, stage_r, tid);
-    ring_store(ring.buf, 1, stage_r, tid);
+    ring_load<CHT>(F.Lb, F.total, 0, stage_r, tid);
+    ring_store<CHT>(ring.buf, 0, stage_r, tid);
+    ring_load<CHT>(F.Lb, F.total, 1, stage_r, tid);
+    ring_store<CHT>(ring.buf, 1, stage_r, tid);
     __syncthreads();
     for (int ci = P.child_ptr[F.f]; ci < P.child_ptr[F.f + 1]; ++ci) {
         const int c = P.child_list[ci];
@@ -1477,12 +1488,12 @@ __global__ __launch_bounds__(ST) void k_front_fwd(Plan P, int f0, int batch, con
     int nlive = F.A, t = 0;
     long long off = 0;
     int2 rec_nx = F.steps > 0 ? s_piv[0] : make_int2(0, -1);   // record of step t, read one step ahead
-    const long long nchunks = (F.total + CH - 1) / CH;
+    const long long nchunks = (F.total + CHT - 1) / CHT;
     if (tid == 0) s_done = 0;
     for (long long c = 0;; ++c) {
-        ring_load(F.Lb, F.total, c + 2, stage_r, tid);     // in flight while wave 0 sweeps
+        ring_load<CHT>(F.Lb, F.total, c + 2, stage_r, tid);     // in flight while wave 0 sweeps
         if (w0) {
-            const long long limit = (c + 2) * CH;
+            const long long limit = (c + 2) * CHT;
             while (t < F.steps) {
                 const int2 rec = rec_nx;
                 const int type = __builtin_amdgcn_readfirstlane(rec.x >> 16);
@@ -1521,7 +1532,7 @@ __global__ __launch_bounds__(ST) void k_front_fwd(Plan P, int f0, int batch, con
         }
         __syncthreads();
         if (s_done != 0) break;
-        ring_store(ring.buf, c + 2, stage_r, tid);
+        ring_store<CHT>(ring.buf, c + 2, stage_r, tid);
         __syncthreads();
         if (c + 2 > nchunks + 2) break;               // safety: never loop past the stream
     }
@@ -1557,7 +1568,8 @@ __global__ __launch_bounds__(ST) void k_front_bwd(Plan P, int f0, int batch, con
                                                   double* __restrict__ x, long long se, long long sb) {
     constexpr int NP = 32 * T;
     constexpr int NQ = (NP + 63) / 64;
-    __shared__ double ring_buf[2 * CH];
+    constexpr int CHT = ring_chunk<T>();
+    __shared__ double ring_buf[2 * CHT];
     __shared__ double cvec[NP];
     __shared__ int2 s_piv[NP];     // (the backward sweep needs no inverse pivot blocks: 4.6 KB less LDS)
     __shared__ int s_done;
@@ -1573,18 +1585,18 @@ __global__ __launch_bounds__(ST) void k_front_bwd(Plan P, int f0, int batch, con
     }
     const int lane = tid & 63;
     const bool w0 = tid < 64;
-    Ring ring{ring_buf};
-    double stage_r[CPT];
-    const long long nchunks = (F.total + CH - 1) / CH;
+    Ring<CHT> ring{ring_buf};
+    double stage_r[CHT / ST];
+    const long long nchunks = (F.total + CHT - 1) / CHT;
     const long long clast = nchunks - 1;
 
     // own: the forward (D-scaled) values; trailing: final values of the ancestors' positions
     for (int i = tid; i < NP; i += ST) cvec[i] = i < F.A ? F.xb[(long long)P.pos_index[F.p0 + i] * se] : 0.0;
     for (int u = tid; u < F.steps; u += ST) s_piv[u] = F.pv[u];
-    ring_load(F.Lb, F.total, clast, stage_r, tid);
-    ring_store(ring.buf, clast, stage_r, tid);
-    ring_load(F.Lb, F.total, clast - 1, stage_r, tid);
-    ring_store(ring.buf, clast - 1, stage_r, tid);
+    ring_load<CHT>(F.Lb, F.total, clast, stage_r, tid);
+    ring_store<CHT>(ring.buf, clast, stage_r, tid);
+    ring_load<CHT>(F.Lb, F.total, clast - 1, stage_r, tid);
+    ring_store<CHT>(ring.buf, clast - 1, stage_r, tid);
     if (tid == 0) s_done = 0;
     __syncthreads();
 
@@ -1604,9 +1616,9 @@ __global__ __launch_bounds__(ST) void k_front_bwd(Plan P, int f0, int batch, con
     long long off = F.total;                                  // stream end of this front
     int2 rec_nx = s_piv[max(t, 0)];
     for (long long c = clast;; --c) {
-        ring_load(F.Lb, F.total, c - 2, stage_r, tid);
+        ring_load<CHT>(F.Lb, F.total, c - 2, stage_r, tid);
         if (w0) {
-            const long long lower = (c - 1) * CH;          // chunks c-1 and c are resident
+            const long long lower = (c - 1) * CHT;          // chunks c-1 and c are resident
             while (t >= 0) {
                 const int2 rec = rec_nx;
                 const int type = __builtin_amdgcn_readfirstlane(rec.x >> 16);
@@ -1653,7 +1665,7 @@ __global__ __launch_bounds__(ST) void k_front_bwd(Plan P, int f0, int batch, con
         }
         __syncthreads();
         if (s_done != 0) break;
-        ring_store(ring.buf, c - 2, stage_r, tid);
+        ring_store<CHT>(ring.buf, c - 2, stage_r, tid);
         __syncthreads();
         if (c < -2) break;                                // safety
     }
@@ -1844,6 +1856,7 @@ int launch_segment(const ato_kkt* h, const Plan& P, const Vals& V, const ato_kkt
         case 6: return ATO_CALL(6);
         case 7: return ATO_CALL(7);
         case 8: return ATO_CALL(8);
+        case 9: return ATO_CALL(9);
         case 111:
             if ((long long)nf * batch >= s16_min_workgroups())
                 return launch_factor_s<11>(h, P, V, f0, nf, batch, list, inertia, st);
@@ -1904,6 +1917,7 @@ int solve_level(const ato_kkt* h, const Plan& P, int l, bool fwd, int batch, con
         case 6: return ATO_CALL(6);
         case 7: return ATO_CALL(7);
         case 8: return ATO_CALL(8);
+        case 9: return ATO_CALL(9);
         default: return fail(ATO_ERR_UNSUPPORTED, "KKT tiles");
     }
 #undef ATO_CALL
@@ -1998,9 +2012,9 @@ int ato_kkt_create(const ato_kkt_plan_desc* d, ato_kkt** out) {
     int own_total = 0;
     for (int l = 0; l < L; ++l) {
         const int T = d->level_tiles[l];
-        if (T < 1 || T > 8) {
+        if (T < 1 || T > MAX_FRONT_TILES) {
             delete h;
-            return fail(ATO_ERR_UNSUPPORTED, "KKT fronts wider than 256 positions");
+            return fail(ATO_ERR_UNSUPPORTED, "KKT fronts wider than 288 positions");
         }
         for (int f = d->level_ptr[l]; f < d->level_ptr[l + 1]; ++f) {
             const int A = d->pos_ptr[f + 1] - d->pos_ptr[f];
@@ -2016,7 +2030,7 @@ int ato_kkt_create(const ato_kkt_plan_desc* d, ato_kkt** out) {
             }
             for (int q = d->n_own[f]; q < A; ++q) {
                 const int pp = d->parent_pos[d->pos_ptr[f] + q];
-                if (pp < 0 || pp >= 256) {
+                if (pp < 0 || pp >= 32 * MAX_FRONT_TILES) {
                     delete h;
                     return fail(ATO_ERR_ARG, "KKT plan: trailing position without a parent position");
                 }

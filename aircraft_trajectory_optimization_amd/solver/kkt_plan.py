@@ -59,7 +59,7 @@ import numpy as np
 SRC_H, SRC_J, SRC_DX, SRC_DR = 0, 1, 2, 3
 SRC_SHIFT = 29
 TILE = 32
-MAX_TILES = 8              # fronts up to 256 positions (kernel register tiles)
+MAX_TILES = 9              # fronts up to 288 positions (kernel register tiles; nine for K = 7 leaves)
 
 
 def src_code(kind: int, idx: int) -> int:

@@ -46,7 +46,7 @@ typedef struct ato_kkt_plan_desc {
     const int32_t* parent_pos;  /* [P] trailing position -> position in the parent, -1 for own   */
     const int32_t* child_ptr;   /* [F + 1] offsets into child_list                               */
     const int32_t* child_list;  /* [C] children of every front (all in lower levels)             */
-    const int32_t* ent_ptr;     /* [F * 8 + 1] entries of (front, 32-row strip)                   */
+    const int32_t* ent_ptr;     /* [F * 9 + 1] entries of (front, 32-row strip), fronts <= 288      */
     const int32_t* ent_pos;     /* [E] (pa << 16) | pb, pa >= pb                                  */
     const int32_t* ent_src;     /* [E][2] (kind << 29) | index; kind 0 H, 1 J, 2 diag_x,          *
                                  * 3 diag_r; -1 = none. The value is the sum of both sources.    */

@@ -254,3 +254,16 @@ def test_device_saddle_racetrack_full_size_and_deterministic():
         fe = Factor(plan, Hb, Jb, dxb, drb)
         assert tuple(inertia[b]) == fe.inertia
         assert len(fe.sad) == spec.N
+
+
+def test_device_kkt_nine_tile_fronts_match_dense():
+    ''' K = 7 collocation (obstacles.py's default degree): the interval leaves have 261-268
+    positions, nine 32-wide tiles (the 512-thread factor kernel at T = 9 and the solve's doubled ring
+    chunk); inertia, dense residual and the CPU emulation as above '''
+    from aircraft_trajectory_optimization_amd.solver.kkt_plan import build_plan as bp
+    cfg = dict(track='race', N=3, K=7)
+    spec = product_spec(**cfg)
+    ev = random_kkt_values(spec, 0)[0]
+    plan = bp(ev.nw, ev.ng, var_stages(spec), ev.j_row_ptr, ev.j_col, ev.h_row_ptr, ev.h_col)
+    assert plan.tiles == 9, plan.tiles
+    test_device_kkt_matches_dense(cfg, 'nd')

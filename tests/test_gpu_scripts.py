@@ -6,7 +6,7 @@ Script-level solves on the device (SURVEY 8(a) rows A3/A17 as the reference's sc
     steps (base_raceline.py:226-230); the drone solve starts from the point-mass raceline;
   * scripts/obstacles.py:27-40 -- ParametricObstacleDroneRaceline with N = 100 (K = 7 collocation),
     r_c = 0.4, no gates, the tube from the mesh, warm-started from the point-mass obstacle raceline
-    (a known gap: its KKT fronts exceed the device kernels, the test is a strict xfail).
+    (its K = 7 interval fronts have 268 positions: the nine-tile KKT kernels).
 
 Each goes through the reference's API (solve() runs the batched device solver at B = 1) and must
 (1) report a feasible raceline, (2) reach the lap time of the host-KKT single-instance solver from the same guess (measured on CPU
@@ -72,12 +72,6 @@ def test_race_script_rk4_drone_solve(frame):
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.xfail(raises=ValueError, strict=True,
-                   reason='obstacles.py keeps the default K = 7: its interval fronts have 268 positions (121 '
-                          'variables + 115 rows own, 32 trailing), past the 256 of the device front kernels '
-                          '(one position per thread, 8 tiles); the device KKT plan refuses it loudly. The '
-                          'host-KKT solver runs the script (tests/script_solves_host.py: 7.4348 s lap, 253 '
-                          'iterations). DESIGN 9: nine-tile fronts.')
 def test_obstacles_script_drone_solve():
     from aircraft_trajectory_optimization_amd.obstacles.mesh_obstacle import MeshObstacle
     from aircraft_trajectory_optimization_amd.pytypes import DroneConfig
@@ -104,8 +98,7 @@ def test_obstacles_script_drone_solve():
           f'min obstacle distance {d.min():.4f} m')
     assert res.feasible and solver.ws_raceline.feasible
     ref = HOST_LAP['obstacles_N100']
-    if ref is not None:
-        assert abs(res.time - ref) <= 1e-5, (res.time, ref)
+    assert abs(res.time - ref) <= 1e-6, (res.time, ref)      # measured 5e-10 (gpurun_out r04t9)
     nlp = RefNLP(oracle_line('obstacles', True), 'drone', 'parametric', 100, 7,
                  veh={'use_quat': True, 'global_r': True, 'collision_radius': 0.4}, fixed_gates=[],
                  spheres=solver.sphere_table, quat_flip=sp.quat_flip, euler_wraps=sp.euler_wraps)

@@ -65,7 +65,7 @@ def test_plan_racetrack_full_size_fits_device_tiles():
                        split_pairs=False)
     assert plain.n_fronts == 100 and plain.n_levels == 8 and plain.level_tiles[0] == 7
     assert plan.max_block <= 256
-    assert (np.diff(plan.ent_ptr[::8]) <= 4096).all()
+    assert (np.diff(plan.ent_ptr[::MAX_TILES]) <= 4096).all()
     chain = build_plan(ev.nw, ev.ng, var_stages(spec), ev.j_row_ptr, ev.j_col, ev.h_row_ptr, ev.h_col, 'chain')
     assert chain.n_fronts == 51 and chain.tiles == 8
 
