@@ -142,6 +142,10 @@ for s in $STEPS; do
                    if [ $v = base ]; then lp=$PWD/tools/diag/_lib/libato_base.so; else lp=; fi
                    ATO_LIB_PATH=$lp ATO_DEBUG_HESS_NONFINITE=1 run solve_nan_$v 300 python tools/solve_batched.py --batch 64 --max-iter 1000 --cold --no-host --out "$OUT/solve_nan_$v.json"
                done ;;
+        pmctile) for t in 0 8; do
+                   ATO_EVAL_TILE=$t run pmc_fetch_tile$t 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_tile$t" -o run -- \
+                       python bench.py --steps 10 --warmup 3 --batch 4096 --no-cpu-baseline --no-solve --eval-steps 10
+                done ;;
         spectests) run pytest_spec 300 python -u -m pytest tests/test_gpu_batched_ipm.py -x -v -s --timeout 200 --timeout-method thread -p no:cacheprovider -k "speculative or deterministic or restoration" ;;
         scripts) run pytest_scripts 900 python -u -m pytest tests/test_gpu_scripts.py -x -v -s --timeout 800 --timeout-method thread -p no:cacheprovider ;;
         mbscale) run mb_store_scale 120 ./tools/mb_store_scale
