@@ -2,6 +2,7 @@
 // and dispatch of ato_eval to the per-model launchers (ato_inst.hip).
 #include <hip/hip_runtime.h>
 #include <string>
+#include <exception>
 #include <new>
 #include <cstdlib>
 #include <cstring>
@@ -63,7 +64,22 @@ const char* ato_last_error(void) { return g_last_error.c_str(); }
 
 const char* ato_version(void) { return "ato 2 gfx950"; }
 
-int ato_create(const ato_problem_desc* desc, ato_handle** out) {
+static int create_impl(const ato_problem_desc* desc, ato_handle** out);
+
+// C++ exceptions (std::bad_alloc, std::length_error of the host layout / Hessian analysis) must not
+// cross the C ABI: they would end the host process in std::terminate (SIGABRT)
+#define ATO_NOEXCEPT_BODY(expr)                                                                   \
+    try {                                                                                        \
+        return (expr);                                                                           \
+    } catch (const std::exception& e_) {                                                         \
+        return fail(ATO_ERR_ARG, std::string("host exception: ") + e_.what());                   \
+    } catch (...) {                                                                              \
+        return fail(ATO_ERR_ARG, "host exception");                                              \
+    }
+
+int ato_create(const ato_problem_desc* desc, ato_handle** out) { ATO_NOEXCEPT_BODY(create_impl(desc, out)) }
+
+static int create_impl(const ato_problem_desc* desc, ato_handle** out) {
     if (!desc || !out) return fail(ATO_ERR_ARG, "null argument");
     *out = nullptr;
     ato_handle* h = new (std::nothrow) ato_handle();
@@ -179,6 +195,8 @@ int ato_bounds(const ato_handle* h, double* lbg, double* ubg) {
 
 static int hess_reserve(ato_handle* h, int32_t max_batch) {
     if (max_batch <= h->hess_reserved) return ATO_OK;
+    // the old scratch may still be read by kernels queued on any stream: drain before freeing
+    if (h->d_dJ || h->d_dgf) ATO_HIP(hipDeviceSynchronize());
     (void)hipFree(h->d_dJ);
     (void)hipFree(h->d_dgf);
     h->d_dJ = h->d_dgf = nullptr;
@@ -196,7 +214,10 @@ int ato_reserve(ato_handle* h, int32_t max_batch) {
         if (rc) return rc;
     }
     if (max_batch <= h->reserved) return ATO_OK;
-    if (h->d_fpart) ATO_HIP(hipFree(h->d_fpart));
+    if (h->d_fpart) {
+        ATO_HIP(hipDeviceSynchronize());        // queued evaluations may still write the old partials
+        ATO_HIP(hipFree(h->d_fpart));
+    }
     h->d_fpart = nullptr;
     h->reserved = 0;
     ATO_HIP(hipMalloc(&h->d_fpart, (size_t)h->L.p.N * max_batch * sizeof(double)));
@@ -281,7 +302,9 @@ extern "C" int ato_timing_read(ato_handle* h, double* eval_ms, double* reduce_ms
 }
 
 // Hessian structure, colouring and recovery tables (host analysis + upload), once per handle
-static int ensure_hess(ato_handle* h) {
+static int ensure_hess_impl(ato_handle* h);
+static int ensure_hess(ato_handle* h) { ATO_NOEXCEPT_BODY(ensure_hess_impl(h)) }
+static int ensure_hess_impl(ato_handle* h) {
     if (h->hess_ready) return ATO_OK;
     std::string err = h->HL.build(h->L);
     if (!err.empty()) return fail(ATO_ERR_UNSUPPORTED, err);

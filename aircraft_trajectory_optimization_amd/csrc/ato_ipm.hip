@@ -524,7 +524,7 @@ __device__ __forceinline__ double tpow(double x, double e) {
 }
 
 struct FilterPrm {
-    double s_phi, s_theta, delta, eta_phi, gamma_theta, gamma_phi;
+    double s_phi, s_theta, delta, eta_phi, gamma_theta, gamma_phi, obj_max_inc;
 };
 
 __global__ __launch_bounds__(CB) void k_filter_accept(int W, int fmax, const double* __restrict__ theta,
@@ -555,8 +555,15 @@ __global__ __launch_bounds__(CB) void k_filter_accept(int W, int fmax, const dou
     const bool arm_case = (th <= theta_min[b]) && switching;
     const bool ok_arm = pt <= ph + (o.eta_phi * al) * gd;
     const bool ok_suf = (tt <= (1.0 - o.gamma_theta) * th) || (pt <= ph - o.gamma_phi * th);
+    // obj_max_inc (FilterLSAcceptor::CheckAcceptabilityOfTrialPoint): the barrier objective may not
+    // grow by more than 10^obj_max_inc of its magnitude
+    bool inc = false;
+    if (pt > ph) {
+        const double base = fabs(ph) > 10.0 ? log10(fabs(ph)) : 1.0;
+        inc = log10(pt - ph) > o.obj_max_inc + base;
+    }
     const bool pd = pend[b] != 0;
-    const bool ok = pd && !rej && !in_f && (arm_case ? ok_arm : ok_suf);
+    const bool ok = pd && !rej && !inc && !in_f && (arm_case ? ok_arm : ok_suf);
     ok_out[b] = ok ? 1 : 0;
     arm_out[b] = (ok && arm_case) ? 1 : 0;
     soc_out[b] = (pd && !ok && first[b] != 0 && tt >= th) ? 1 : 0;
@@ -696,7 +703,7 @@ int ato_ipm_filter_accept(int32_t W, int32_t fmax, const double* theta, const do
     if (!theta || !phi || !gphi_d || !alpha || !tht || !pht || (fmax && !F) || !nf || !theta_max || !theta_min ||
         !pend || !first || !ok || !arm || !soc)
         return fail(ATO_ERR_ARG, "ato_ipm_filter_accept: arguments");
-    const FilterPrm o{prm[0], prm[1], prm[2], prm[3], prm[4], prm[5]};   // prm: host array (ato_ipm.h)
+    const FilterPrm o{prm[0], prm[1], prm[2], prm[3], prm[4], prm[5], prm[6]};   // prm: host array (ato_ipm.h)
     hipLaunchKernelGGL(k_filter_accept, dim3((W + CB - 1) / CB), dim3(CB), 0, static_cast<hipStream_t>(stream), W,
                        fmax, theta, phi, gphi_d, alpha, tht, pht, F, nf, theta_max, theta_min, pend, first, o, ok,
                        arm, soc);

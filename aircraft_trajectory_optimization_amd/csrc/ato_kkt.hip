@@ -24,6 +24,7 @@
 // 256-thread workgroup per (front, instance): wave 0 sweeps with the front vector in
 // registers (4 positions per lane), all four waves stream the factor columns through a
 // two-slot LDS ring so that the sweep reads LDS only.
+#include <exception>
 #include <hip/hip_runtime.h>
 #include <algorithm>
 #include <string>
@@ -1985,7 +1986,20 @@ int ato_kkt_diag_stamps(unsigned long long* out) {
 }
 #endif
 
+static int kkt_create_impl(const ato_kkt_plan_desc* d, ato_kkt** out);
+
+// host exceptions of the plan set-up must not cross the C ABI (std::terminate would abort the process)
 int ato_kkt_create(const ato_kkt_plan_desc* d, ato_kkt** out) {
+    try {
+        return kkt_create_impl(d, out);
+    } catch (const std::exception& e) {
+        return fail(ATO_ERR_ARG, std::string("host exception: ") + e.what());
+    } catch (...) {
+        return fail(ATO_ERR_ARG, "host exception");
+    }
+}
+
+static int kkt_create_impl(const ato_kkt_plan_desc* d, ato_kkt** out) {
     if (!d || !out) return fail(ATO_ERR_ARG, "null argument");
     *out = nullptr;
     if (d->n_fronts < 1 || d->n_levels < 1 || d->n < 0 || d->m < 0) return fail(ATO_ERR_ARG, "bad KKT plan sizes");
@@ -2155,6 +2169,7 @@ int ato_kkt_destroy(ato_kkt* h) {
 int ato_kkt_reserve(ato_kkt* h, int32_t max_batch) {
     if (!h || max_batch < 0) return fail(ATO_ERR_ARG, "bad argument");
     if (max_batch <= h->cap) return ATO_OK;
+    if (h->d_L) KKT_HIP(hipDeviceSynchronize());    // queued factor / solve kernels may still use the old storage
     free_storage(h);
     const size_t B = (size_t)max_batch;
     KKT_HIP(hipMalloc((void**)&h->d_L, sizeof(double) * std::max<size_t>(1, (size_t)h->l_size * B)));

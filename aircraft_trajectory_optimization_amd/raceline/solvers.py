@@ -30,6 +30,10 @@ from aircraft_trajectory_optimization_amd.utils.discretization_utils import inte
     interpolate_linear
 
 # decision vectors of solutions produced here, so a RacelineResults can warm-start a drone solve
+# further solver options for every solve (the reference passes ipopt.* options as a dict to
+# ca.nlpsol, base_raceline.py:752-799): IPMOptions field names, e.g. {'max_soc': 0}
+SOLVER_OPTIONS: dict = {}
+
 _SOLUTIONS: Dict[int, Tuple[ProblemSpec, np.ndarray, RacelineResults]] = {}
 
 
@@ -80,7 +84,8 @@ class _Raceline:
     def solve(self) -> RacelineResults:
         from aircraft_trajectory_optimization_amd.raceline.evaluator import DeviceEvaluator
         from aircraft_trajectory_optimization_amd.solver.ipm import IPMOptions
-        opts = IPMOptions(max_iter=self.config.max_iter, verbose=bool(getattr(self.config, 'verbose', False)))
+        opts = IPMOptions(**{'max_iter': self.config.max_iter, 'verbose': bool(getattr(self.config, 'verbose', False)),
+                             **SOLVER_OPTIONS})
         if isinstance(self.evaluator, DeviceEvaluator):
             x, success = self._solve_device(opts)
         else:

@@ -5,22 +5,24 @@ ca.nlpsol('solver', 'ipopt', ...), base_raceline.py:752-799), driving the HIP ev
     min f(x)  s.t.  g_L <= g(x) <= g_U,  x_L <= x <= x_U
 
 Algorithm (Waechter & Biegler, Math. Prog. 106 (2006), the published IPOPT method) with
-IPOPT's default options:
+IPOPT's default options (the reference sets only max_iter, honor_original_bounds and the linear
+solver, base_raceline.py:765-799):
   * gradient-based NLP scaling (max gradient 100), bound relaxation 1e-8, bound push 1e-2,
     least-squares constraint multipliers (dropped above 1e3), bound multipliers 1
   * equality rows c(x) = 0; inequality rows d(x) - s = 0 with bounded slacks
-  * monotone (Fiacco-McCormick) barrier: mu0 = 0.1, kappa_mu = 0.2, theta_mu = 1.5,
-    kappa_eps = 10, tau = max(0.99, 1 - mu), linear damping 1e-5 of one-sided bounds
-  * Newton step on the primal-dual system with the slack block eliminated; regularisation
-    delta_w / delta_c by IPOPT's rules (PDPerturbationHandler), including its structural
-    degeneracy test: while undetermined, every iteration first tries delta_w = delta_c = 0; an
-    iteration that needs no perturbation marks the Hessian and the Jacobian non-degenerate for
-    good, and after degen_iters_max (3) iterations that needed one, the Hessian (delta_w > 0) or the
-    Jacobian (delta_c > 0) is declared degenerate: its perturbation then starts at
-    max(delta_w_min, kappa_w^- delta_w_last) (resp. delta_c > 0) without the unperturbed attempt.
-    Without the stage structure (no inertia from the sparse LU) the inertia-free curvature test
-    (Chiang & Zavala 2016) decides when delta_w must grow
-  * filter line search with switching / Armijo conditions and second-order corrections
+  * monotone (Fiacco-McCormick) barrier (MonotoneMuUpdate): mu0 = 0.1, kappa_mu = 0.2,
+    theta_mu = 1.5, kappa_eps = 10, floor min(tol, compl_inf_tol) / (kappa_eps + 1),
+    tau = max(0.99, 1 - mu), linear damping 1e-5 of one-sided bounds; no update in the first
+    iteration of a restoration phase
+  * Newton step on the primal-dual system with the slack block eliminated; the regularisation
+    delta_w / delta_c follows IPOPT's PDPerturbationHandler state by state (PerturbationHandler
+    below): the structural-degeneracy test, singular matrices (a zero eigenvalue, too few negative
+    eigenvalues, an unrefinable solve) perturbed first in delta_c, wrong inertia in delta_w
+    (kappa_w^- / kappa_w^+ / kappa_w^+bar, max_hessian_perturbation 1e20). Without the stage
+    structure (no inertia from the sparse LU) the inertia-free curvature test (Chiang & Zavala
+    2016) decides when delta_w must grow
+  * filter line search with switching / Armijo conditions, obj_max_inc (5) and second-order
+    corrections
   * convergence on the scaled optimality error E_0 <= tol (1e-8) plus IPOPT's unscaled
     dual / constraint / complementarity limits; "acceptable" level 1e-6 for 15 iterations
   * the watchdog (non-monotone) procedure: after 10 consecutive shortened steps the full step is
@@ -31,11 +33,20 @@ IPOPT's default options:
     the constraint violation below 1e-4) is taken in full without a line search and forces a
     barrier decrease; with the barrier already at its minimum the solve stops ('tiny_step', IPOPT's
     "search direction becomes too small")
-  * feasibility restoration when the line search fails or no search direction can be computed
-    (IPOPT's fallback mechanism; its min ||c||_1 phase): an
-    interior-point solve of  min rho sum(p + n) + zeta/2 |D_R (x - x_r)|^2  s.t.  c(x) - p + n
-    within the bounds, p, n >= 0  (rho = 1000, zeta = sqrt(mu), D_R = min(1, 1/|x_r|)), started
-    from the closed-form p, n and stopped as soon as the original filter accepts its iterate
+  * the soft restoration phase (soft_resto_pderror_reduction_factor 0.9999, max_soft_resto_iters
+    10): when the line search fails, the full fraction-to-the-boundary step of primal and dual
+    variables is taken if it reduces the primal-dual system error; the phase ends when a step is
+    acceptable to the original filter, and the regular restoration follows when it cannot go on
+  * feasibility restoration when the soft phase fails or no search direction can be computed
+    (IPOPT's fallback mechanism; MinC_1NrmRestorationPhase): an interior-point solve of
+    min rho sum(p + n) + zeta/2 |D_R (x - x_r)|^2  s.t.  c(x) - p + n = 0, d(x) - p + n - s = 0
+    (rho = 1000, zeta = sqrt of the restoration's barrier parameter, D_R = min(1, 1/|x_r|)), started
+    from the current x, s, the
+    closed-form p, n and mu_R = max(mu, |c|_inf, |d - s|_inf), theta_max_fact 1e8, left as soon as
+    the original filter accepts its iterate with a 0.9 reduction of the violation; its iterations
+    count toward max_iter. On return the bound multipliers take the Newton step of the whole
+    restoration move (reset to 1 above bound_mult_reset_threshold = 1000) and the constraint
+    multipliers are zero (constr_mult_reset_threshold = 0: the least-squares estimate is not used)
 
 The evaluator supplies f, g, grad f, the Jacobian (CSR) and the Lagrangian Hessian (lower
 CSR); in the product it is the HIP library (raceline/evaluator.py).
@@ -88,21 +99,28 @@ class IPMOptions:
     kappa_soc: float = 0.99
     theta_max_fact: float = 1e4
     theta_min_fact: float = 1e-4
-    # inertia correction
-    delta_w_0: float = 1e-4
-    delta_w_min: float = 1e-20
-    delta_w_max: float = 1e40
-    kappa_w_minus: float = 1.0 / 3.0
-    kappa_w_plus: float = 8.0
-    kappa_w_plus_bar: float = 100.0
-    delta_c_base: float = 1e-8
-    kappa_c: float = 0.25
+    obj_max_inc: float = 5.0
+    # inertia correction (PDPerturbationHandler)
+    delta_w_0: float = 1e-4                 # first_hessian_perturbation
+    delta_w_min: float = 1e-20              # min_hessian_perturbation
+    delta_w_max: float = 1e20               # max_hessian_perturbation
+    kappa_w_minus: float = 1.0 / 3.0        # perturb_dec_fact
+    kappa_w_plus: float = 8.0               # perturb_inc_fact
+    kappa_w_plus_bar: float = 100.0         # perturb_inc_fact_first
+    delta_c_base: float = 1e-8              # jacobian_regularization_value
+    kappa_c: float = 0.25                   # jacobian_regularization_exponent
     degen_iters_max: int = 3
     honor_original_bounds: bool = True
     nlp_scaling: bool = True
+    # restoration (MinC_1NrmRestorationPhase)
     resto_penalty: float = 1000.0
-    resto_kappa: float = 0.9
-    max_resto: int = 50
+    resto_kappa: float = 0.9                # required_infeasibility_reduction
+    resto_theta_max_fact: float = 1e8       # resto.theta_max_fact
+    bound_mult_reset_threshold: float = 1000.0
+    constr_mult_reset_threshold: float = 0.0
+    soft_resto_pderror_reduction_factor: float = 0.9999
+    max_soft_resto_iters: int = 10
+    max_resto: int = 10 ** 9               # (IPOPT has no limit on restoration phases)
     # watchdog (IPOPT: watchdog_shortened_iter_trigger, watchdog_trial_iter_max)
     watchdog_shortened_iter_trigger: int = 10
     watchdog_trial_iter_max: int = 3
@@ -110,6 +128,11 @@ class IPMOptions:
     tiny_step_tol: float = 10 * 2.220446049250313e-16
     tiny_step_y_tol: float = 1e-2
     verbose: bool = False
+
+    @property
+    def mu_min(self) -> float:
+        ''' MonotoneMuUpdate's floor: min(tol, compl_inf_tol) / (barrier_tol_factor + 1) '''
+        return min(self.tol, self.compl_inf_tol) / (self.kappa_eps + 1.0)
 
 
 @dataclass
@@ -127,50 +150,126 @@ class IPMResult:
 
 
 DEG_UNKNOWN, DEG_NO, DEG_YES = 0, 1, 2
+# PDPerturbationHandler's test states: no test, (delta_c, delta_x) = (0, 0), (>0, 0), (0, >0), (>0, >0)
+T_NONE, T_C0X0, T_CPX0, T_C0XP, T_CPXP = range(5)
 
 
-def degeneracy_update(hdeg, jdeg, diters, dc_pos, dw_pos, iters_max):
+class PerturbationHandler:
     '''
-    IPOPT's structural-degeneracy test (PDPerturbationHandler::finalize_test) after an iteration
-    whose perturbation was tested from zero: (hdeg, jdeg, diters) updated from whether the accepted
-    factorisation needed delta_c > 0 / delta_w > 0
+    IPOPT's PDPerturbationHandler (IpPDPerturbationHandler.cpp) for one instance: the delta_w
+    (delta_x = delta_s) and delta_c (= delta_d) of every factorisation of an iteration, and the
+    structural-degeneracy test. consider_new_system() opens an iteration; after a factorisation,
+    perturb_for_singularity() (a zero eigenvalue, too few negative eigenvalues, an unrefinable
+    solve) or perturb_for_wrong_inertia() (too many negative eigenvalues) gives the next attempt;
+    None means no perturbation is left (delta_w above its maximum: no search direction).
     '''
-    if not dc_pos and not dw_pos:         # no perturbation needed: nothing is degenerate
-        return (DEG_NO if hdeg == DEG_UNKNOWN else hdeg), (DEG_NO if jdeg == DEG_UNKNOWN else jdeg), diters
-    if dw_pos and not dc_pos:
-        jdeg = DEG_NO if jdeg == DEG_UNKNOWN else jdeg
-        if hdeg == DEG_UNKNOWN:
-            diters += 1
-            if diters >= iters_max:
-                hdeg = DEG_YES
-        return hdeg, jdeg, diters
-    if dc_pos and not dw_pos:
-        hdeg = DEG_NO if hdeg == DEG_UNKNOWN else hdeg
-        if jdeg == DEG_UNKNOWN:
-            diters += 1
-            if diters >= iters_max:
-                jdeg = DEG_YES
-        return hdeg, jdeg, diters
-    diters += 1
-    if diters >= iters_max:
-        hdeg = DEG_YES if hdeg == DEG_UNKNOWN else hdeg
-        jdeg = DEG_YES if jdeg == DEG_UNKNOWN else jdeg
-    return hdeg, jdeg, diters
 
+    def __init__(self, o: IPMOptions):
+        self.o = o
+        self.hdeg = self.jdeg = DEG_UNKNOWN
+        self.diters = 0
+        self.test = T_NONE
+        self.dx = self.dc = 0.0              # delta_x_curr_, delta_c_curr_
+        self.dx_last = self.dc_last = 0.0
 
-def degeneracy_update_cols(hdeg, jdeg, diters, dc_pos, dw_pos, iters_max, testing):
-    ''' degeneracy_update per column (torch tensors); only the `testing` columns change '''
-    import torch
-    unk_h, unk_j = hdeg == DEG_UNKNOWN, jdeg == DEG_UNKNOWN
-    none = testing & ~dc_pos & ~dw_pos
-    only_w, only_c, both = testing & dw_pos & ~dc_pos, testing & dc_pos & ~dw_pos, testing & dc_pos & dw_pos
-    diters = torch.where((only_w & unk_h) | (only_c & unk_j) | both, diters + 1, diters)
-    reach = diters >= iters_max
-    hdeg = torch.where(((none | only_c) & unk_h), torch.full_like(hdeg, DEG_NO),
-                       torch.where((only_w | both) & unk_h & reach, torch.full_like(hdeg, DEG_YES), hdeg))
-    jdeg = torch.where(((none | only_w) & unk_j), torch.full_like(jdeg, DEG_NO),
-                       torch.where((only_c | both) & unk_j & reach, torch.full_like(jdeg, DEG_YES), jdeg))
-    return hdeg, jdeg, diters
+    def delta_cd(self, mu):
+        return self.o.delta_c_base * mu ** self.o.kappa_c
+
+    def finalize_test(self):
+        o, t = self.o, self.test
+        if t == T_NONE:
+            return
+        if t == T_C0X0:
+            if self.hdeg == DEG_UNKNOWN and self.jdeg == DEG_UNKNOWN:
+                self.hdeg = self.jdeg = DEG_NO
+            elif self.hdeg == DEG_UNKNOWN:
+                self.hdeg = DEG_NO
+            elif self.jdeg == DEG_UNKNOWN:
+                self.jdeg = DEG_NO
+        elif t == T_CPX0:
+            if self.hdeg == DEG_UNKNOWN:
+                self.hdeg = DEG_NO
+            if self.jdeg == DEG_UNKNOWN:
+                self.diters += 1
+                if self.diters >= o.degen_iters_max:
+                    self.jdeg = DEG_YES
+        elif t == T_C0XP:
+            if self.jdeg == DEG_UNKNOWN:
+                self.jdeg = DEG_NO
+            if self.hdeg == DEG_UNKNOWN:
+                self.diters += 1
+                if self.diters >= o.degen_iters_max:
+                    self.hdeg = DEG_YES
+        else:
+            self.diters += 1
+            if self.diters >= o.degen_iters_max:
+                self.hdeg = self.jdeg = DEG_YES
+
+    def _wrong_inertia(self):
+        ''' get_deltas_for_wrong_inertia: the next delta_x; False past max_hessian_perturbation '''
+        o = self.o
+        if self.dx == 0.0:
+            self.dx = o.delta_w_0 if self.dx_last == 0.0 else max(o.delta_w_min, self.dx_last * o.kappa_w_minus)
+        elif self.dx_last == 0.0 or 1e5 * self.dx_last < self.dx:
+            self.dx *= o.kappa_w_plus_bar
+        else:
+            self.dx *= o.kappa_w_plus
+        return self.dx <= o.delta_w_max
+
+    def consider_new_system(self, mu):
+        self.finalize_test()
+        if self.dx > 0:
+            self.dx_last = self.dx
+        if self.dc > 0:
+            self.dc_last = self.dc
+        self.test = T_C0X0 if (self.hdeg == DEG_UNKNOWN or self.jdeg == DEG_UNKNOWN) else T_NONE
+        self.dc = self.delta_cd(mu) if self.jdeg == DEG_YES else 0.0
+        self.dx = 0.0
+        if self.hdeg == DEG_YES and not self._wrong_inertia():
+            return None
+        return self.dx, self.dc
+
+    def perturb_for_singularity(self, mu):
+        if self.hdeg == DEG_UNKNOWN or self.jdeg == DEG_UNKNOWN:
+            t = self.test
+            if t == T_C0X0:
+                if self.jdeg == DEG_UNKNOWN:
+                    self.dc = self.delta_cd(mu)
+                    self.test = T_CPX0
+                else:
+                    if not self._wrong_inertia():
+                        return None
+                    self.test = T_C0XP
+            elif t == T_CPX0:
+                self.dc = 0.0
+                if not self._wrong_inertia():
+                    return None
+                self.test = T_C0XP
+            elif t == T_C0XP:
+                self.dc = self.delta_cd(mu)
+                if not self._wrong_inertia():
+                    return None
+                self.test = T_CPXP
+            elif not self._wrong_inertia():
+                return None
+        elif self.dc > 0 or self.jdeg == DEG_YES:
+            if not self._wrong_inertia():
+                return None
+        else:
+            self.dc = self.delta_cd(mu)
+        return self.dx, self.dc
+
+    def perturb_for_wrong_inertia(self, mu):
+        self.finalize_test()
+        ok = self._wrong_inertia()
+        if not ok and self.dc == 0.0:
+            self.dc = self.delta_cd(mu)
+            self.dx = 0.0
+            self.test = T_NONE
+            if self.hdeg == DEG_YES:
+                self.hdeg = DEG_UNKNOWN
+            ok = self._wrong_inertia()
+        return (self.dx, self.dc) if ok else None
 
 
 def _lower_to_full(n, row_ptr, col, vals):
@@ -237,7 +336,13 @@ class InteriorPointSolver:
         with threadpool_limits(limits=1, user_api='blas'):
             return self._solve(x0, mu0, stop_check, in_resto)
 
-    def _solve(self, x0, mu0, stop_check, in_resto) -> IPMResult:
+    def _solve(self, x0, mu0, stop_check, in_resto, resto_init=None) -> IPMResult:
+        '''
+        stop_check(x) -> bool ends the solve with 'stopped' (checked from the second iteration on).
+        resto_init (the restoration phase's own solve, RestoIterateInitializer): dict with the
+        starting slacks 's', bound multipliers 'zl', 'zu', 'vl', 'vu' (None: bound_mult_init_val),
+        'accept' (x, s) -> bool (the return test on the original problem), 'theta_max_fact'
+        '''
         o = self.o
         n, m = self.n, self.m
         x = np.asarray(x0, float).copy()
@@ -263,16 +368,23 @@ class InteriorPointSolver:
                              np.where(self.ubx0 < INF, self.ubx0, np.inf))
         hxl, hxu, hsl, hsu = np.isfinite(xL), np.isfinite(xU), np.isfinite(dL), np.isfinite(dU)
         ieq, iin = np.nonzero(self.eq)[0], np.nonzero(self.ineq)[0]
-        me, mi = len(ieq), len(iin)
+        self.geom = (c_rhs, dL, dU, xL, xU, ieq, iin)
 
         # ---- initial point
-        x = self._push(x, xL, xU)
-        f, g, gf, jv = self._eval(x)
-        s = self._push(g[iin], dL, dU)
-        zl = np.where(hxl, o.bound_mult_init_val, 0.0)
-        zu = np.where(hxu, o.bound_mult_init_val, 0.0)
-        vl = np.where(hsl, o.bound_mult_init_val, 0.0)
-        vu = np.where(hsu, o.bound_mult_init_val, 0.0)
+        if resto_init is None:
+            x = self._push(x, xL, xU)
+            f, g, gf, jv = self._eval(x)
+            s = self._push(g[iin], dL, dU)
+            zl = np.where(hxl, o.bound_mult_init_val, 0.0)
+            zu = np.where(hxu, o.bound_mult_init_val, 0.0)
+            vl = np.where(hsl, o.bound_mult_init_val, 0.0)
+            vu = np.where(hsu, o.bound_mult_init_val, 0.0)
+        else:
+            f, g, gf, jv = self._eval(x)
+            s = np.asarray(resto_init['s'], float).copy()
+            zl, zu, vl, vu = (np.where(h, resto_init[k], 0.0) if resto_init.get(k) is not None else
+                              np.where(h, o.bound_mult_init_val, 0.0)
+                              for k, h in (('zl', hxl), ('zu', hxu), ('vl', hsl), ('vu', hsu)))
         J = self._J(jv)
         y = self._ls_multipliers(J, gf, zl, zu, vl, vu, iin)
         mu = o.mu_init if mu0 is None else mu0
@@ -325,22 +437,48 @@ class InteriorPointSolver:
             co = np.abs(compl).max(initial=0)
             return max(du / s_d, pr, co / s_c), du, pr, co
 
+        def pd_error(gf, J, g, x, s, y, zl, zu, vl, vu, mu):
+            ''' IpoptCalculatedQuantities::*_primal_dual_system_error: 1-norms of the dual,
+            primal and complementarity residuals over the number of their entries '''
+            a, b, c, d = slacks(x, s)
+            dual_x = gf + J.T @ y - zl + zu
+            dual_s = -y[iin] - vl + vu
+            _, r = theta_of(g, s)
+            compl = np.concatenate([(a * zl - mu)[hxl], (b * zu - mu)[hxu], (c * vl - mu)[hsl], (d * vu - mu)[hsu]])
+            cnt = n + len(iin) + m + len(compl)
+            return (np.abs(dual_x).sum() + np.abs(dual_s).sum() + np.abs(r).sum() + np.abs(compl).sum()) / max(cnt, 1)
+
+        def kappa_sigma(x, s, zl, zu, vl, vu, mu):
+            # AcceptTrialPoint: keep bound multipliers within kappa_sigma of mu / slack
+            a, b, c, d = slacks(x, s)
+            ks = o.kappa_sigma
+            return (np.where(hxl, np.clip(zl, mu / (ks * a), ks * mu / a), 0),
+                    np.where(hxu, np.clip(zu, mu / (ks * b), ks * mu / b), 0),
+                    np.where(hsl, np.clip(vl, mu / (ks * c), ks * mu / c), 0),
+                    np.where(hsu, np.clip(vu, mu / (ks * d), ks * mu / d), 0))
+
         theta0, _ = theta_of(g, s)
-        theta_max = o.theta_max_fact * max(1.0, theta0)
+        tmf = o.theta_max_fact if resto_init is None else resto_init.get('theta_max_fact', o.theta_max_fact)
+        theta_max = tmf * max(1.0, theta0)
         theta_min = o.theta_min_fact * max(1.0, theta0)
         filt: List[tuple] = []
-        delta_w_last = 0.0
+        pert = PerturbationHandler(o)
+        self.pert = pert
+        self._last_step = ''
         n_acc = 0
         history = []
         status = 'max_iter'
-        it = 0
-        hdeg = jdeg = DEG_UNKNOWN      # structural degeneracy of the Hessian / the Jacobian (IPOPT)
-        diters = 0
+        it = 0                    # iterations, restoration iterations included (IPOPT's iter_count)
         ws_short = 0              # consecutive accepted steps shorter than alpha_max (watchdog trigger)
         wd = None                 # watchdog point and direction while the watchdog is active
         tiny_flag = False         # the last step was tiny: force a barrier decrease
+        in_soft = False           # soft restoration phase
+        soft_count = 0
+        first_resto_iter = in_resto
         self.wd_stats = {'started': 0, 'succeeded': 0, 'reverted': 0, 'tiny_steps': 0}
-        for it in range(o.max_iter + 1):
+        self.soft_stats = {'entered': 0, 'steps': 0, 'left': 0}
+        resto_accept = None if resto_init is None else resto_init.get('accept')
+        while True:
             J = self._J(jv)
             E0, du, pr, co = errors(gf, J, g, x, s, y, zl, zu, vl, vu, 0.0)
             # unscaled checks (IPOPT): dual on f-units, primal on g-units
@@ -348,10 +486,16 @@ class InteriorPointSolver:
             history.append({'iter': it, 'f': f / self.sf, 'inf_pr': pr, 'inf_du': du, 'mu': mu, 'E0': E0,
                             'resto': n_resto})
             if o.verbose:
-                print(f'{"r" if in_resto else " "}{it:4d} f={f / self.sf: .10e} pr={pr:.2e} du={du:.2e} mu={mu:.1e}')
-            if stop_check is not None and it > 0 and stop_check(x):
-                status = 'stopped'
-                break
+                print(f'{"r" if in_resto else " "}{it:4d} f={f / self.sf: .10e} pr={pr:.2e} du={du:.2e} mu={mu:.1e}'
+                      f' dw={pert.dx:.1e} {self._last_step}{" s" if in_soft else ""}')
+            self._last_step = ''
+            if len(history) > 1:
+                if stop_check is not None and stop_check(x):
+                    status = 'stopped'
+                    break
+                if resto_accept is not None and resto_accept(x, s):
+                    status = 'stopped'
+                    break
             if E0 <= o.tol and du / self.sf <= o.dual_inf_tol and pr_uns <= o.constr_viol_tol and \
                     co <= o.compl_inf_tol:
                 status = 'optimal'
@@ -360,23 +504,31 @@ class InteriorPointSolver:
             if n_acc >= o.acceptable_iter:
                 status = 'acceptable'
                 break
-            if it == o.max_iter:
+            if it >= o.max_iter:
                 break
             # ---- barrier update (monotone); a tiny step forces one decrease, and with mu already at
-            # its minimum ends the solve (IPOPT: MonotoneMuUpdate, TINY_STEP_DETECTED)
+            # its minimum ends the solve (IPOPT: MonotoneMuUpdate, TINY_STEP_DETECTED); not in the first
+            # iteration of a restoration phase
             force, tiny_flag = tiny_flag, False
-            while True:
+            while not first_resto_iter:
                 Emu = errors(gf, J, g, x, s, y, zl, zu, vl, vu, mu)[0]
                 if Emu > o.kappa_eps * mu and not force:
                     break
-                if mu <= o.tol / 10:
+                mu_new = max(o.mu_min, min(o.kappa_mu * mu, mu ** o.theta_mu))
+                if mu_new == mu:
                     if force:
                         status = 'tiny_step'
                     break
-                mu = max(o.tol / 10, min(o.kappa_mu * mu, mu ** o.theta_mu))
+                mu = mu_new
                 tau = max(o.tau_min, 1.0 - mu)
                 filt = []
                 force = False
+                if hasattr(self.ev, 'set_mu'):
+                    # the restoration objective depends on the barrier parameter (RestoIpoptNLP::f(x, mu):
+                    # proximity weight sqrt(mu)): f and its gradient at the current point for the new mu
+                    self.ev.set_mu(mu)
+                    f, g, gf, jv = self._eval(x)
+            first_resto_iter = False
             if status == 'tiny_step':
                 break
             # ---- Newton step
@@ -390,12 +542,8 @@ class InteriorPointSolver:
             rhs_x = -(gx + J.T @ y)
             rhs_s = -(gs - y[iin])
             rhs_y = -r
-            testing = hdeg == DEG_UNKNOWN or jdeg == DEG_UNKNOWN
-            step = self._kkt(W, J, Sx, Ss, rhs_x, rhs_s, rhs_y, iin, mu, delta_w_last,
-                             start_dw=hdeg == DEG_YES, start_dc=jdeg == DEG_YES)
-            if testing and step is not None:
-                hdeg, jdeg, diters = degeneracy_update(hdeg, jdeg, diters, self._last_dc > 0, step[3] > 0,
-                                                       o.degen_iters_max)
+            step = self._kkt(W, J, Sx, Ss, rhs_x, rhs_s, rhs_y, iin, mu, pert)
+            goto_resto = False
             if step is None and wd is not None:
                 # IPOPT: no direction inside the watchdog -> back to the watchdog point, and the line
                 # search continues along its stored direction
@@ -407,29 +555,11 @@ class InteriorPointSolver:
                 if in_resto:
                     status = 'kkt_failure'
                     break
-                if n_resto >= o.max_resto:
-                    status = 'restoration_failed'
-                    break
+                goto_resto = True
                 theta, _ = theta_of(g, s)
                 phi = phi_of(f, x, s, mu)
-                n_resto += 1
-                filt.append(((1 - o.gamma_theta) * theta, phi - o.gamma_phi * theta))
-                xr = self._restore(x, g, mu, theta, filt, theta_of, phi_of, lbg, ubg, xL, xU, dL, dU, iin)
-                if xr is None:
-                    status = 'restoration_failed'
-                    break
-                x = xr
-                f, g, gf, jv = self._eval(x)
-                s = self._push(g[iin], dL, dU)
-                a, b, c, d = slacks(x, s)
-                zl, zu = np.where(hxl, mu / a, 0), np.where(hxu, mu / b, 0)
-                vl, vu = np.where(hsl, mu / c, 0), np.where(hsu, mu / d, 0)
-                y = self._ls_multipliers(self._J(jv), gf, zl, zu, vl, vu, iin)
-                continue
-            if step != 'revert':
-                dx, ds, dy, delta_w, solve = step
-                if delta_w > 0:
-                    delta_w_last = delta_w
+            if step is not None and step != 'revert':
+                dx, ds, dy, solve = step
                 # ---- bound multiplier steps
                 dzl = np.where(hxl, mu / a - zl - zl / a * dx, 0)
                 dzu = np.where(hxu, mu / b - zu + zu / b * dx, 0)
@@ -443,20 +573,31 @@ class InteriorPointSolver:
                 phi = phi_of(f, x, s, mu)
                 gphi_d = gx @ dx + gs @ ds
             accepted = None
+            soft = None               # an accepted soft-restoration step: (x, s, y, zl, zu, vl, vu, f, g, gf, jv, S)
             skip_first = False
             tiny = False
-            if step != 'revert':
+            if not goto_resto and step != 'revert':
                 # ---- tiny step (IPOPT DetectTinyStep): taken in full, no line search
                 tiny = (wd is None and o.tiny_step_tol > 0 and
                         np.max(np.abs(dx) / (1.0 + np.abs(x)), initial=0) <= o.tiny_step_tol and
                         np.max(np.abs(ds) / (1.0 + np.abs(s)), initial=0) <= o.tiny_step_tol and
-                        np.max(np.abs(dy), initial=0) <= o.tiny_step_y_tol and np.abs(r).max(initial=0) <= 1e-4)
+                        np.max(np.abs(dy), initial=0) <= o.tiny_step_y_tol and theta <= 1e-4)
                 if tiny:
                     self.wd_stats['tiny_steps'] += 1
                     tiny_flag = True
                     xt, st = x + alpha_max * dx, s + alpha_max * ds
                     ft, gt, gft, jvt = self._eval(xt)
                     accepted = (alpha_max, xt, st, ft, gt, gft, jvt, True, dy)
+                elif in_soft:
+                    # ---- soft restoration phase: the damped primal-dual step while it reduces the
+                    # primal-dual error (at most max_soft_resto_iters in a row)
+                    soft_count += 1
+                    if soft_count <= o.max_soft_resto_iters:
+                        soft = self._soft_step(x, s, y, zl, zu, vl, vu, f, g, gf, jv, dx, ds, dy, dzl, dzu, dvl,
+                                               dvu, alpha_max, alpha_z, theta, phi, mu, filt, theta_max,
+                                               theta_of, phi_of, pd_error)
+                    if soft is None:
+                        goto_resto = True
                 elif wd is None and o.watchdog_shortened_iter_trigger > 0 and \
                         ws_short >= o.watchdog_shortened_iter_trigger:
                     # ---- start the watchdog at this iterate and direction
@@ -496,54 +637,98 @@ class InteriorPointSolver:
                 wd = None
                 skip_first = True
                 solve = None
-            # ---- filter line search
-            if gphi_d < 0 and theta <= theta_min:
-                amin = min(o.gamma_theta, o.gamma_phi * theta / -gphi_d,
-                           o.delta * theta ** o.s_theta / (-gphi_d) ** o.s_phi)
-            elif gphi_d < 0:
-                amin = min(o.gamma_theta, o.gamma_phi * theta / -gphi_d)
-            else:
-                amin = o.gamma_theta
-            alpha_min = o.alpha_min_frac * amin
-            alpha = alpha_max * (0.5 if skip_first else 1.0)
-            first = not skip_first
-            while accepted is None and alpha >= alpha_min:
-                xt, st = x + alpha * dx, s + alpha * ds
-                ft, gt, gft, jvt = self._eval(xt)
-                tht, rt = theta_of(gt, st)
-                pht = phi_of(ft, xt, st, mu)
-                ok, armijo_step = self._accept(theta, phi, gphi_d, alpha, tht, pht, filt, theta_max, theta_min)
-                if ok:
-                    accepted = (alpha, xt, st, ft, gt, gft, jvt, armijo_step, dy)
-                    break
-                if first and tht >= theta and solve is not None:
-                    # second-order corrections (IPOPT A-5.7 ... A-5.10)
-                    soc = self._soc(solve, rhs_x, rhs_s, x, s, alpha, r, rt, theta, phi, gphi_d, filt, theta_max,
-                                    theta_min, theta_of, phi_of, tau, a, b, c, d, hxl, hxu, hsl, hsu, mu)
-                    if soc is not None:
-                        accepted = soc
+            # ---- filter line search (not in the soft restoration phase, not on the way to restoration)
+            if accepted is None and soft is None and not goto_resto and not in_soft:
+                if gphi_d < 0 and theta <= theta_min:
+                    amin = min(o.gamma_theta, o.gamma_phi * theta / -gphi_d,
+                               o.delta * theta ** o.s_theta / (-gphi_d) ** o.s_phi)
+                elif gphi_d < 0:
+                    amin = min(o.gamma_theta, o.gamma_phi * theta / -gphi_d)
+                else:
+                    amin = o.gamma_theta
+                alpha_min = o.alpha_min_frac * amin
+                alpha = alpha_max * (0.5 if skip_first else 1.0)
+                first = not skip_first
+                while alpha > alpha_min:
+                    xt, st = x + alpha * dx, s + alpha * ds
+                    ft, gt, gft, jvt = self._eval(xt)
+                    tht, rt = theta_of(gt, st)
+                    pht = phi_of(ft, xt, st, mu)
+                    ok, armijo_step = self._accept(theta, phi, gphi_d, alpha, tht, pht, filt, theta_max, theta_min)
+                    if ok:
+                        accepted = (alpha, xt, st, ft, gt, gft, jvt, armijo_step, dy)
                         break
-                first = False
-                alpha *= 0.5
-            if accepted is None:
+                    if first and tht >= theta and solve is not None:
+                        # second-order corrections (IPOPT A-5.7 ... A-5.10)
+                        soc = self._soc(solve, rhs_x, rhs_s, x, s, alpha, r, rt, theta, phi, gphi_d, filt, theta_max,
+                                        theta_min, theta_of, phi_of, tau, a, b, c, d, hxl, hxu, hsl, hsu, mu)
+                        if soc is not None:
+                            accepted = soc
+                            break
+                    first = False
+                    alpha *= 0.5
+                if accepted is None and o.soft_resto_pderror_reduction_factor > 0:
+                    # ---- the line search failed: try the soft restoration phase first (the current
+                    # point is abandoned: its filter entry is added as before a restoration)
+                    filt.append(((1 - o.gamma_theta) * theta, phi - o.gamma_phi * theta))
+                    soft = self._soft_step(x, s, y, zl, zu, vl, vu, f, g, gf, jv, dx, ds, dy, dzl, dzu, dvl, dvu,
+                                           alpha_max, alpha_z, theta, phi, mu, filt, theta_max, theta_of, phi_of,
+                                           pd_error)
+                    if soft is not None:
+                        self.soft_stats['entered'] += 1
+                        if not soft[-1]:
+                            in_soft, soft_count = True, 0
+                if accepted is None and soft is None:
+                    goto_resto = True
+            if soft is not None:
+                # ---- a soft restoration step: primal and dual variables take the same step
+                x, s, y, zl, zu, vl, vu, f, g, gf, jv, satisfies = soft
+                self._last_step = 'S' if satisfies else 's'
+                self.soft_stats['steps'] += 1
+                if satisfies:                 # acceptable to the original filter: back to the regular search
+                    if in_soft:
+                        self.soft_stats['left'] += 1
+                    in_soft, soft_count = False, 0
+                    filt.append(((1 - o.gamma_theta) * theta, phi - o.gamma_phi * theta))
+                zl, zu, vl, vu = kappa_sigma(x, s, zl, zu, vl, vu, mu)
+                it += 1
+                continue
+            if goto_resto:
+                # ---- feasibility restoration (MinC_1NrmRestorationPhase)
                 if in_resto or n_resto >= o.max_resto:
                     status = 'restoration_failed'
                     break
                 n_resto += 1
+                self._last_step = 'R'
+                in_soft, soft_count = False, 0
                 filt.append(((1 - o.gamma_theta) * theta, phi - o.gamma_phi * theta))
-                xr = self._restore(x, g, mu, theta, filt, theta_of, phi_of, lbg, ubg, xL, xU, dL, dU, iin)
-                if xr is None:
+                rr = self._restore(x, s, zl, zu, vl, vu, g, mu, theta, phi, filt, theta_of, phi_of, lbg, ubg, it)
+                if rr is None:
                     status = 'restoration_failed'
                     break
-                x = xr
-                f, g, gf, jv = self._eval(x)
-                s = self._push(g[iin], dL, dU)
-                a, b, c, d = slacks(x, s)
-                zl, zu = np.where(hxl, mu / a, 0), np.where(hxu, mu / b, 0)
-                vl, vu = np.where(hsl, mu / c, 0), np.where(hsu, mu / d, 0)
-                y = self._ls_multipliers(self._J(jv), gf, zl, zu, vl, vu, iin)
+                xr, sr, k_r, hit_max = rr
+                it += k_r + 1
+                if hit_max:                   # the restoration ran into max_iter
+                    x = xr
+                    f, g, gf, jv = self._eval(x)
+                    s = sr
+                    status = 'max_iter'
+                    break
+                f, g, gf, jv = self._eval(xr)
+                zl, zu, vl, vu = self._post_resto_bound_mults(x, s, xr, sr, zl, zu, vl, vu, mu, tau, slacks,
+                                                              hxl, hxu, hsl, hsu)
+                x, s = xr, sr
+                # equality multipliers (MinC_1NrmRestorationPhase via least_square_mults with
+                # constr_mult_reset_threshold as the bound; IPOPT's option text: the least-squares estimates
+                # "should be ignored" above it): 0, the default, gives y = 0; a positive threshold the
+                # estimate, or 0 above the threshold
+                y = np.zeros(m)
+                if o.constr_mult_reset_threshold > 0:
+                    y = self._ls_multipliers(self._J(jv), gf, zl, zu, vl, vu, iin, o.constr_mult_reset_threshold)
+                zl, zu, vl, vu = kappa_sigma(x, s, zl, zu, vl, vu, mu)
                 continue
             alpha, xt, st, ft, gt, gft, jvt, armijo_step, dyacc = accepted
+            self._last_step = f'a={alpha:.1e}/{alpha_max:.1e}{"" if armijo_step else "h"}'
             if not armijo_step:
                 filt.append(((1 - o.gamma_theta) * theta, phi - o.gamma_phi * theta))
             if wd is None and not tiny:
@@ -555,14 +740,10 @@ class InteriorPointSolver:
             y = y + alpha * dyacc
             zl, zu = zl + alpha_z * dzl, zu + alpha_z * dzu
             vl, vu = vl + alpha_z * dvl, vu + alpha_z * dvu
-            # safeguard: keep bound multipliers within kappa_sigma of mu / slack
-            a, b, c, d = slacks(x, s)
-            ks = o.kappa_sigma
-            zl = np.where(hxl, np.clip(zl, mu / (ks * a), ks * mu / a), 0)
-            zu = np.where(hxu, np.clip(zu, mu / (ks * b), ks * mu / b), 0)
-            vl = np.where(hsl, np.clip(vl, mu / (ks * c), ks * mu / c), 0)
-            vu = np.where(hsu, np.clip(vu, mu / (ks * d), ks * mu / d), 0)
+            zl, zu, vl, vu = kappa_sigma(x, s, zl, zu, vl, vu, mu)
+            it += 1
 
+        self.final = dict(x=x, s=s, y=y, zl=zl, zu=zu, vl=vl, vu=vu, mu=mu)
         if o.honor_original_bounds:
             x = np.clip(x, np.where(self.lbx0 > -INF, self.lbx0, -np.inf), np.where(self.ubx0 < INF, self.ubx0, np.inf))
         fu, gu, _, _ = self.ev.eval(x)
@@ -572,48 +753,114 @@ class InteriorPointSolver:
         stats = dict(self.evals)
         stats['restorations'] = n_resto
         stats['watchdog'] = dict(self.wd_stats)
+        stats['soft_resto'] = dict(self.soft_stats)
+        stats['degenerate'] = (pert.hdeg, pert.jdeg)
         return IPMResult(x=x, f=float(fu), g=gu, lam_g=lam_g, lam_x=lam_x, status=status, success=success,
                          iters=it, stats=stats, history=history)
 
+    # ------------------------------------------------------------------ soft restoration
+    def _soft_step(self, x, s, y, zl, zu, vl, vu, f, g, gf, jv, dx, ds, dy, dzl, dzu, dvl, dvu, alpha_max,
+                   alpha_z, theta, phi, mu, filt, theta_max, theta_of, phi_of, pd_error):
+        '''
+        BacktrackingLineSearch::TrySoftRestoStep: primal and dual variables take the step
+        min(alpha_primal_max, alpha_dual_max). Accepted if the trial point is acceptable to the
+        original criterion (filter and sufficient decrease, alpha test 0) or if it reduces the
+        primal-dual system error by soft_resto_pderror_reduction_factor. Returns the trial
+        (x, s, y, zl, zu, vl, vu, f, g, gf, jv, satisfies_original_criterion) or None.
+        '''
+        o = self.o
+        al = min(alpha_max, alpha_z)
+        xt, st, yt = x + al * dx, s + al * ds, y + al * dy
+        zlt, zut, vlt, vut = zl + al * dzl, zu + al * dzu, vl + al * dvl, vu + al * dvu
+        ft, gt, gft, jvt = self._eval(xt)
+        tht, _ = theta_of(gt, st)
+        pht = phi_of(ft, xt, st, mu)
+        ok, _ = self._accept(theta, phi, 0.0, 0.0, tht, pht, filt, theta_max, -1.0)
+        if ok:
+            return (xt, st, yt, zlt, zut, vlt, vut, ft, gt, gft, jvt, True)
+        e_cur = pd_error(gf, self._J(jv), g, x, s, y, zl, zu, vl, vu, mu)
+        e_tr = pd_error(gft, self._J(jvt), gt, xt, st, yt, zlt, zut, vlt, vut, mu)
+        if e_tr <= o.soft_resto_pderror_reduction_factor * e_cur:
+            return (xt, st, yt, zlt, zut, vlt, vut, ft, gt, gft, jvt, False)
+        return None
+
     # ------------------------------------------------------------------ feasibility restoration
-    def _restore(self, x, g, mu, theta_start, filt, theta_of, phi_of, lbg, ubg, xL, xU, dL, dU, iin):
-        ''' IPOPT's restoration phase on the scaled problem; returns the new x or None '''
+    @staticmethod
+    def _post_resto_bound_mults(x, s, xr, sr, zl, zu, vl, vu, mu, tau, slacks, hxl, hxu, hsl, hsu):
+        '''
+        MinC_1NrmRestorationPhase after a successful phase: the whole primal move is taken as one
+        primal-dual Newton step of the bound multipliers (ComputeBoundMultiplierStep:
+        dz = mu / s_c - z - z (s_t - s_c) / s_c), damped by the fraction to the boundary; all of
+        them are reset to 1 when the largest exceeds bound_mult_reset_threshold
+        '''
+        cur = slacks(x, s)
+        tri = slacks(xr, sr)
+        zs = (zl, zu, vl, vu)
+        hs = (hxl, hxu, hsl, hsu)
+        dz = [np.where(h, ((sc - st) * z + mu) / sc - z, 0.0) for z, sc, st, h in zip(zs, cur, tri, hs)]
+        adual = min(InteriorPointSolver._ftb(z, d_, h, tau) for z, d_, h in zip(zs, dz, hs))
+        new = [z + adual * d_ for z, d_ in zip(zs, dz)]
+        if max(np.abs(z).max(initial=0) for z in new) > 1000.0:
+            new = [np.where(h, 1.0, 0.0) for h in hs]
+        return tuple(new)
+
+    def _restore(self, x, s, zl, zu, vl, vu, g, mu, theta_start, phi_start, filt, theta_of, phi_of, lbg, ubg,
+                 it0):
+        '''
+        IPOPT's restoration phase on the scaled problem (MinC_1NrmRestorationPhase with
+        RestoIterateInitializer and RestoConvergenceCheck). Returns (x, s, restoration iterations,
+        ran into max_iter) or None when the phase fails.
+        '''
         o = self.o
         n, m = self.n, self.m
+        c_rhs, dL, dU, xL, xU, ieq, iin = self.geom
         rho = o.resto_penalty
-        # violation of every (scaled) row: c_i = g_i - proj(g_i, [lbg_i, ubg_i])
-        viol = g - np.clip(g, lbg, ubg)
-        mu_r = max(mu, np.abs(viol).max(initial=0))
-        a_ = (mu_r - rho * viol) / (2 * rho)
-        nn = a_ + np.sqrt(a_ * a_ + mu_r * viol / (2 * rho))
-        pp = viol + nn
-        rev = _RestorationEvaluator(self.ev, self.sg, x, np.sqrt(mu), rho, self.blocks)
+        # residuals of the current iterate: c(x) and d(x) - s with the current slacks
+        r = np.empty(m)
+        r[ieq] = g[ieq] - c_rhs
+        r[iin] = g[iin] - s
+        mu_r = max(mu, np.abs(r).max(initial=0))
+        a_ = (mu_r - rho * r) / (2 * rho)
+        nn = a_ + np.sqrt(a_ * a_ + mu_r * r / (2 * rho))
+        pp = r + nn
+        rev = _RestorationEvaluator(self.ev, self.sg, x, np.sqrt(mu_r), rho, self.blocks)
         xr0 = np.concatenate([x, pp, nn])
         lbx = np.concatenate([self.lbx0, np.zeros(2 * m)])
         ubx = np.concatenate([self.ubx0, np.full(2 * m, np.inf)])
-        ro = IPMOptions(**{**o.__dict__, 'nlp_scaling': False, 'verbose': o.verbose, 'max_iter': 3000})
+        remaining = o.max_iter - (it0 + 1)
+        ro = IPMOptions(**{**o.__dict__, 'nlp_scaling': False, 'verbose': o.verbose, 'max_iter': max(remaining, 0)})
         sub = InteriorPointSolver(rev, lbx, ubx, lbg, ubg, ro)
-        s_of = lambda gx: self._push(gx[iin], dL, dU)      # noqa: E731
 
-        def accept(xr):
+        def accept(xr, sr):
+            # RestoConvergenceCheck: the original problem at the restoration iterate (x, s)
             xo = xr[:n]
             f2, g2, _, _ = self._eval(xo)
-            s2 = s_of(g2)
-            th, _ = theta_of(g2, s2)
+            th, _ = theta_of(g2, sr)
             if th > o.resto_kappa * theta_start:
                 return False
-            ph = phi_of(f2, xo, s2, mu)
+            ph = phi_of(f2, xo, sr, mu)
             for tf, pf in filt:
                 if th >= tf and ph >= pf:
                     return False
             return True
 
-        res = sub.solve(xr0, mu0=mu_r, stop_check=accept, in_resto=True)
+        # multipliers of the original bounds: the current ones, at most rho; of p and n: mu_R / p, mu_R / n
+        init = dict(s=s, accept=accept, theta_max_fact=o.resto_theta_max_fact,
+                    zl=np.concatenate([np.minimum(zl, rho), mu_r / pp, mu_r / nn]),
+                    zu=np.concatenate([np.minimum(zu, rho), np.zeros(2 * m)]),
+                    vl=np.minimum(vl, rho), vu=np.minimum(vu, rho))
+        with threadpool_limits(limits=1, user_api='blas'):
+            res = sub._solve(xr0, mu_r, None, True, resto_init=init)
         for k, v in sub.evals.items():
             self.evals[k] = self.evals.get(k, 0) + v
+        if res.status == 'max_iter':
+            fx = sub.final
+            return np.clip(fx['x'][:n], xL, xU), fx['s'], res.iters, True
         if res.status != 'stopped':
             return None
-        return np.clip(res.x[:n], np.where(np.isfinite(xL), xL, -np.inf), np.where(np.isfinite(xU), xU, np.inf))
+        fx = sub.final
+        return np.clip(fx['x'][:n], np.where(np.isfinite(xL), xL, -np.inf),
+                       np.where(np.isfinite(xU), xU, np.inf)), fx['s'], res.iters, False
 
     # ------------------------------------------------------------------ pieces
     @staticmethod
@@ -624,7 +871,7 @@ class InteriorPointSolver:
             return 1.0
         return float(min(1.0, (-tau * v[sel] / dv[sel]).min()))
 
-    def _ls_multipliers(self, J, gf, zl, zu, vl, vu, iin):
+    def _ls_multipliers(self, J, gf, zl, zu, vl, vu, iin, ymax=None):
         ''' least-squares y of the dual equations (IPOPT constr_mult_init):
             [I 0 J^T; 0 I -E^T; J -E 0] [w_x; w_s; y] = -[gf - z_L + z_U; -v_L + v_U; 0]
         with w_s eliminated: [I J^T; J -E E^T] [w_x; y] = [-(gf - z_L + z_U); -E (v_U - v_L)] '''
@@ -638,7 +885,8 @@ class InteriorPointSolver:
         if solve_k is None or (inertia is not None and inertia[2] > 0):
             return np.zeros(m)
         y = solve_k(np.concatenate([-(gf - zl + zu), rs]))[n:]
-        if not np.all(np.isfinite(y)) or np.abs(y).max(initial=0) > self.o.constr_mult_init_max:
+        ymax = self.o.constr_mult_init_max if ymax is None else ymax
+        if not np.all(np.isfinite(y)) or np.abs(y).max(initial=0) > ymax:
             return np.zeros(m)
         return y
 
@@ -672,78 +920,69 @@ class InteriorPointSolver:
             return x
         return solve, inertia
 
-    def _kkt(self, W, J, Sx, Ss, rhs_x, rhs_s, rhs_y, iin, mu, delta_w_last, start_dw=False, start_dc=False):
+    def _kkt(self, W, J, Sx, Ss, rhs_x, rhs_s, rhs_y, iin, mu, pert: PerturbationHandler):
         '''
         Solve the primal-dual system with the slack block eliminated,
             [W + Sx + dw I   J^T ] [dx]   [rhs_x                 ]
             [J              -D   ] [dy] = [rhs_y + rhs_s / (Ss+dw)]   (slack rows of D: 1/(Ss+dw) + dc)
-        with IPOPT's inertia correction (IC-1 ... IC-6): the inertia must be (n, m, 0).
-        Without inertia (sparse LU fallback) the curvature test of Chiang & Zavala decides.
-        Returns (dx, ds, dy, delta_w, solve) or None when delta_w exceeds its maximum (delta_c in
-        self._last_dc). start_dw / start_dc: the Hessian / Jacobian is structurally degenerate, the
-        first attempt is already perturbed.
+        with IPOPT's inertia correction (PDFullSpaceSolver::SolveOnce + PDPerturbationHandler): the
+        inertia must be (n, m, 0); a zero eigenvalue, too few negative eigenvalues or an
+        unrefinable solve count as a singular matrix, too many negative eigenvalues as wrong
+        inertia. Without inertia (sparse LU fallback) the curvature test of Chiang & Zavala
+        decides. Returns (dx, ds, dy, solve) or None when no perturbation is left.
         '''
-        o = self.o
         n, m = self.n, self.m
-        delta_c = o.delta_c_base * mu ** o.kappa_c if start_dc else 0.0
-        delta_w = 0.0
-        first = True
-        if start_dw:
-            delta_w = o.delta_w_0 if delta_w_last == 0 else max(o.delta_w_min, o.kappa_w_minus * delta_w_last)
-            first = False
-        self._last_dc = delta_c
-        while True:
+        d = pert.consider_new_system(mu)
+        while d is not None:
+            delta_w, delta_c = d
             Ds_tot = Ss + delta_w
             D = np.full(m, delta_c)
             D[iin] += 1.0 / Ds_tot
             H = W + sp.diags(Sx + delta_w)
             K = sp.bmat([[H, J.T], [J, -sp.diags(D)]], format='csr')
             solve_k, inertia = self._factor(K)
-            ok = False
             if inertia is not None:
-                ok = inertia[0] == n and inertia[1] == m and inertia[2] == 0
-                singular = inertia[2] > 0
+                singular = inertia[2] > 0 or inertia[1] < m
+                wrong = not singular and inertia[1] > m
             else:
-                singular = solve_k is None
-            if not singular and (ok or inertia is None):
+                singular, wrong = solve_k is None, False
+            if not singular and not wrong:
                 r_y = rhs_y.copy()
                 r_y[iin] += rhs_s / Ds_tot
                 sol = solve_k(np.concatenate([rhs_x, r_y]))
-                if np.all(np.isfinite(sol)) and self._last_solve_ok:
+                if not (np.all(np.isfinite(sol)) and self._last_solve_ok):
+                    singular = True
+                else:
                     dx, dy = sol[:n], sol[n:]
                     ds = (rhs_s + dy[iin]) / Ds_tot
                     if inertia is None:
                         curv = dx @ (H @ dx) + ds @ (Ds_tot * ds)
-                        ok = curv >= 1e-12 * (dx @ dx + ds @ ds) or (dx @ dx + ds @ ds) == 0
-                    if ok:
+                        wrong = not (curv >= 1e-12 * (dx @ dx + ds @ ds) or (dx @ dx + ds @ ds) == 0)
+                    if not wrong:
                         def solve(rx, rs, ry, solve_k=solve_k, Ds_tot=Ds_tot):
                             ry2 = ry.copy()
                             ry2[iin] += rs / Ds_tot
                             z = solve_k(np.concatenate([rx, ry2]))
                             return z[:n], (rs + z[n:][iin]) / Ds_tot, z[n:]
-                        return dx, ds, dy, delta_w, solve
-                else:
-                    singular = True
-            if first:
-                first = False
-                if singular:
-                    delta_c = o.delta_c_base * mu ** o.kappa_c
-                delta_w = o.delta_w_0 if delta_w_last == 0 else max(o.delta_w_min, o.kappa_w_minus * delta_w_last)
-            else:
-                delta_w *= o.kappa_w_plus_bar if delta_w_last == 0 else o.kappa_w_plus
-            self._last_dc = delta_c
-            if delta_w > o.delta_w_max:
-                return None
+                        return dx, ds, dy, solve
+            d = pert.perturb_for_singularity(mu) if singular else pert.perturb_for_wrong_inertia(mu)
+        return None
 
     def _accept(self, theta, phi, gphi_d, alpha, tht, pht, filt, theta_max, theta_min):
-        ''' filter acceptance; returns (accepted, is_armijo_step) '''
+        ''' filter acceptance (FilterLSAcceptor::CheckAcceptabilityOfTrialPoint); returns
+        (accepted, is_armijo_step) '''
         o = self.o
         if tht > theta_max:
             return False, False
+        if pht > phi:
+            # obj_max_inc: the barrier objective may not grow by more than 10^5 of its magnitude
+            base = np.log10(abs(phi)) if abs(phi) > 10.0 else 1.0
+            if np.log10(pht - phi) > o.obj_max_inc + base:
+                return False, False
         for tf, pf in filt:
             if tht >= tf and pht >= pf:
                 return False, False
-        switching = gphi_d < 0 and alpha * (-gphi_d) ** o.s_phi > o.delta * theta ** o.s_theta
+        switching = alpha > 0 and gphi_d < 0 and alpha * (-gphi_d) ** o.s_phi > o.delta * theta ** o.s_theta
         if theta <= theta_min and switching:
             return pht <= phi + o.eta_phi * alpha * gphi_d, True
         ok = tht <= (1 - o.gamma_theta) * theta or pht <= phi - o.gamma_phi * theta
@@ -779,8 +1018,13 @@ class _RestorationEvaluator:
     Restoration problem over (x, p, n) on the scaled rows of the original evaluator:
         min  rho sum(p + n) + zeta/2 |D_R (x - x_r)|^2   s.t.  sg * g(x) - p + n  (original bounds)
     Jacobian rows [sg_i J_i, -1 (p_i), +1 (n_i)]; Hessian = original constraint Hessian (sigma = 0)
-    plus zeta D_R^2 on the x diagonal.
+    plus zeta D_R^2 on the x diagonal. zeta = sqrt(mu) follows the restoration's own barrier
+    parameter (RestoIpoptNLP: Eta(mu) = resto_proximity_weight mu^0.5): set_mu() on every change.
     '''
+
+    def set_mu(self, mu):
+        self.zeta = float(np.sqrt(mu))
+
 
     def __init__(self, ev, sg, x_ref, zeta, rho, blocks):
         n, m = ev.nw, ev.ng

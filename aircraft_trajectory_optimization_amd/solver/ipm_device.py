@@ -162,9 +162,9 @@ class DeviceIPMKernels:
         F = F.contiguous()
         nf = nf.to(torch.int64).contiguous()
         pend, first = pend.to(torch.bool).contiguous(), first.to(torch.bool).contiguous()
-        key = (o.s_phi, o.s_theta, o.delta, o.eta_phi, o.gamma_theta, o.gamma_phi)
+        key = (o.s_phi, o.s_theta, o.delta, o.eta_phi, o.gamma_theta, o.gamma_phi, o.obj_max_inc)
         prm = self._prm.get(key)
-        if prm is None:     # host array: the six parameters are read on the host and passed by value
+        if prm is None:     # host array: the seven parameters are read on the host and passed by value
             prm = self._prm[key] = np.array(key, dtype=np.float64)
         out = torch.empty((3, W), dtype=torch.bool, device=self.device)
         th, ph, gd, al, tt, pt, tmax, tmin = cols

@@ -96,7 +96,7 @@ int ato_ipm_multipliers(const ato_ipm_dims* d, const ato_ipm_bounds* bd, const d
  * derivative; alpha: trial step; tht, pht: measures of the trial point; F [W][fmax][2] the
  * filter entries (theta, phi) of every column, nf [W] (int64) how many are valid; theta_max,
  * theta_min [W]; pend, first [W] (bytes 0/1): columns still searching, first trial of the
- * search. prm = HOST array {s_phi, s_theta, delta, eta_phi, gamma_theta, gamma_phi} (read on the
+ * search. prm = HOST array {s_phi, s_theta, delta, eta_phi, gamma_theta, gamma_phi, obj_max_inc} (read on the
  * host and passed to the kernel by value; every other pointer is a device array). Outputs (bytes 0/1,
  * [W]): ok = pend and accepted, arm = ok and the Armijo (f-type) case, soc = pend, not
  * accepted, first trial and tht >= theta (a second-order correction is tried). */

@@ -113,9 +113,9 @@ def test_kkt_failure_falls_back_to_restoration():
         out = orig_step(*args, **kw)
         calls['n'] += 1
         if calls['n'] == 3:
-            ok = out[4].clone()
+            ok = out[3].clone()
             ok[1] = False
-            out = out[:4] + (ok,) + out[5:]
+            out = out[:3] + (ok,) + out[4:]
         return out
 
     bs._kkt_step = failing_step

@@ -47,6 +47,47 @@ def test_watchdog_starts_succeeds_reverts_and_converges():
     assert np.abs(rb.x[:, 0].numpy() - r40.x).max() <= 1e-8 * max(1.0, np.abs(r40.x).max())
 
 
+def test_kkt_failure_inside_the_watchdog_reverts_in_both_solvers():
+    ''' no search direction while the watchdog is active: both solvers return to the watchdog point
+    and backtrack along its stored direction with an ordinary line search (the batched solver used
+    to keep such a column among the watchdog trials) -- same iterates and statistics '''
+    spec = product_spec(track='fig8', N=6, K=2)
+    ev = HostEvaluator(spec)
+    W, L, U = seeded_instances(spec, [4])
+    o = IPMOptions(max_iter=40)
+    hs = InteriorPointSolver(ev, L[0], U[0], ev.lbg, ev.ubg, o)
+    calls = {'n': 0, 'failed': None}
+    orig = hs._kkt
+
+    def kkt(*a, **kw):
+        calls['n'] += 1
+        wd = hs.wd_stats
+        out = orig(*a, **kw)                         # (the perturbation handler steps as in the batched run)
+        if calls['failed'] is None and wd['started'] > wd['succeeded'] + wd['reverted']:
+            calls['failed'] = calls['n']            # the first direction computed inside a watchdog
+            return None
+        return out
+    hs._kkt = kkt
+    ref = hs.solve(W[0])
+    assert calls['failed'] is not None and ref.stats['watchdog']['reverted'] >= 1
+    bev = HostBatchEvaluator(spec, 1)
+    bs = BatchedInteriorPoint(bev, HostBlockKKT(bev), L, U, o)
+    bcalls = {'n': 0}
+    borig = bs._kkt_step
+
+    def step(*a, **kw):
+        out = borig(*a, **kw)
+        bcalls['n'] += 1
+        if bcalls['n'] == calls['failed']:
+            out = out[:3] + (torch.zeros_like(out[3]),) + out[4:]
+        return out
+    bs._kkt_step = step
+    rb = bs.solve(W)
+    assert rb.status[0] == ref.status and int(rb.iters[0]) == ref.iters
+    assert rb.stats['watchdog'] == ref.stats['watchdog']
+    assert np.abs(rb.x[:, 0].numpy() - ref.x).max() <= 1e-8 * max(1.0, np.abs(ref.x).max())
+
+
 class _Toy:
     ''' min (x0 - 0.3)^2 + (x1 - 0.3)^2  s.t.  x0 + x1 = 1,  0 <= x <= 1  (solution 0.5, 0.5), as the
     single-instance evaluator and as a batched CPU evaluator of `batch` identical instances '''

@@ -31,7 +31,16 @@ run() {  # run <name> <seconds> <cmd...>
 
 for s in $STEPS; do
     case $s in
-        tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider ${GPU_TESTS:-} ;;
+        tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --capture=sys --timeout 300 --timeout-method thread -p no:cacheprovider ${GPU_TESTS:-} ;;
+        ab)    run ab_new 900 python -u tools/solver_ab.py --what fig8,config3 --tag new --out "$OUT/ab_new.json"
+               PYTHONPATH=$PWD/tools/r04_baseline run ab_r04 900 python -u tools/solver_ab.py --what fig8,config3 --tag r04 --out "$OUT/ab_r04.json" ;;
+        abl)   i=0
+               for o in ${AB_ARMS:-'{}' '{"soft_resto_pderror_reduction_factor": 0}' '{"constr_mult_reset_threshold": 1000}' \
+                        '{"soft_resto_pderror_reduction_factor": 0, "constr_mult_reset_threshold": 1000}'}; do
+                   i=$((i+1))
+                   ATO_AB_OPTS="$o" run abl_$i 900 python -u tools/solver_ab.py --what ${AB_WHAT:-fig8,fig8k4,config3} --tag "$o" --out "$OUT/abl_$i.json"
+               done ;;
+        abnew) run ab_new 900 python -u tools/solver_ab.py --what ${AB_WHAT:-fig8,config3} --tag new --out "$OUT/ab_new.json" ;;
         smoke) run smoke 300 python -c 'import __graft_entry__ as g; g.smoke()' ;;
         bench) run bench 900 python bench.py --steps 50 --warmup 10 ;;
         bench32) run bench_f32 300 python bench.py --steps 50 --warmup 10 --dtype f32 --no-cpu-baseline --no-solve ;;
