@@ -184,6 +184,34 @@ int ato_sphere_rows(const ato_handle* h, int32_t* rows) {
     return ATO_OK;
 }
 
+int ato_gradf_mode(ato_handle* h, int32_t sparse) {
+    if (!h) return fail(ATO_ERR_ARG, "null handle");
+    for (ato::ProbD* p : {&h->pd, &h->pd_lf}) p->gf_sparse = sparse ? 1 : 0;
+    return ATO_OK;
+}
+
+int ato_gradf_sparsity(const ato_handle* h, int32_t* nnz, int32_t* idx) {
+    if (!h || !nnz) return fail(ATO_ERR_ARG, "null argument");
+    // the entries the gradient passes write with a value (Layout units: interval n writes h_n, node
+    // (n, k) its inputs u and input rates du); everything else is a structural zero of grad f
+    const ato::ProbD& p = h->L.p;
+    const int N = p.N, NZ = p.NZ, NU = p.NU, NV = p.NV;
+    const int per_interval = p.K1;          // (RK4: K = 0, one node per interval)
+    int32_t c = 0;
+    for (int n = 0; n < N; ++n) {
+        if (idx) idx[c] = n;
+        ++c;
+    }
+    for (int n = 0; n < N; ++n)
+        for (int k = 0; k < per_interval; ++k)
+            for (int i = 0; i < 2 * NU; ++i) {
+                if (idx) idx[c] = N + (n * per_interval + k) * NV + NZ + i;
+                ++c;
+            }
+    *nnz = c;
+    return ATO_OK;
+}
+
 int ato_bounds(const ato_handle* h, double* lbg, double* ubg) {
     if (!h) return fail(ATO_ERR_ARG, "null handle");
     for (size_t i = 0; i < h->L.lbg.size(); ++i) {
@@ -347,7 +375,8 @@ extern "C" int ato_hess_eval(ato_handle* h, int32_t batch, int32_t layout, const
                           mk ? h->d_amask : nullptr, h->HL.mask_words,
                           h->HL.take_off.data(), h->HL.n_colors, h->HL.nnz()};
     hipError_t e = hipSuccess;
-    const ato::ProbD& p = batch <= h->lf_max_batch ? h->pd_lf : h->pd;   // unit order as in ato_eval
+    ato::ProbD p = batch <= h->lf_max_batch ? h->pd_lf : h->pd;   // unit order as in ato_eval
+    p.gf_sparse = 0;    // the seeded passes' grad f tangents fill a scratch buffer: every entry is written
     ato::with_model(p, [&]<class M>() {
         e = ato::launch_hess<M>(p, hd, batch, layout, w, lam, sigma, hess, h->d_dJ, h->d_dgf,
                                 (hipStream_t)stream);

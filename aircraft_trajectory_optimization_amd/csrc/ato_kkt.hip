@@ -50,6 +50,7 @@ struct ato_kkt {
     int32_t* d_forder = nullptr;     // [F] fronts of every level grouped by kernel class (factor launches)
     int32_t* d_n_sad = nullptr;      // [F] saddle fronts: nS, else 0 (NULL: the plan has none)
     int32_t* d_sad_txy = nullptr;    // [F][2] saddle fronts: (tx, ty)
+    double sad_tau = 0.0;            // saddle fallback on the barrier diagonal (Plan::sad_tau; ATO_KKT_SADDLE_TAU)
     // cls: kernel class; saddle segments (cls SADDLE_CLS): nsm = the k_front_saddle variant, lds its
     // shared-memory bytes, cls2 the Bunch-Kaufman class of the fallback launch
     struct Seg { int start, count, cls, nsm = 0, cls2 = 0; size_t lds = 0; };
@@ -141,6 +142,10 @@ struct Plan {
     const int2* sad_txy;          // [F] saddle fronts: trailing rows [0, tx) coupled to X, [T - ty, T) to Y
     long long l_size, cb_size;
     int sc_size;
+    // saddle fronts fall back to Bunch-Kaufman when max |H_XX diagonal| > sad_tau max|J_YX|^2 (0: never):
+    // G = -E^T H E carries the barrier diagonal (up to 1e10 near active bounds) through J^-1, where
+    // Bunch-Kaufman would take those entries first as 1 x 1 pivots
+    double sad_tau;
 };
 
 struct Vals {
@@ -1095,7 +1100,7 @@ __device__ __forceinline__ void sad_mfma(int M, int N, int K, FA a, FB b, FC c, 
 
 struct SadLds {      // shared-memory carve of one saddle front (runtime sizes)
     double *E, *H, *Bx, *By, *col, *dv, *mx, *prow;
-    int *piv, *pp, *flag;
+    int *piv, *pp, *flag, *hkey;
     int ldn;
 };
 
@@ -1115,12 +1120,13 @@ __device__ __forceinline__ SadLds sad_lds(double* smem, int nS, int tx, int ty) 
     L.piv = reinterpret_cast<int*>(L.prow + 64);     // [nS] pivot row of every step
     L.pp = L.piv + nS;                           // [2]
     L.flag = L.pp + 2;
+    L.hkey = L.flag + 1;                         // max |H diagonal| (float bits)
     return L;
 }
 
 inline size_t sad_lds_bytes(int nS, int tx, int ty) {
     const size_t d = (size_t)(2 * nS + tx + ty) * (nS + 1) + 128 + 2 + SAD_NW + 64;
-    return d * sizeof(double) + sizeof(int) * (nS + 3);
+    return d * sizeof(double) + sizeof(int) * (nS + 4);
 }
 
 template <int NSM>
@@ -1146,7 +1152,10 @@ __global__ __launch_bounds__(SAD_NT) void k_front_saddle(Plan P, Vals V, int f0,
 
     // ---- assembly: J (Y x X) into E, H (X x X), K_TX, K_TY; a Y diagonal -> fallback
     for (int i = tid; i < (2 * nS + tx + txy.y) * ldn; i += SAD_NT) L.E[i] = 0.0;
-    if (tid == 0) *L.flag = 0;
+    if (tid == 0) {
+        *L.flag = 0;
+        *L.hkey = 0;
+    }
     __syncthreads();
     {
         const int e0 = P.ent_ptr[f * MAXT], e1 = P.ent_ptr[(f + 1) * MAXT];
@@ -1158,6 +1167,7 @@ __global__ __launch_bounds__(SAD_NT) void k_front_saddle(Plan P, Vals V, int f0,
             if (pa < nS) {
                 L.H[pa * ldn + pb] = v;
                 L.H[pb * ldn + pa] = v;
+                if (pa == pb) atomicMax(reinterpret_cast<unsigned*>(L.hkey), __float_as_uint((float)fabs(v)));
             } else if (pa < n2) {
                 if (pb < nS) L.E[(pa - nS) * ldn + pb] = v;
                 else if (v != 0.0) *L.flag = 1;
@@ -1188,6 +1198,13 @@ __global__ __launch_bounds__(SAD_NT) void k_front_saddle(Plan P, Vals V, int f0,
     double mx = 0.0;
 #pragma unroll
     for (int w = 0; w < SAD_NW; ++w) mx = fmax(mx, L.mx[w]);
+    // a nonzero Y diagonal, or a barrier diagonal too large for the structured elimination: fall back
+    // before the Gauss-Jordan sweep (uniform: every thread reads the same shared values)
+    if (*L.flag || (P.sad_tau > 0.0 && (double)__uint_as_float(*reinterpret_cast<unsigned*>(L.hkey)) >
+                                          P.sad_tau * mx * mx)) {
+        if (tid == 0) sinfo[(long long)b * P.F + f] = make_int2(SAD_FALLBACK, 0);
+        return;
+    }
     bool used = false;
     int mystep = -1;
     for (int k = 0; k < nS; ++k) {
@@ -1949,6 +1966,7 @@ Plan make_plan(const ato_kkt* h) {
     P.l_size = h->l_size;
     P.cb_size = h->cb_size;
     P.sc_size = h->sc_size;
+    P.sad_tau = h->sad_tau;
     return P;
 }
 
@@ -2059,6 +2077,7 @@ static int kkt_create_impl(const ato_kkt_plan_desc* d, ato_kkt** out) {
     // (ATO_KKT_SPLIT=0: one launch per level at the level's tile count; ATO_KKT_S16=0: no
     // 16-wide-tile class), each group in plan order
     {
+        if (const char* e_tau = getenv("ATO_KKT_SADDLE_TAU")) h->sad_tau = atof(e_tau);
         const char* e_split = getenv("ATO_KKT_SPLIT");
         const char* e_s16 = getenv("ATO_KKT_S16");
         const bool split = !(e_split && e_split[0] == '0');

@@ -231,13 +231,15 @@ ATO_HD void run_unit(const ProbD& p, int kind, int n, int k, const W& w, S& s, c
                 stage_cost<M, T, KS>(p, n, k, w, gu, gdu);
                 const T hB = w(n) * T(p.Bq[k]);
                 const long base = c.node(n, k);
+                if (!p.gf_sparse) {        // structural zeros: written only in the dense mode
 #pragma unroll
-                for (int i = 0; i < NZ; ++i) go.put_gf(base + i, T(0));
+                    for (int i = 0; i < NZ; ++i) go.put_gf(base + i, T(0));
+                }
 #pragma unroll
                 for (int i = 0; i < NU; ++i) go.put_gf(base + NZ + i, hB * gu[i]);
 #pragma unroll
                 for (int i = 0; i < NU; ++i) go.put_gf(base + NZ + NU + i, hB * gdu[i]);
-                if (p.cpc_m > 0) {      // the progress variables are not in the cost
+                if (p.cpc_m > 0 && !p.gf_sparse) {      // the progress variables are not in the cost
                     const long cb = p.cpc_off + 3L * p.cpc_m * ((long)n * K1S(p) + k);
                     for (int i = 0; i < 3 * p.cpc_m; ++i) go.put_gf(cb + i, T(0));
                 }

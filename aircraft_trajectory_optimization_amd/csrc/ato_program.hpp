@@ -90,6 +90,9 @@ struct ProbD {
     // kernel argument an indexed array would be copied into registers)
     int32_t cpc_m, cpc_off;
     const double* cpc_wp;
+    // 1: the gradient passes write only the structural nonzeros of grad f (h and the inputs; the
+    // caller zero-fills the buffer once, ato_gradf_mode); 0: every entry (the states' zeros too)
+    int32_t gf_sparse;
 };
 
 // nodes per interval: compile-time KS (specialised kernels for common K) or runtime p.K1

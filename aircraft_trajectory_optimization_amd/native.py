@@ -111,7 +111,7 @@ EXPORTED_SYMBOLS = ('ato_create', 'ato_destroy', 'ato_sizes', 'ato_sparsity', 'a
                     'ato_timing', 'ato_timing_read', 'ato_timing_stride', 'ato_last_error', 'ato_version',
                     'ato_kkt_create', 'ato_kkt_destroy', 'ato_kkt_reserve', 'ato_kkt_factor', 'ato_kkt_solve',
                     'ato_kkt_residual', 'ato_kkt_residual_list', 'ato_set_instance_spheres',
-                    'ato_sphere_rows') + IPM_SYMBOLS
+                    'ato_sphere_rows', 'ato_gradf_mode', 'ato_gradf_sparsity') + IPM_SYMBOLS
 
 
 def library_path() -> str:
@@ -145,6 +145,8 @@ def declare(lib: ctypes.CDLL, prefix: str = 'ato') -> ctypes.CDLL:
         lib.ato_timing_stride.argtypes = [vp, ctypes.c_int32]
         lib.ato_set_instance_spheres.argtypes = [vp, vp, ctypes.c_int64]
         lib.ato_sphere_rows.argtypes = [vp, i32p]
+        lib.ato_gradf_mode.argtypes = [vp, ctypes.c_int32]
+        lib.ato_gradf_sparsity.argtypes = [vp, i32p, i32p]
         lib.ato_kkt_create.argtypes = [vp, ctypes.POINTER(vp)]
         lib.ato_kkt_destroy.argtypes = [vp]
         lib.ato_kkt_reserve.argtypes = [vp, ctypes.c_int32]
@@ -172,7 +174,7 @@ def declare(lib: ctypes.CDLL, prefix: str = 'ato') -> ctypes.CDLL:
         for fn in ('ato_create', 'ato_destroy', 'ato_sizes', 'ato_sparsity', 'ato_bounds', 'ato_reserve',
                    'ato_eval', 'ato_eval_f32', 'ato_hess_sparsity', 'ato_hess_eval', 'ato_timing',
                    'ato_timing_read', 'ato_timing_stride', 'ato_mesh_create', 'ato_mesh_destroy', 'ato_mesh_signed_distance',
-                   'ato_set_instance_spheres', 'ato_sphere_rows'):
+                   'ato_set_instance_spheres', 'ato_sphere_rows', 'ato_gradf_mode', 'ato_gradf_sparsity'):
             getattr(lib, fn).restype = ctypes.c_int
     return lib
 
@@ -317,6 +319,23 @@ class NativeProblem:
         self._check(self.lib.ato_bounds(self.handle, lb.ctypes.data_as(_c_double_p),
                                         ub.ctypes.data_as(_c_double_p)))
         return lb, ub
+
+    def gradf_mode(self, sparse: bool):
+        ''' sparse: evaluations write only the structural nonzeros of grad f (gradf_sparsity); the
+        other entries of the caller's buffer are left as they are (zero-fill it once) '''
+        self._check(self.lib.ato_gradf_mode(self.handle, 1 if sparse else 0))
+
+    def gradf_sparsity(self) -> np.ndarray:
+        ''' indices of the structural nonzeros of grad f (ascending) '''
+        n = ctypes.c_int32()
+        self._check(self.lib.ato_gradf_sparsity(self.handle, ctypes.byref(n), None))
+        idx = np.zeros(n.value, np.int32)
+        self._check(self.lib.ato_gradf_sparsity(self.handle, ctypes.byref(n),
+                                                idx.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))))
+        return idx
+
+    def gradf_nnz(self) -> int:
+        return int(len(self.gradf_sparsity()))
 
     def set_instance_spheres(self, centres: int, stride: int):
         ''' per-instance sphere centres: device pointer to [P][2][stride] doubles (0 clears) '''

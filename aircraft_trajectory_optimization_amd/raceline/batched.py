@@ -40,6 +40,9 @@ class BatchedNLP:
         self.grad_f = torch.zeros(shape(nw), **opts)
         self.f = torch.zeros(B, **opts)
         self.problem.reserve(B)
+        # evaluations write only the structural nonzeros of grad f (its other entries stay the zeros of
+        # the buffers above; the solver's fresh output tensors are zero-filled, solver/batched_ipm.py)
+        self.problem.gradf_mode(True)
         self.row_ptr, self.col = self.problem.sparsity()
         self.lbg, self.ubg = self.problem.bounds()
         self.isph = None          # per-instance sphere centres [2 P][B] (set_instance_spheres)

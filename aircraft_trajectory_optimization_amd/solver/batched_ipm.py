@@ -160,7 +160,7 @@ def _eval_into(problem, binder, B, X, n, m, nnz, jac):
     dev = X.device
     f = torch.empty(B, dtype=torch.float64, device=dev)
     g = torch.empty((m, B), dtype=torch.float64, device=dev)
-    gf = torch.empty((n, B), dtype=torch.float64, device=dev)
+    gf = torch.zeros((n, B), dtype=torch.float64, device=dev)     # (sparse grad f mode: zeros stay)
     J = torch.empty((nnz, B), dtype=torch.float64, device=dev) if jac else None
     st = torch.cuda.current_stream(dev)
     binder._bind_spheres()

@@ -44,17 +44,18 @@ SPEC_KW = dict(track='race', model='drone', frame='parametric', N=50, K=4, use_q
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=200, help='timed lockstep SQP iterations')
-    ap.add_argument('--warmup', type=int, default=10, help='untimed lockstep iterations before the window')
+    ap.add_argument('--steps', type=int, default=20, help='timed lockstep SQP iterations (the driver runs 20)')
+    ap.add_argument('--warmup', type=int, default=5, help='untimed lockstep iterations before the window (driver: 5)')
     ap.add_argument('--batch', type=int, default=512, help='instances per GPU')
     ap.add_argument('--max-iter', type=int, default=1000, help="IPOPT's max_iter (base_raceline.py:54)")
     ap.add_argument('--eval-steps', type=int, default=50)
     ap.add_argument('--eval-warmup', type=int, default=10)
     ap.add_argument('--dtype', choices=['f64', 'f32'], default='f64', help='evaluation-kernel bench dtype')
     ap.add_argument('--layout', choices=['interleaved', 'instance'], default='interleaved')
-    ap.add_argument('--track', choices=['race', 'fig8'], default='race',
+    ap.add_argument('--track', choices=['race', 'fig8', 'obstacles'], default='race',
                     help='fig8: the config-5 evaluation workload (scripts/fig_8.py, N = 50, K = 4), with --dtype f32 '
-                         '--batch 8192 --no-solve')
+                         '--batch 8192 --no-solve; obstacles: config 4 (obstacles.py pipeline over perturbed '
+                         'tubes, raceline/obstacle_batch.py)')
     ap.add_argument('--pose', choices=['esp', 'dcm'], default='esp',
                     help='attitude: esp (quaternion, the reference\'s) or dcm (config 5\'s direction-cosine-matrix '
                          'pose, build-side): --track fig8 --pose dcm --dtype f32 --batch 8192 --no-solve')
@@ -111,7 +112,10 @@ def eval_bench(spec, W, args, dev, world):
     g, _, f, _ = bn.results()
     assert np.isfinite(g).all() and np.isfinite(f).all(), 'non-finite evaluation results'
     elem = 8 if args.dtype == 'f64' else 4
-    bytes_per_eval = elem * (nw + ng + nnz + nw + 1)   # read w; write g, J, grad f, f
+    # read w; write g, J, the structural nonzeros of grad f (h and the inputs: the states
+    # never enter the cost) and f
+    nnz_gf = bn.problem.gradf_nnz()
+    bytes_per_eval = elem * (nw + ng + nnz + nnz_gf + 1)
     kernel_s = (k_ms / max(calls, 1)) / 1e3
     achieved = B * bytes_per_eval / kernel_s / 1e9
     traffic = None
@@ -126,7 +130,7 @@ def eval_bench(spec, W, args, dev, world):
     evals = {'value': world * B * args.eval_steps / elapsed, 'unit': 'constraint+Jacobian evals/s (g, dg/dw, f, '
              'grad f per instance, all GPUs)', 'steps': args.eval_steps, 'warmup': args.eval_warmup,
              'ms_per_step': elapsed / args.eval_steps * 1e3, 'dtype': args.dtype, 'layout': args.layout,
-             'nw': nw, 'ng': ng, 'nnz': nnz}
+             'nw': nw, 'ng': ng, 'nnz': nnz, 'nnz_grad_f': nnz_gf}
     roofline = {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                 'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic, 'kernel': 'k_eval',
                 'kernel_avg_us': kernel_s * 1e6, 'reduce_avg_us': r_ms / max(calls, 1) * 1e3,
@@ -224,6 +228,8 @@ def main():
     if world > 1:
         dist.init_process_group('nccl', device_id=dev)
 
+    if args.track == 'obstacles':
+        return obstacles_main(args, dev, world, rank)
     spec_kw = dict(SPEC_KW, track=args.track, use_dcm=args.pose == 'dcm')
     if args.cpc:
         if not args.no_solve:
@@ -246,8 +252,20 @@ def main():
         sync()
         if world > 1:
             dist.barrier()
-        t0 = time.perf_counter()
-        res, solver, _ = solve_shard(spec, seeds, IPMOptions(max_iter=args.max_iter), on_iteration=hook)
+        if args.track == 'fig8':
+            # config 5 as a solve: the fig-8 drone (ESP or DCM pose) from perturbed point-mass warm starts
+            # (raceline/batch_instances.py), fp64 evaluation and KKT
+            from aircraft_trajectory_optimization_amd.raceline.batch_instances import warm_started_batch
+            from aircraft_trajectory_optimization_amd.solver.batched_ipm import device_solver
+            wkw = {k: v for k, v in spec_kw.items() if k not in ('model',)}
+            spec, Wws, LBW, UBW, _ = warm_started_batch(len(seeds), device=dev, seeds=seeds, **wkw)
+            sync()
+            t0 = time.perf_counter()
+            solver = device_solver(spec, len(seeds), LBW, UBW, IPMOptions(max_iter=args.max_iter), device=dev)
+            res = solver.solve(Wws, on_iteration=hook)
+        else:
+            t0 = time.perf_counter()
+            res, solver, _ = solve_shard(spec, seeds, IPMOptions(max_iter=args.max_iter), on_iteration=hook)
         sync()
         t_solve = time.perf_counter() - t0
         if win['t0'] is None or win['t1'] is None:
@@ -278,14 +296,23 @@ def main():
                 sqp_full['solutions_all_gathered'] = sol_gather
             lap_err = None
             if not args.no_single:
-                # instance 0 re-solved alone (B = 1) from the same start: batched vs single-instance
+                # the first OPTIMAL instance re-solved alone (B = 1) from the same start: batched vs
+                # single-instance lap time (an unconverged instance would compare two stopped iterates)
                 from aircraft_trajectory_optimization_amd.raceline.batched_solve import solve_shard as one
-                r1, s1, _ = one(spec, [seeds[0]], IPMOptions(max_iter=args.max_iter))
+                opt = [i for i, st in enumerate(res.status) if st == 'optimal']
+                i0 = opt[0] if opt else 0
+                if args.track == 'fig8':
+                    s1 = device_solver(spec, 1, LBW[i0:i0 + 1], UBW[i0:i0 + 1], IPMOptions(max_iter=args.max_iter),
+                                       device=dev)
+                    r1 = s1.solve(Wws[i0:i0 + 1])
+                else:
+                    r1, s1, _ = one(spec, [seeds[i0]], IPMOptions(max_iter=args.max_iter))
                 lap1 = float(r1.x[:spec.N].sum())
-                lap_err = abs(float(allrec[0, 0]) - lap1)
-                sqp_full['instance0'] = {'batched_lap_s': float(allrec[0, 0]), 'single_lap_s': lap1,
-                                         'batched_status': res.status[0], 'single_status': r1.status[0],
-                                         'batched_iters': int(res.iters[0]), 'single_iters': int(r1.iters[0])}
+                lap_err = abs(float(allrec[i0, 0]) - lap1)
+                sqp_full['lap_check_instance'] = {'seed': int(seeds[i0]), 'batched_lap_s': float(allrec[i0, 0]),
+                                                  'single_lap_s': lap1, 'batched_status': res.status[i0],
+                                                  'single_status': r1.status[0], 'batched_iters': int(res.iters[i0]),
+                                                  'single_iters': int(r1.iters[0])}
             out = {
                 'metric': METRIC,
                 'value': value,
@@ -298,8 +325,11 @@ def main():
                 'scaling': 'weak',
                 'vs_baseline': None,
                 'dtype': 'f64',
-                'data': 'synthetic: seeded cold-start instances (SURVEY 8(d) config 3 generator, raceline/instances.py)',
-                'config': {'workload': f'{track}_parametric_{args.pose}_drone_colloc_N50_K4_cold_start_batched_sqp',
+                'data': ('synthetic: perturbed point-mass warm starts (raceline/batch_instances.py)' if args.track == 'fig8'
+                         else 'synthetic: seeded cold-start instances (SURVEY 8(d) config 3 generator, '
+                              'raceline/instances.py)'),
+                'config': {'workload': f'{track}_parametric_{args.pose}_drone_colloc_N50_K4_'
+                                       f'{"warm" if args.track == "fig8" else "cold"}_start_batched_sqp',
                            'N': 50, 'K': 4, 'nz': spec.nz, 'nu': 4, 'batch_per_gpu': B, 'global_batch': world * B,
                            'max_iter': args.max_iter, 'layout': args.layout,
                            'parallelism': f'instances sharded x{world}, records all-gathered'},
@@ -307,7 +337,8 @@ def main():
                 'lap_time_err_note': 'CasADi/IPOPT cannot run in this pipeline (SURVEY F8): lap-time parity with it '
                                      'is unpinned; the transcription is pinned to the reference\'s own code '
                                      '(tests/golden), solutions by oracle KKT + second-order certificates; '
-                                     'lap_time_err_batched_vs_single_s compares instance 0 batched vs alone',
+                                     'lap_time_err_batched_vs_single_s compares the first optimal instance '
+                                     'batched vs alone (sqp_full.lap_check_instance)',
                 'lap_time_err_batched_vs_single_s': lap_err,
                 'roofline': roofline,
                 'cpu_baseline': None,
@@ -340,6 +371,70 @@ def main():
                           'global_batch': world * B, 'layout': args.layout},
                'roofline': roofline, 'cpu_baseline': None, 'evals': evals}
     if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def obstacles_main(args, dev, world, rank):
+    '''
+    Config 4: obstacles.py's pipeline over perturbed planning tubes, this rank's shard of
+    the seeds (raceline/obstacle_batch.py): point-mass racelines on every tube in one batched solve,
+    drone guesses, drone solves batched per quaternion closure sign. The timed window is lockstep
+    iterations [W, W + K) of the largest drone batch; the whole pipeline is reported beside it.
+    '''
+    import torch
+    import torch.distributed as dist
+    from aircraft_trajectory_optimization_amd.raceline.batched_solve import window_timer
+    from aircraft_trajectory_optimization_amd.raceline.obstacle_batch import config4_problem, solve_config4_shard
+    from aircraft_trajectory_optimization_amd.raceline.problem import ProblemSpec
+    from aircraft_trajectory_optimization_amd.raceline.shard import max_over_ranks, shard_seeds
+    from aircraft_trajectory_optimization_amd.solver.ipm import IPMOptions
+    B = args.batch
+    seeds = shard_seeds(rank, world, B)
+    prob = config4_problem()
+    dspec = ProblemSpec(prob['line'], prob['cfg'].copy(), prob['dveh'], 'parametric', sphere_table=prob['table'])
+    evals, roofline = eval_bench(dspec, np.repeat(dspec.w0[None], B, axis=0), args, dev, world)
+    sync = lambda: torch.cuda.synchronize(dev)  # noqa: E731
+    hook, win = window_timer(args.warmup, args.steps, sync)
+    sync()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    r = solve_config4_shard(seeds, IPMOptions(max_iter=args.max_iter), prob, on_iteration=hook)
+    sync()
+    t_all = max_over_ranks(time.perf_counter() - t0, dev)
+    if win['t0'] is None or win['t1'] is None:
+        raise RuntimeError('the drone solve ended before the timed window began')
+    window_s = max_over_ranks(win['t1'] - win['t0'], dev)
+    counts = torch.tensor([float(win['count']), float(win['timed'])], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(counts, op=dist.ReduceOp.SUM)
+    st = r['status']
+    ok = np.array([x in ('optimal', 'acceptable') for x in st])
+    if rank == 0:
+        steps_timed = int(win['timed'])
+        out = {'metric': METRIC, 'value': float(counts[0].item()) / window_s,
+               'unit': 'SQP iterations/s (instance-iterations of the batched drone solve, all GPUs)',
+               'n_gpus': world, 'steps': steps_timed, 'warmup': args.warmup,
+               'ms_per_step': window_s / max(steps_timed, 1) * 1e3, 'higher_is_better': True, 'scaling': 'weak',
+               'vs_baseline': None, 'dtype': 'f64',
+               'data': 'synthetic: seeded perturbed planning tubes (SURVEY 8(d) config 4 generator, '
+                       'ObstacleFreeTube.perturbed_tables)',
+               'config': {'workload': 'obstacles_parametric_esp_drone_colloc_N50_K4_perturbed_tubes_batched_sqp',
+                          'N': 50, 'K': 4, 'batch_per_gpu': B, 'global_batch': world * B, 'max_iter': args.max_iter,
+                          'drone_batches_by_closure_sign': r['groups'],
+                          'parallelism': f'instances sharded x{world}'},
+               'lap_time_err_vs_casadi': None,
+               'roofline': roofline, 'cpu_baseline': None, 'evals': evals,
+               'pipeline': {'wall_s': t_all, 'point_mass_solve_s': r['point_solve_s'],
+                            'drone_solve_s': r['drone_solve_s'],
+                            'point_mass_optimal': int(sum(x == 'optimal' for x in r['point_status'])),
+                            'statuses': {k: st.count(k) for k in sorted(set(st))},
+                            'converged_per_s': float(ok.sum()) / t_all,
+                            'drone_iterations': {'median': float(np.median(r['iters'])), 'sum': int(r['iters'].sum())},
+                            'lap_converged': {'min': float(r['lap'][ok].min()), 'median': float(np.median(r['lap'][ok])),
+                                              'max': float(r['lap'][ok].max())} if ok.any() else None}}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -132,6 +132,16 @@ int ato_sparsity(const ato_handle* h, const int32_t** row_ptr, const int32_t** c
 /* lbg / ubg (host arrays of ng doubles, caller owned). */
 int ato_bounds(const ato_handle* h, double* lbg, double* ubg);
 
+/* Structural nonzeros of grad f: idx (host, caller owned, may be NULL to query nnz) gets the
+ * ascending indices of h_n and of every node's inputs u and input rates du -- the only variables
+ * in the cost J = sum h_n B_k (u'Ru + du'dR du + 1) (base_raceline.py:601-623); the states'
+ * entries are structural zeros. */
+int ato_gradf_sparsity(const ato_handle* h, int32_t* nnz, int32_t* idx);
+
+/* sparse != 0: ato_eval / ato_eval_f32 write only the ato_gradf_sparsity entries of grad_f and
+ * leave the others untouched (the caller zero-fills its buffer once); 0 (default): every entry. */
+int ato_gradf_mode(ato_handle* h, int32_t sparse);
+
 /* Reserve device scratch for batches up to max_batch (call before graph capture). */
 int ato_reserve(ato_handle* h, int32_t max_batch);
 

@@ -143,32 +143,6 @@ def test_batched_device_solve_is_deterministic():
     assert [int(i) for i in r1.iters] == [int(i) for i in r2.iters]
 
 
-def test_speculative_inertia_passes_match_serial(monkeypatch):
-    ''' the speculative inertia-correction passes (BatchedInteriorPoint._speculate: the next members
-    of each hard instance's delta_w sequence factorised side by side in spare storage) give the
-    serial passes' iterates bitwise -- statuses, iteration counts, solutions -- with fewer
-    factorisation calls on long inertia corrections; config-3 cold starts at race 12 x 3 '''
-    from aircraft_trajectory_optimization_amd.raceline.instances import seeded_instances
-    from aircraft_trajectory_optimization_amd.solver.batched_ipm import device_solver
-    from aircraft_trajectory_optimization_amd.tracks import make_spec
-    spec = make_spec(track='race', N=12, K=3)
-    B = 16
-    W, LBW, UBW = seeded_instances(spec, range(B))
-    runs = []
-    for flag in ('0', '1'):
-        monkeypatch.setenv('ATO_KKT_SPECULATE', flag)
-        sol = device_solver(spec, B, LBW, UBW, IPMOptions(max_iter=300))
-        sol.async_restoration = False
-        runs.append(sol.solve(W))
-    r0, r1 = runs
-    print('serial', r0.stats['factorizations'], 'factorisations; speculative', r1.stats['factorizations'],
-          r1.stats.get('speculative'))
-    assert 'speculative' not in r0.stats and r1.stats['speculative'][0] > 0
-    assert r0.status == r1.status
-    assert [int(i) for i in r0.iters] == [int(i) for i in r1.iters]
-    assert torch.equal(r0.x, r1.x)
-
-
 def test_asynchronous_restoration_matches_synchronous():
     ''' restoration phases in the worker thread (own stream, library handle and KKT storage) while
     the other instances iterate: every instance ends with the status, iteration count and

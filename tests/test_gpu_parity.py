@@ -109,6 +109,39 @@ def test_deterministic_and_partial_outputs():
     _close(bn.results()[1], J1, 1e-14)
 
 
+@pytest.mark.parametrize('cfg', [dict(N=50, K=4), dict(track='fig8', N=8, K=7), dict(frame='global', N=7, K=2),
+                                 dict(N=7, K=2, rk4=True), dict(model='point', use_quat=False, N=6, K=3),
+                                 dict(track='fig8', frame='global', use_dcm=True, N=8, K=3,
+                                      cpc={'waypoints': None, 'tol': 0.3})], ids=_id)
+@pytest.mark.parametrize('dtype', [torch.float64, torch.float32])
+def test_sparse_grad_f_writes_exactly_its_pattern(cfg, dtype):
+    ''' ato_gradf_sparsity lists every entry grad f can be non-zero at (h and the inputs; the
+    states -- and CPC's progress variables -- never enter the cost J = sum h B (u'Ru + du'dR du + 1)),
+    and in the sparse mode the kernels write exactly those entries: on NaN-prefilled buffers the
+    listed entries equal the dense mode's, the others stay untouched '''
+    spec = product_spec(**cfg)
+    B = 67                                   # a partial last chunk as well as full ones
+    rng = np.random.default_rng(3)
+    W = np.stack([random_w(spec, rng) for _ in range(B)])
+    bn = _batched(spec, B, dtype=dtype)
+    idx = bn.problem.gradf_sparsity()
+    assert np.all(np.diff(idx) > 0) and idx[0] == 0 and idx[-1] < bn.problem.nw
+    bn.set_w(W)
+    bn.problem.gradf_mode(False)
+    bn.grad_f.fill_(float('nan'))
+    bn.evaluate()
+    dense = bn.grad_f.cpu().numpy().copy()
+    assert np.isfinite(dense).all()
+    off = np.setdiff1d(np.arange(bn.problem.nw), idx)
+    assert np.all(dense[off] == 0), 'a non-zero outside ato_gradf_sparsity'
+    bn.problem.gradf_mode(True)
+    bn.grad_f.fill_(float('nan'))
+    bn.evaluate()
+    sparse = bn.grad_f.cpu().numpy()
+    assert np.all(np.isnan(sparse[off])), 'the sparse mode wrote a structural zero'
+    np.testing.assert_array_equal(sparse[idx], dense[idx])
+
+
 def test_fp32_tracks_fp64():
     spec, _, W, _ = _racetrack(64)
     d = _batched(spec, 64)

@@ -31,7 +31,7 @@ run() {  # run <name> <seconds> <cmd...>
 
 for s in $STEPS; do
     case $s in
-        tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --capture=sys --timeout 300 --timeout-method thread -p no:cacheprovider ${GPU_TESTS:-} ;;
+        tests) run pytest_gpu 1000 python -u -m pytest tests -m gpu --maxfail=6 -v --capture=sys --timeout 300 --timeout-method thread -p no:cacheprovider ${GPU_TESTS:-} ;;
         ab)    run ab_new 900 python -u tools/solver_ab.py --what fig8,config3 --tag new --out "$OUT/ab_new.json"
                PYTHONPATH=$PWD/tools/r04_baseline run ab_r04 900 python -u tools/solver_ab.py --what fig8,config3 --tag r04 --out "$OUT/ab_r04.json" ;;
         abl)   i=0
@@ -40,9 +40,18 @@ for s in $STEPS; do
                    i=$((i+1))
                    ATO_AB_OPTS="$o" run abl_$i 900 python -u tools/solver_ab.py --what ${AB_WHAT:-fig8,fig8k4,config3} --tag "$o" --out "$OUT/abl_$i.json"
                done ;;
+        sadtau) for t in 0 1e2 1e4 1e6; do
+                   ATO_KKT_SADDLE_TAU=$t run kkt_sad_tau$t 200 python tools/bench_kkt.py --batch 512 --reps 5 --saddle 1 --out "$OUT/kkt_sad_tau$t.json"
+               done
+               run kkt_bk 200 python tools/bench_kkt.py --batch 512 --reps 5 --saddle 0 --out "$OUT/kkt_bk.json"
+               for t in 1e2 1e4; do
+                   ATO_KKT_SADDLE=1 ATO_KKT_SADDLE_TAU=$t run c3_sad_tau$t 600 python -u tools/solver_ab.py --what config3 --tag "saddle tau $t" --out "$OUT/c3_sad_tau$t.json"
+               done ;;
+        bench5solve) run bench5_dcm_solve 900 python bench.py --track fig8 --pose dcm --batch ${B5:-8192} --no-cpu-baseline ;;
+        bench4) run bench4_obstacles 900 python bench.py --track obstacles --batch 512 --no-cpu-baseline ;;
         abnew) run ab_new 900 python -u tools/solver_ab.py --what ${AB_WHAT:-fig8,config3} --tag new --out "$OUT/ab_new.json" ;;
         smoke) run smoke 300 python -c 'import __graft_entry__ as g; g.smoke()' ;;
-        bench) run bench 900 python bench.py --steps 50 --warmup 10 ;;
+        bench) run bench 900 python bench.py ;;
         bench32) run bench_f32 300 python bench.py --steps 50 --warmup 10 --dtype f32 --no-cpu-baseline --no-solve ;;
         benchim) run bench_im 300 python bench.py --steps 50 --warmup 10 --layout instance --no-cpu-baseline --no-solve ;;
         benchbig) run bench_b4096 300 python bench.py --steps 20 --warmup 5 --batch 4096 --no-cpu-baseline --no-solve ;;
@@ -133,12 +142,6 @@ for s in $STEPS; do
                 for t in 0 8; do
                     ATO_EVAL_TILE=$t run eval_tile${t}_f32_b8192 300 python bench.py --track fig8 --pose dcm --dtype f32 --batch 8192 --no-solve --no-cpu-baseline --eval-steps 50
                 done ;;
-        specab) for v in 0 1; do
-                    ATO_KKT_SPECULATE=$v run solve_spec$v 600 python tools/solve_batched.py --batch 512 --max-iter 200 --cold --no-host --out "$OUT/solve_spec$v.json"
-                done ;;
-        specfull) for v in 0 1; do
-                    ATO_KKT_SPECULATE=$v run solvefull_spec$v 600 python tools/solve_batched.py --batch 512 --max-iter 1000 --cold --no-host --out "$OUT/solvefull_spec$v.json"
-                done ;;
         c3ab)  for v in base cur; do
                    if [ $v = base ]; then lp=$PWD/tools/diag/_lib/libato_base.so; else lp=; fi
                    ATO_LIB_PATH=$lp ATO_KKT_SPECULATE=0 run pytest_c3_$v 300 python -u -m pytest tests/test_gpu_batched_ipm.py -x -v -s --timeout 200 --timeout-method thread -p no:cacheprovider -k config3_full
@@ -155,7 +158,6 @@ for s in $STEPS; do
                    ATO_EVAL_TILE=$t run pmc_fetch_tile$t 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_tile$t" -o run -- \
                        python bench.py --steps 10 --warmup 3 --batch 4096 --no-cpu-baseline --no-solve --eval-steps 10
                 done ;;
-        spectests) run pytest_spec 300 python -u -m pytest tests/test_gpu_batched_ipm.py -x -v -s --timeout 200 --timeout-method thread -p no:cacheprovider -k "speculative or deterministic or restoration" ;;
         scripts) run pytest_scripts 900 python -u -m pytest tests/test_gpu_scripts.py -x -v -s --timeout 800 --timeout-method thread -p no:cacheprovider ;;
         mbscale) run mb_store_scale 120 ./tools/mb_store_scale
                run bench_b4096 300 python bench.py --steps 20 --warmup 5 --batch 4096 --no-cpu-baseline --no-solve --eval-steps 30 ;;
