@@ -20,7 +20,8 @@ class BatchedNLP:
     ''' device-resident batch of NLP instances '''
 
     def __init__(self, spec: ProblemSpec, batch: int, dtype: torch.dtype = torch.float64,
-                 layout: int = native.ATO_LAYOUT_INTERLEAVED, device: Optional[torch.device] = None):
+                 layout: int = native.ATO_LAYOUT_INTERLEAVED, device: Optional[torch.device] = None,
+                 buffers: bool = True):
         if not torch.cuda.is_available():
             raise RuntimeError('BatchedNLP needs a HIP device (torch.cuda.is_available() is False)')
         self.device = device or torch.device('cuda', torch.cuda.current_device())
@@ -34,11 +35,13 @@ class BatchedNLP:
         nw, ng, nnz, B = self.problem.nw, self.problem.ng, self.problem.nnz, self.batch
         shape = (lambda n: (n, B)) if layout == native.ATO_LAYOUT_INTERLEAVED else (lambda n: (B, n))
         opts = {'device': self.device, 'dtype': dtype}
-        self.w = torch.zeros(shape(nw), **opts)
-        self.g = torch.zeros(shape(ng), **opts)
-        self.jac = torch.zeros(shape(nnz), **opts)
-        self.grad_f = torch.zeros(shape(nw), **opts)
-        self.f = torch.zeros(B, **opts)
+        # resident input / output buffers of evaluate(); buffers=False: the caller passes its own
+        # (the solver's evaluator, whose outputs are fresh tensors: at B = 8192 J alone is GBs)
+        self.w = torch.zeros(shape(nw), **opts) if buffers else None
+        self.g = torch.zeros(shape(ng), **opts) if buffers else None
+        self.jac = torch.zeros(shape(nnz), **opts) if buffers else None
+        self.grad_f = torch.zeros(shape(nw), **opts) if buffers else None
+        self.f = torch.zeros(B, **opts) if buffers else None
         self.problem.reserve(B)
         # evaluations write only the structural nonzeros of grad f (its other entries stay the zeros of
         # the buffers above; the solver's fresh output tensors are zero-filled, solver/batched_ipm.py)

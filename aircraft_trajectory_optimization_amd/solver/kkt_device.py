@@ -160,13 +160,24 @@ class DeviceKKT:
         return _residual(self, self.cap, H, J, dx, dr, x, rhs, stream, instances)
 
     def fork(self) -> 'DeviceKKT':
-        ''' a second factorisation with its own storage (the asynchronous restoration phase) '''
-        return DeviceKKT(self.plan, self.cap, self.device)
+        ''' a second factorisation with its own storage (the asynchronous restoration phase). It is
+        driven through views only, so its storage starts small and grows with the largest view
+        (at B = 8192 a full-width copy of the factor storage would be tens of GB per phase in flight) '''
+        return DeviceKKT(self.plan, min(self.cap, 64), self.device)
+
+    def ensure(self, count: int):
+        ''' grow the factor storage to `count` instances (the library drains the device first) '''
+        if count > self.cap:
+            with torch.cuda.device(self.device):
+                self._check(self.lib.ato_kkt_reserve(self.handle, int(count)))
+            self.cap = int(count)
+            self.inertia = torch.zeros((self.cap, 3), dtype=torch.int32, device=self.device)
 
     def view(self, count: int) -> '_KKTView':
         ''' the same factor storage driven with [element][count] value arrays (instances 0 .. count-1
         of the view's own numbering use storage slots 0 .. count-1): the restoration phase runs
         its nested solve on a compacted batch between two outer factorisations '''
+        self.ensure(count)
         return _KKTView(self, count)
 
     def close(self):

@@ -67,6 +67,7 @@ def parse():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-solve', action='store_true', help='evaluation kernel only')
     ap.add_argument('--no-single', action='store_true', help='skip the B = 1 re-solve of instance 0')
+    ap.add_argument('--progress', type=int, default=0, help='solver progress line every N lockstep iterations')
     ap.add_argument('--traffic-json', default=os.path.join(ROOT, 'profiles', 'traffic_latest.json'))
     return ap.parse_args()
 
@@ -262,10 +263,11 @@ def main():
             sync()
             t0 = time.perf_counter()
             solver = device_solver(spec, len(seeds), LBW, UBW, IPMOptions(max_iter=args.max_iter), device=dev)
-            res = solver.solve(Wws, on_iteration=hook)
+            res = solver.solve(Wws, on_iteration=hook, progress=args.progress)
         else:
             t0 = time.perf_counter()
-            res, solver, _ = solve_shard(spec, seeds, IPMOptions(max_iter=args.max_iter), on_iteration=hook)
+            res, solver, _ = solve_shard(spec, seeds, IPMOptions(max_iter=args.max_iter), on_iteration=hook,
+                                         progress=args.progress)
         sync()
         t_solve = time.perf_counter() - t0
         if win['t0'] is None or win['t1'] is None:
