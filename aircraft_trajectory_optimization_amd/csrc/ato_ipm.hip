@@ -185,33 +185,38 @@ __device__ __forceinline__ void fold_chunks(const double* __restrict__ work, int
     }
 }
 
-__global__ __launch_bounds__(CB * FG) void k_errors_fold(int W, int NC, int m, double s_max,
-                                                         const double* __restrict__ n_bounds,
-                                                         const double* __restrict__ work, double* __restrict__ out) {
-    __shared__ double part[FG][QMAX][CB];
-    const int lane = threadIdx.x % CB, grp = threadIdx.x / CB;
-    const int b = blockIdx.x * CB + lane;
+// The errors fold in two launches (k_errors_fold above kept 8 workgroups busy at W = 512 and ran
+// 368 us, gpurun_out r05l): EG chunk ranges per column in parallel, then the EG partials of every
+// column in range order (deterministic).
+constexpr int EG = 32;
+__device__ __forceinline__ void errors_fold_q(double (&q)[QMAX], const double (&v)[QMAX]) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) q[k] = nmax(q[k], v[k]);
+#pragma unroll
+    for (int k = 4; k < QMAX; ++k) q[k] += v[k];
+}
+
+__global__ __launch_bounds__(CB) void k_errors_fold1(int W, int NC, const double* __restrict__ work,
+                                                     double* __restrict__ part) {
+    const int b = blockIdx.x * CB + threadIdx.x, g = blockIdx.y;
+    if (b >= W) return;
+    const int c0 = (int)((long long)NC * g / EG), c1 = (int)((long long)NC * (g + 1) / EG);
     double q[QMAX] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-    auto fold = [&](const double (&v)[QMAX]) {
+    fold_chunks<QMAX, 2>(work, NC, W, b, c0, c1, [&](const double (&v)[QMAX]) { errors_fold_q(q, v); });
 #pragma unroll
-        for (int k = 0; k < 4; ++k) q[k] = nmax(q[k], v[k]);
-#pragma unroll
-        for (int k = 4; k < QMAX; ++k) q[k] += v[k];
-    };
-    if (b < W) {
-        int c0, c1;
-        fold_range(NC, grp, c0, c1);
-        fold_chunks<QMAX, 4>(work, NC, W, b, c0, c1, fold);
-    }
-#pragma unroll
-    for (int k = 0; k < QMAX; ++k) part[grp][k][lane] = q[k];
-    __syncthreads();
-    if (grp != 0 || b >= W) return;
-    for (int g = 1; g < FG; ++g) {
+    for (int k = 0; k < QMAX; ++k) part[((long long)k * EG + g) * W + b] = q[k];
+}
+
+__global__ __launch_bounds__(CB) void k_errors_fold2(int W, int m, double s_max, const double* __restrict__ n_bounds,
+                                                     const double* __restrict__ part, double* __restrict__ out) {
+    const int b = blockIdx.x * CB + threadIdx.x;
+    if (b >= W) return;
+    double q[QMAX] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (int g = 0; g < EG; ++g) {
         double v[QMAX];
 #pragma unroll
-        for (int k = 0; k < QMAX; ++k) v[k] = part[g][k][lane];
-        fold(v);
+        for (int k = 0; k < QMAX; ++k) v[k] = part[((long long)k * EG + g) * W + b];
+        errors_fold_q(q, v);
     }
     const double nz = n_bounds[b];
     const double zsum = ((q[4] + q[5]) + q[6]) + q[7];
@@ -596,9 +601,147 @@ __global__ __launch_bounds__(256) void k_kkt_diag(Dev d, const double* __restric
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// IPOPT's PDPerturbationHandler per column (batched_ipm.py BatchedPerturbation, solver/ipm.py
+// PerturbationHandler) and the bookkeeping of one inertia-correction pass of _kkt_step, one
+// thread per column: the whole per-pass state machine in one launch instead of ~40 masked
+// torch operations per call.
+// ------------------------------------------------------------------------------------------
+enum { DEG_UNK = 0, DEG_NO = 1, DEG_YES = 2 };
+enum { T_NONE = 0, T_C0X0 = 1, T_CPX0 = 2, T_C0XP = 3, T_CPXP = 4 };
+
+struct PertPrm {
+    double delta_w_0, delta_w_min, delta_w_max, kappa_w_minus, kappa_w_plus, kappa_w_plus_bar, delta_c_base, kappa_c;
+    long long degen_iters_max;
+};
+
+struct PertCol {           // one column's handler state (registers)
+    long long hdeg, jdeg, diters, test;
+    double dx, dc, dx_last, dc_last;
+};
+
+__device__ inline double cmax(double a, double b) { return a != a ? a : (a < b ? b : a); }   // torch.clamp(min=b)
+
+__device__ inline void pert_finalize(PertCol& c, const PertPrm& o) {
+    const bool uh = c.hdeg == DEG_UNK, uj = c.jdeg == DEG_UNK;
+    const long long t = c.test;
+    if ((t == T_CPX0 && uj) || (t == T_C0XP && uh) || t == T_CPXP) c.diters += 1;
+    const bool reach = c.diters >= o.degen_iters_max;
+    if ((t == T_C0X0 || t == T_CPX0) && uh) c.hdeg = DEG_NO;
+    else if (((t == T_C0XP && uh) || t == T_CPXP) && reach) c.hdeg = DEG_YES;
+    if ((t == T_C0X0 || t == T_C0XP) && uj) c.jdeg = DEG_NO;
+    else if (((t == T_CPX0 && uj) || t == T_CPXP) && reach) c.jdeg = DEG_YES;
+}
+
+__device__ inline bool pert_wrong_inertia(PertCol& c, const PertPrm& o) {   // get_deltas_for_wrong_inertia
+    const double last = c.dx_last;
+    const double first = last == 0.0 ? o.delta_w_0 : cmax(last * o.kappa_w_minus, o.delta_w_min);
+    const double grow = (last == 0.0 || 1e5 * last < c.dx) ? c.dx * o.kappa_w_plus_bar : c.dx * o.kappa_w_plus;
+    c.dx = c.dx == 0.0 ? first : grow;
+    return c.dx <= o.delta_w_max;
+}
+
+__device__ inline double pert_cd(double mu, const PertPrm& o) { return o.delta_c_base * tpow(mu, o.kappa_c); }
+
+__device__ inline bool pert_consider(PertCol& c, double mu, const PertPrm& o) {       // returns: failed
+    pert_finalize(c, o);
+    if (c.dx > 0.0) c.dx_last = c.dx;
+    if (c.dc > 0.0) c.dc_last = c.dc;
+    c.test = (c.hdeg == DEG_UNK || c.jdeg == DEG_UNK) ? T_C0X0 : T_NONE;
+    c.dc = c.jdeg == DEG_YES ? pert_cd(mu, o) : 0.0;
+    c.dx = 0.0;
+    return c.hdeg == DEG_YES && !pert_wrong_inertia(c, o);
+}
+
+__device__ inline bool pert_singular(PertCol& c, double mu, const PertPrm& o) {
+    bool wi;
+    if (c.hdeg == DEG_UNK || c.jdeg == DEG_UNK) {
+        if (c.test == T_C0X0) {
+            if (c.jdeg == DEG_UNK) { c.dc = pert_cd(mu, o); c.test = T_CPX0; wi = false; }
+            else { c.test = T_C0XP; wi = true; }
+        } else if (c.test == T_CPX0) { c.dc = 0.0; c.test = T_C0XP; wi = true; }
+        else if (c.test == T_C0XP) { c.dc = pert_cd(mu, o); c.test = T_CPXP; wi = true; }
+        else wi = true;
+    } else if (c.dc > 0.0 || c.jdeg == DEG_YES) wi = true;
+    else { c.dc = pert_cd(mu, o); wi = false; }
+    return wi && !pert_wrong_inertia(c, o);
+}
+
+__device__ inline bool pert_wrong(PertCol& c, double mu, const PertPrm& o) {
+    pert_finalize(c, o);
+    if (pert_wrong_inertia(c, o)) return false;
+    if (c.dc != 0.0) return true;
+    // fallback: delta_c > 0 and a fresh delta_w, with the Hessian's degeneracy unknown again
+    c.dc = pert_cd(mu, o);
+    c.dx = 0.0;
+    c.test = T_NONE;
+    if (c.hdeg == DEG_YES) c.hdeg = DEG_UNK;
+    return !pert_wrong_inertia(c, o);
+}
+
+__global__ __launch_bounds__(CB) void k_perturb(int op, int W, int m, PertPrm o, long long* __restrict__ hdeg,
+                                                long long* __restrict__ jdeg, long long* __restrict__ diters,
+                                                long long* __restrict__ test, double* __restrict__ pdx,
+                                                double* __restrict__ pdc, double* __restrict__ pdxl,
+                                                double* __restrict__ pdcl, const double* __restrict__ mu,
+                                                uint8_t* __restrict__ pend, const int32_t* __restrict__ inertia,
+                                                double* __restrict__ dw_out, double* __restrict__ dc_out,
+                                                uint8_t* __restrict__ tosolve, const uint8_t* __restrict__ fin) {
+    const int b = blockIdx.x * CB + threadIdx.x;
+    if (b >= W) return;
+    bool p = pend[b] != 0;
+    if (op == 2) {                              // after the solves: unrefinable ones count as singular
+        p = tosolve[b] != 0 && fin[b] == 0;
+        tosolve[b] = 0;
+    }
+    if (!p) {
+        pend[b] = 0;
+        return;
+    }
+    PertCol c{hdeg[b], jdeg[b], diters[b], test[b], pdx[b], pdc[b], pdxl[b], pdcl[b]};
+    const double u = mu[b];
+    if (op == 0) {
+        p = !pert_consider(c, u, o);
+    } else if (op == 1) {                       // one factorisation pass: classify the inertia
+        const int* in = inertia + 3 * (long long)b;
+        const bool sing = in[2] > 0 || in[1] < m;
+        const bool wrong = !sing && in[1] > m;
+        if (!sing && !wrong) {
+            dw_out[b] = c.dx;
+            dc_out[b] = c.dc;
+            tosolve[b] = 1;
+            p = false;
+        } else {
+            p = !(sing ? pert_singular(c, u, o) : pert_wrong(c, u, o));
+        }
+    } else {
+        p = !pert_singular(c, u, o);
+    }
+    hdeg[b] = c.hdeg; jdeg[b] = c.jdeg; diters[b] = c.diters; test[b] = c.test;
+    pdx[b] = c.dx; pdc[b] = c.dc; pdxl[b] = c.dx_last; pdcl[b] = c.dc_last;
+    pend[b] = p ? 1 : 0;
+}
+
 }  // namespace
 
 extern "C" {
+
+int ato_ipm_perturb(int32_t op, int32_t W, int32_t m, const double* prm, int64_t* hdeg, int64_t* jdeg,
+                    int64_t* diters, int64_t* test, double* dx, double* dc, double* dx_last, double* dc_last,
+                    const double* mu, uint8_t* pend, const int32_t* inertia, double* dw_out, double* dc_out,
+                    uint8_t* tosolve, const uint8_t* fin, void* stream) {
+    if (op < 0 || op > 2 || W < 0 || !prm) return fail(ATO_ERR_ARG, "ato_ipm_perturb: arguments");
+    if (W == 0) return 0;
+    if (!hdeg || !jdeg || !diters || !test || !dx || !dc || !dx_last || !dc_last || !mu || !pend ||
+        (op == 1 && (!inertia || !dw_out || !dc_out || !tosolve)) || (op == 2 && (!tosolve || !fin)))
+        return fail(ATO_ERR_ARG, "ato_ipm_perturb: arguments");
+    const PertPrm o{prm[0], prm[1], prm[2], prm[3], prm[4], prm[5], prm[6], prm[7], (long long)prm[8]};
+    hipLaunchKernelGGL(k_perturb, dim3((W + CB - 1) / CB), dim3(CB), 0, static_cast<hipStream_t>(stream), (int)op, W,
+                       m, o, reinterpret_cast<long long*>(hdeg), reinterpret_cast<long long*>(jdeg),
+                       reinterpret_cast<long long*>(diters), reinterpret_cast<long long*>(test), dx, dc, dx_last,
+                       dc_last, mu, pend, inertia, dw_out, dc_out, tosolve, fin);
+    return check_launch("ato_ipm_perturb");
+}
 
 int ato_ipm_kkt_diag(const ato_ipm_dims* d, const double* Sx, const double* Ss, const double* dw, const double* dc,
                      double* dx, double* dr, double* Ds, void* stream) {
@@ -616,7 +759,7 @@ int ato_ipm_kkt_diag(const ato_ipm_dims* d, const double* Sx, const double* Ss, 
 size_t ato_ipm_work_size(const ato_ipm_dims* d) {
     if (!d || d->W <= 0) return 0;
     const Parts P = make_parts(d->n, d->mi, d->meq, d->m);
-    return (size_t)QMAX * P.c0[4] * d->W;
+    return (size_t)QMAX * (P.c0[4] + EG) * d->W;      // chunk partials + the errors fold's range partials
 }
 
 int ato_ipm_errors(const ato_ipm_dims* d, const ato_ipm_bounds* bd, const double* x, const double* s,
@@ -629,8 +772,9 @@ int ato_ipm_errors(const ato_ipm_dims* d, const ato_ipm_bounds* bd, const double
     auto st = static_cast<hipStream_t>(stream);
     hipLaunchKernelGGL(k_errors, col_grid(d->W, P.c0[4]), dim3(CB), 0, st, v, P, x, s, g, c_rhs, sg, y, zl, zu, vl,
                        vu, dual_x, mu, work);
-    hipLaunchKernelGGL(k_errors_fold, col_grid(d->W, 1), dim3(CB * FG), 0, st, d->W, P.c0[4], d->m, s_max, n_bounds,
-                       work, out);
+    double* part = work + (size_t)QMAX * P.c0[4] * d->W;
+    hipLaunchKernelGGL(k_errors_fold1, col_grid(d->W, EG), dim3(CB), 0, st, d->W, P.c0[4], work, part);
+    hipLaunchKernelGGL(k_errors_fold2, col_grid(d->W, 1), dim3(CB), 0, st, d->W, d->m, s_max, n_bounds, part, out);
     return check_launch("ato_ipm_errors");
 }
 

@@ -12,9 +12,10 @@ import numpy as np
 from aircraft_trajectory_optimization_amd.raceline.problem import ProblemSpec
 
 
-def perturbed_warm_starts(spec: ProblemSpec, B: int, seeds=None):
+def perturbed_warm_starts(spec: ProblemSpec, B: int, seeds=None, scale: float = 1.0):
     ''' (W [B, nw], LBW [B, nw], UBW [B, nw]) around spec.w0; seeds (default 0..B-1): instance i draws
-    from default_rng(seeds[i]), seed 0 is the unperturbed warm start '''
+    from default_rng(seeds[i]), seed 0 is the unperturbed warm start; scale multiplies every
+    perturbation amplitude (0.05 relative / 0.05 m at scale 1) '''
     seeds = list(range(B)) if seeds is None else list(seeds)
     N, P, nv = spec.N, spec.P, spec.nv
     node = N + np.arange(P) * nv
@@ -27,11 +28,11 @@ def perturbed_warm_starts(spec: ProblemSpec, B: int, seeds=None):
         if seeds[b] == 0:
             continue
         rng = np.random.default_rng(seeds[b])
-        W[b, :N] *= rng.uniform(0.95, 1.05, N)
+        W[b, :N] *= (1 + scale * rng.uniform(-0.05, 0.05, N))
         if spec.param:
-            W[b, node + 1] += rng.normal(0.0, 0.05, P)
-            W[b, node + 2] += rng.normal(0.0, 0.05, P)
-        W[b, (node[:, None] + iv + np.arange(3)).reshape(-1)] *= np.repeat(rng.uniform(0.95, 1.05, P), 3)
+            W[b, node + 1] += scale * rng.normal(0.0, 0.05, P)
+            W[b, node + 2] += scale * rng.normal(0.0, 0.05, P)
+        W[b, (node[:, None] + iv + np.arange(3)).reshape(-1)] *= np.repeat(1 + scale * rng.uniform(-0.05, 0.05, P), 3)
         W[b] = np.clip(W[b], LBW[b], UBW[b])
     return W, LBW, UBW
 
@@ -55,3 +56,68 @@ def warm_started_batch(B: int, device=None, seeds=None, **kw):
     W, LBW, UBW = perturbed_warm_starts(spec, B, seeds)
     return spec, W, LBW, UBW, float(x[:pspec.N].sum())
 
+
+
+def corridor_bounds(spec: ProblemSpec, seeds, lbw=None, ubw=None):
+    '''
+    Per-instance corridors (build-defined; config 5's batch): seed 0 keeps the track's tube, seed b > 0
+    bounds the lateral offset y of every node (parametric frame) by +-w_b(s), a half-width
+    w_b = U[0.8, 1.3] m modulated along the lap by 0.1 m * sin(2 pi k_b s / L + phi_b), k_b in {1, 2, 3}.
+    Returns (LBW [B, nw], UBW [B, nw]) from spec's (or the given) bounds.
+    '''
+    if not spec.param:
+        raise ValueError('corridor instances need the parametric frame (lateral offset y)')
+    seeds = list(seeds)
+    B = len(seeds)
+    lbw = spec.lbw if lbw is None else lbw
+    ubw = spec.ubw if ubw is None else ubw
+    LBW = np.repeat(np.asarray(lbw, float)[None], B, axis=0) if np.ndim(lbw) == 1 else np.array(lbw, float)
+    UBW = np.repeat(np.asarray(ubw, float)[None], B, axis=0) if np.ndim(ubw) == 1 else np.array(ubw, float)
+    node = spec.N + np.arange(spec.P) * spec.nv
+    s = np.array([spec.get_s(n, k) for n in range(spec.N) for k in range(spec.K1)])
+    L = spec.line.s_max() - spec.line.s_min()
+    for b, sd in enumerate(seeds):
+        if sd == 0:
+            continue
+        rng = np.random.default_rng(sd)
+        w0, k, ph = rng.uniform(0.8, 1.3), rng.integers(1, 4), rng.uniform(0, 2 * np.pi)
+        w = w0 + 0.1 * np.sin(2 * np.pi * k * (s - spec.line.s_min()) / L + ph)
+        LBW[b, node + 1] = np.maximum(LBW[b, node + 1], -w)
+        UBW[b, node + 1] = np.minimum(UBW[b, node + 1], w)
+    return LBW, UBW
+
+
+def corridor_batch(B: int, device=None, seeds=None, progress: int = 0, **kw):
+    '''
+    B drone instances over per-instance corridors (corridor_bounds) of a parametric scenario (make_spec
+    keywords, e.g. track='fig8', use_dcm=True: config 5's batch), each warm-started the reference's way
+    (use_ws, drone_raceline.py:158-274) from ITS OWN point-mass raceline: one batched point-mass solve on
+    the device over the B corridors, then the drone guesses of all of them (drone_guess_batch).
+    Returns (drone spec, W, LBW, UBW, point-mass statuses, point-mass lap times [B]); the drone bounds
+    carry the instance's corridor and the guess's step-size bounds. Instances whose point-mass solve did
+    not converge keep that guess anyway (their status is returned).
+    '''
+    from aircraft_trajectory_optimization_amd.raceline.warmstart import drone_guess_batch
+    from aircraft_trajectory_optimization_amd.solver.batched_ipm import device_solver
+    from aircraft_trajectory_optimization_amd.solver.ipm import IPMOptions
+    from aircraft_trajectory_optimization_amd.tracks import make_spec
+    seeds = list(range(B)) if seeds is None else list(seeds)
+    pspec = make_spec(**{**kw, 'model': 'point', 'use_quat': False, 'use_dcm': False})
+    PL, PU = corridor_bounds(pspec, seeds)
+    psolver = device_solver(pspec, B, PL, PU, IPMOptions(max_iter=1000), device=device)
+    pres = psolver.solve(np.repeat(pspec.w0[None], B, axis=0), progress=progress)
+    XP = pres.x.T.cpu().numpy()
+    if hasattr(psolver.kkt, 'close'):
+        psolver.kkt.close()
+    del psolver
+    spec = make_spec(**{**kw, 'model': 'drone'})
+    if spec.vehicle.use_quat and not spec.use_dcm:
+        raise NotImplementedError('corridor_batch: one closure sign per batch (DCM or Euler poses)')
+    W, LBW, UBW, _, wraps = drone_guess_batch(spec, pspec, XP)
+    if np.any(wraps != wraps[0]):
+        raise NotImplementedError('corridor_batch: Euler wraps differ between instances')
+    if wraps[0]:
+        spec = make_spec(**{**kw, 'model': 'drone', 'euler_wraps': float(wraps[0])})
+    LBW, UBW = corridor_bounds(spec, seeds, LBW, UBW)
+    W = np.clip(W, LBW, UBW)
+    return spec, W, LBW, UBW, list(pres.status), XP[:, :pspec.N].sum(1)

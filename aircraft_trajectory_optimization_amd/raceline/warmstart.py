@@ -100,3 +100,81 @@ def drone_guess(drone: ProblemSpec, point: ProblemSpec, x_point: np.ndarray) \
     quat_flip = bool(veh.use_quat and not dcm and closed and np.linalg.norm(first_r - last_r) > 1)
     wraps = float(np.round((last_r - first_r)[0] / 2 / np.pi)) if (closed and not veh.use_quat and not dcm) else 0.0
     return w0, lbw, ubw, quat_flip, wraps
+
+
+def drone_guess_batch(drone: ProblemSpec, point: ProblemSpec, XP: np.ndarray):
+    '''
+    drone_guess for B point-mass solutions XP [B, point.nw] at once (vectorised over the instances,
+    node by node as drone_guess): (W [B, nw], LBW [B, nw], UBW [B, nw], quat_flip [B], euler_wraps [B]).
+    Equal to drone_guess applied to every row (tests/test_corridor_cpu.py).
+    '''
+    if (drone.N, drone.K) != (point.N, point.K):
+        raise ValueError('warm start needs the same discretisation')
+    XP = np.atleast_2d(np.asarray(XP, float))
+    B = XP.shape[0]
+    veh: DroneConfig = drone.vehicle
+    closed = bool(drone.config.closed)
+    dcm = bool(getattr(veh, 'use_dcm', False))
+    N, K1 = drone.N, drone.K1
+    W = np.repeat(drone.w0[None], B, axis=0)
+    LBW = np.repeat(drone.lbw[None], B, axis=0)
+    UBW = np.repeat(drone.ubw[None], B, axis=0)
+    h = XP[:, :N]
+    W[:, :N], LBW[:, :N], UBW[:, :N] = h, h / 100, h * 10
+    first_r = last_r = None
+    ez = np.array([0., 0., 1.])
+    for n in range(N):
+        for k in range(K1):
+            pi = point.N + (n * K1 + k) * point.nv
+            zp, up, dup = XP[:, pi:pi + 6], XP[:, pi + 6:pi + 9], XP[:, pi + 9:pi + 12]
+            Rw = _point_frame(point, n, k)
+            T, vg, dT = up @ Rw.T, zp[:, 3:6] @ Rw.T, dup @ Rw.T
+            Tn = np.linalg.norm(T, axis=1)
+            if closed:
+                e1 = vg / np.linalg.norm(vg, axis=1)[:, None]
+                e3 = T / Tn[:, None]
+                e1 = e1 - e3 * np.sum(e1 * e3, axis=1)[:, None]
+                e1 = e1 / np.linalg.norm(e1, axis=1)[:, None]
+                e2 = np.cross(e3, e1)
+                R = np.stack([e1, e2, e3], axis=2)                     # columns e1 e2 e3
+            else:
+                t = T / Tn[:, None]
+                v = -np.cross(t, ez)
+                s = np.linalg.norm(v, axis=1)
+                c = t @ ez
+                hat = np.zeros((B, 3, 3))
+                hat[:, 0, 1], hat[:, 0, 2], hat[:, 1, 2] = -v[:, 2], v[:, 1], -v[:, 0]
+                hat[:, 1, 0], hat[:, 2, 0], hat[:, 2, 1] = v[:, 2], -v[:, 1], v[:, 0]
+                R = np.eye(3)[None] + hat + (hat @ hat) * ((1 - c) / s ** 2)[:, None, None]
+            if not veh.global_r:
+                R = drone.line.p2Rp(drone.get_s(n, k)).T[None] @ R
+            if dcm:
+                r = R.reshape(B, 9)
+            elif veh.use_quat:
+                r = Rotation.from_matrix(R).as_quat()
+                if last_r is not None:
+                    flip = np.linalg.norm(r - last_r, axis=1) >= 1
+                    r[flip] = -r[flip]
+            else:
+                r = np.flip(Rotation.from_matrix(R).as_euler('xyz', degrees=False), axis=1).copy()
+                if last_r is not None:
+                    far = np.linalg.norm(r - last_r, axis=1) > 1
+                    d0 = r[:, 0] - last_r[:, 0]
+                    r[far & (d0 > np.pi), 0] -= 2 * np.pi
+                    r[far & ~(d0 > np.pi) & (d0 <= -np.pi), 0] += 2 * np.pi
+                    if np.any(far & (np.linalg.norm(r - last_r, axis=1) > 1)):
+                        raise NotImplementedError('Warmstart continuity failed for euler angles, try quaternion')
+            if first_r is None:
+                first_r = r
+            last_r = r
+            vb = np.einsum('bji,bj->bi', R, vg)
+            wb = np.einsum('bji,bj->bi', R, np.cross(T, dT)) / (Tn ** 2)[:, None]
+            di = drone.N + (n * K1 + k) * drone.nv
+            W[:, di:di + drone.nz] = np.concatenate([zp[:, :3], r, vb, wb], axis=1)
+            W[:, di + drone.nz:di + drone.nz + 4] = (Tn / 4)[:, None]
+            W[:, di + drone.nz + 4:di + drone.nz + 8] = 0.0
+    quat_flip = (np.zeros(B, bool) if (dcm or not veh.use_quat or not closed)
+                 else np.linalg.norm(first_r - last_r, axis=1) > 1)
+    wraps = (np.round((last_r - first_r)[:, 0] / 2 / np.pi) if (closed and not veh.use_quat and not dcm)
+             else np.zeros(B))
+    return W, LBW, UBW, quat_flip, wraps

@@ -681,7 +681,11 @@ class BatchedInteriorPoint:
         storage); ok is False where no perturbation is left (no search direction).
         '''
         n, m, B = self.n, self.m, self.B
-        pend = act & ~pert.consider(act, mu)
+        dev_pert = self.vk is not None and hasattr(self.vk, 'perturb')
+        if dev_pert:      # the handler's state machine in one kernel per pass (ato_ipm_perturb)
+            pend = self.vk.perturb(0, pert, mu, act.clone())
+        else:
+            pend = act & ~pert.consider(act, mu)
         ok_all = torch.zeros(B, dtype=torch.bool, device=self.dev)
         sol = torch.zeros((n + m, B), dtype=torch.float64, device=self.dev)
         dw_out = torch.zeros(B, dtype=torch.float64, device=self.dev)
@@ -707,6 +711,11 @@ class BatchedInteriorPoint:
                 rec[0] += 1
                 rec[1] += len(pidx)
                 npass += 1
+                if dev_pert:
+                    self.vk.perturb(1, pert, mu, pend, inertia=inertia, dw_out=dw_out, dc_out=dc_out,
+                                    tosolve=tosolve, m=m)
+                    pidx = _idx(pend)
+                    continue
                 sing = pend & ((inertia[:, 2] > 0) | (inertia[:, 1] < m))
                 wrong = pend & ~sing & (inertia[:, 1] > m)
                 good = pend & ~sing & ~wrong
@@ -728,9 +737,12 @@ class BatchedInteriorPoint:
             okd = tosolve & fin
             sol = torch.where(okd[None, :], xs, sol)
             ok_all = ok_all | okd
-            bad = tosolve & ~fin                 # unrefinable solves count as singular matrices
-            tosolve = torch.zeros_like(tosolve)
-            pend = bad & ~pert.singular(bad, mu)
+            if dev_pert:                         # unrefinable solves count as singular matrices
+                self.vk.perturb(2, pert, mu, pend, tosolve=tosolve, fin=fin)
+            else:
+                bad = tosolve & ~fin
+                tosolve = torch.zeros_like(tosolve)
+                pend = bad & ~pert.singular(bad, mu)
             pidx = _idx(pend)
             if not len(pidx):
                 break

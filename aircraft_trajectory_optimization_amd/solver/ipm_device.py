@@ -173,3 +173,32 @@ class DeviceIPMKernels:
                                                    _p(out[0]), _p(out[1]), _p(out[2]), self._stream()),
                     'ato_ipm_filter_accept')
         return out[0], out[1], out[2]
+
+    def perturb(self, op, pert, mu, pend, inertia=None, dw_out=None, dc_out=None, tosolve=None, fin=None, m=0):
+        ''' one step of the per-column PDPerturbationHandler (ato_ipm_perturb, op 0 / 1 / 2 as in
+        include/ato_ipm.h) on the handler state `pert` (batched_ipm.py BatchedPerturbation, updated in
+        place); pend, tosolve: bool [W], updated in place; returns pend '''
+        W = mu.shape[0]
+        o = pert.o
+        key = ('pert', o.delta_w_0, o.delta_w_min, o.delta_w_max, o.kappa_w_minus, o.kappa_w_plus,
+               o.kappa_w_plus_bar, o.delta_c_base, o.kappa_c, o.degen_iters_max)
+        prm = self._prm.get(key)
+        if prm is None:
+            prm = self._prm[key] = np.array(key[1:], dtype=np.float64)
+        st = [pert.hdeg, pert.jdeg, pert.diters, pert.test]
+        fl = [pert.dx, pert.dc, pert.dx_last, pert.dc_last]
+        for t in st:
+            if t.dtype != torch.int64 or t.shape != (W,) or not t.is_contiguous():
+                raise ValueError('perturbation state: expected contiguous int64 [W]')
+        fl = [self._c(t, W) for t in fl]
+        for t in (pend, tosolve):
+            if t is not None and (t.dtype != torch.bool or t.shape != (W,) or not t.is_contiguous()):
+                raise ValueError('perturbation masks: expected contiguous bool [W]')
+        if op == 1 and (inertia is None or inertia.dtype != torch.int32 or inertia.shape[0] < W or
+                        not inertia.is_contiguous()):
+            raise ValueError('perturbation pass: expected int32 inertia [W, 3]')
+        self._check(self.lib.ato_ipm_perturb(int(op), W, int(m), prm.ctypes.data, *[_p(t) for t in st],
+                                             *[_p(t) for t in fl], _p(self._c(mu, W)), _p(pend),
+                                             _p(inertia), _p(dw_out), _p(dc_out), _p(tosolve), _p(fin),
+                                             self._stream()), 'ato_ipm_perturb')
+        return pend

@@ -254,12 +254,16 @@ def main():
         if world > 1:
             dist.barrier()
         if args.track == 'fig8':
-            # config 5 as a solve: the fig-8 drone (ESP or DCM pose) from perturbed point-mass warm starts
-            # (raceline/batch_instances.py), fp64 evaluation and KKT
-            from aircraft_trajectory_optimization_amd.raceline.batch_instances import warm_started_batch
+            # config 5 as a solve: the fig-8 drone (DCM or ESP pose) over per-instance corridors, each
+            # warm-started from its own point-mass raceline (raceline/batch_instances.py corridor_batch:
+            # one batched point-mass solve, before the timed solve), fp64 evaluation and KKT
+            from aircraft_trajectory_optimization_amd.raceline.batch_instances import corridor_batch
             from aircraft_trajectory_optimization_amd.solver.batched_ipm import device_solver
             wkw = {k: v for k, v in spec_kw.items() if k not in ('model',)}
-            spec, Wws, LBW, UBW, _ = warm_started_batch(len(seeds), device=dev, seeds=seeds, **wkw)
+            if args.pose == 'esp':
+                raise SystemExit('the fig-8 solve batch is the DCM pose (config 5): --pose dcm')
+            spec, Wws, LBW, UBW, _, _ = corridor_batch(len(seeds), device=dev, seeds=seeds,
+                                                        progress=args.progress, **wkw)
             sync()
             t0 = time.perf_counter()
             solver = device_solver(spec, len(seeds), LBW, UBW, IPMOptions(max_iter=args.max_iter), device=dev)
@@ -327,7 +331,8 @@ def main():
                 'scaling': 'weak',
                 'vs_baseline': None,
                 'dtype': 'f64',
-                'data': ('synthetic: perturbed point-mass warm starts (raceline/batch_instances.py)' if args.track == 'fig8'
+                'data': ('synthetic: seeded per-instance corridors, each warm-started from its own point-mass raceline '
+                         '(raceline/batch_instances.py corridor_batch)' if args.track == 'fig8'
                          else 'synthetic: seeded cold-start instances (SURVEY 8(d) config 3 generator, '
                               'raceline/instances.py)'),
                 'config': {'workload': f'{track}_parametric_{args.pose}_drone_colloc_N50_K4_'

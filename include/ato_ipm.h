@@ -105,6 +105,25 @@ int ato_ipm_filter_accept(int32_t W, int32_t fmax, const double* theta, const do
                           const int64_t* nf, const double* theta_max, const double* theta_min,
                           const uint8_t* pend, const uint8_t* first, const double* prm, uint8_t* ok,
                           uint8_t* arm, uint8_t* soc, void* stream);
+
+/* IPOPT's PDPerturbationHandler per column (IpPDPerturbationHandler: ConsiderNewSystem,
+ * PerturbForSingularity, PerturbForWrongInertia with the structural-degeneracy test; batched_ipm.py
+ * BatchedPerturbation) and the bookkeeping of an inertia-correction pass (batched_ipm.py _kkt_step),
+ * one thread per column. Handler state, device arrays [W]: hdeg, jdeg (0 unknown / 1 no / 2 yes),
+ * diters, test (0 none, 1 C0X0, 2 CPX0, 3 C0XP, 4 CPXP), dx, dc (delta_w, delta_c), dx_last, dc_last.
+ * pend [W] bytes 0/1, in/out. op 0 (new system): pend = columns to factorise, out: those that got a
+ * perturbation. op 1 (after a factorisation of the pend columns; inertia [W][3] int32 = (positive,
+ * negative, zero) eigenvalues, m constraint rows): a right inertia sets dw_out, dc_out = the column's
+ * deltas and tosolve = 1; a singular matrix (zero eigenvalues or fewer than m negative ones) or a
+ * wrong inertia (more than m negative) gets the next perturbation; out pend = columns to factorise
+ * again. op 2 (after the solves): columns with tosolve = 1 and fin = 0 (unrefinable solve) count as
+ * singular; tosolve is cleared, out pend as op 1. A column that runs out of perturbations (delta_w
+ * above max) leaves pend = 0 without tosolve. prm = HOST array {delta_w_0, delta_w_min, delta_w_max,
+ * kappa_w_minus, kappa_w_plus, kappa_w_plus_bar, delta_c_base, kappa_c, degen_iters_max}. */
+int ato_ipm_perturb(int32_t op, int32_t W, int32_t m, const double* prm, int64_t* hdeg, int64_t* jdeg,
+                    int64_t* diters, int64_t* test, double* dx, double* dc, double* dx_last, double* dc_last,
+                    const double* mu, uint8_t* pend, const int32_t* inertia, double* dw_out, double* dc_out,
+                    uint8_t* tosolve, const uint8_t* fin, void* stream);
 #ifdef __cplusplus
 }
 #endif

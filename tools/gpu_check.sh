@@ -133,6 +133,7 @@ for s in $STEPS; do
                    i=$((i+1))
                    ATO_KKT_S16_MIN=$v run solve_s16min${v}_$i 600 python tools/solve_batched.py --batch 512 --max-iter 200 --cold --no-host --out "$OUT/solve_s16min${v}_$i.json"
                done ;;
+        opcount) run opcount_device 300 python tools/diag/ipm_opcount.py --device -v ;;
         listpmc) run listpmc 120 rocprofv3 -L ;;
         mb)    run mb_store 120 ./tools/mb_store ;;
         tileab) for t in 0 8 16 4; do
