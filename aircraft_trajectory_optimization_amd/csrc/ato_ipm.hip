@@ -722,6 +722,82 @@ __global__ __launch_bounds__(CB) void k_perturb(int op, int W, int m, PertPrm o,
     pend[b] = p ? 1 : 0;
 }
 
+
+// ------------------------------------------------------------------------------------------
+// Termination tests of a lockstep iteration (batched_ipm.py solve, the `check` block) and the
+// monotone barrier update (MonotoneMuUpdate, the `barrier` loop), one thread per column.
+// ------------------------------------------------------------------------------------------
+enum { ST_OPTIMAL = 1, ST_ACCEPTABLE = 2, ST_MAX_ITER = 3, ST_TINY_STEP = 8 };
+
+struct StatusPrm {
+    double tol, dual_inf_tol, constr_viol_tol, compl_inf_tol, acceptable_tol;
+    long long acceptable_iter;
+};
+
+__global__ __launch_bounds__(CB) void k_status(int W, StatusPrm o, const double* __restrict__ E0,
+                                               const double* __restrict__ du, const double* __restrict__ pr_uns,
+                                               const double* __restrict__ co, const double* __restrict__ sf,
+                                               const long long* __restrict__ own, const long long* __restrict__ lim,
+                                               uint8_t* __restrict__ act, long long* __restrict__ n_acc,
+                                               long long* __restrict__ status) {
+    const int b = blockIdx.x * CB + threadIdx.x;
+    if (b >= W) return;
+    bool a = act[b] != 0;
+    long long st = status[b], na = n_acc[b];
+    const double e = E0[b];
+    if (a && e <= o.tol && du[b] / sf[b] <= o.dual_inf_tol && pr_uns[b] <= o.constr_viol_tol &&
+        co[b] <= o.compl_inf_tol) {
+        st = ST_OPTIMAL;
+        a = false;
+    }
+    na = (a && e <= o.acceptable_tol) ? na + 1 : 0;
+    if (a && na >= o.acceptable_iter) {
+        st = ST_ACCEPTABLE;
+        a = false;
+    }
+    if (a && own[b] >= lim[b]) {
+        st = ST_MAX_ITER;
+        a = false;
+    }
+    act[b] = a ? 1 : 0;
+    n_acc[b] = na;
+    status[b] = st;
+}
+
+struct BarrierPrm {
+    double kappa_eps, kappa_mu, theta_mu, mu_min, tau_min;
+};
+
+__global__ __launch_bounds__(CB) void k_barrier(int W, BarrierPrm o, const double* __restrict__ Emu,
+                                                uint8_t* __restrict__ mu_act, uint8_t* __restrict__ force,
+                                                uint8_t* __restrict__ act, long long* __restrict__ status,
+                                                double* __restrict__ mu, double* __restrict__ tau,
+                                                long long* __restrict__ nf, uint8_t* __restrict__ upd) {
+    const int b = blockIdx.x * CB + threadIdx.x;
+    if (b >= W) return;
+    const double m = mu[b];
+    const bool fo = force[b] != 0;
+    bool ma = mu_act[b] != 0;
+    const bool want = ma && ((Emu[b] <= o.kappa_eps * m) || fo);
+    const double a = o.kappa_mu * m, c = tpow(m, o.theta_mu);
+    const double mn = cmax(nmin(a, c), o.mu_min);             // torch.clamp(torch.minimum(.), min=)
+    const bool same = mn == m;
+    if (want && fo && same) {                                  // tiny step with mu at its floor
+        status[b] = ST_TINY_STEP;
+        act[b] = 0;
+        ma = false;
+    }
+    const bool u = want && !same;
+    if (u) {
+        mu[b] = mn;
+        tau[b] = cmax(1.0 - mn, o.tau_min);
+        nf[b] = 0;
+    }
+    mu_act[b] = ma ? 1 : 0;
+    force[b] = 0;
+    upd[b] = u ? 1 : 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -852,6 +928,34 @@ int ato_ipm_filter_accept(int32_t W, int32_t fmax, const double* theta, const do
                        fmax, theta, phi, gphi_d, alpha, tht, pht, F, nf, theta_max, theta_min, pend, first, o, ok,
                        arm, soc);
     return check_launch("ato_ipm_filter_accept");
+}
+
+int ato_ipm_status(int32_t W, const double* prm, const double* E0, const double* du, const double* pr_uns,
+                   const double* co, const double* sf, const int64_t* own, const int64_t* lim, uint8_t* act,
+                   int64_t* n_acc, int64_t* status, void* stream) {
+    if (W < 0 || !prm) return fail(ATO_ERR_ARG, "ato_ipm_status: arguments");
+    if (W == 0) return 0;
+    if (!E0 || !du || !pr_uns || !co || !sf || !own || !lim || !act || !n_acc || !status)
+        return fail(ATO_ERR_ARG, "ato_ipm_status: arguments");
+    const StatusPrm o{prm[0], prm[1], prm[2], prm[3], prm[4], (long long)prm[5]};
+    hipLaunchKernelGGL(k_status, dim3((W + CB - 1) / CB), dim3(CB), 0, static_cast<hipStream_t>(stream), W, o, E0, du,
+                       pr_uns, co, sf, reinterpret_cast<const long long*>(own),
+                       reinterpret_cast<const long long*>(lim), act, reinterpret_cast<long long*>(n_acc),
+                       reinterpret_cast<long long*>(status));
+    return check_launch("ato_ipm_status");
+}
+
+int ato_ipm_barrier(int32_t W, const double* prm, const double* Emu, uint8_t* mu_act, uint8_t* force, uint8_t* act,
+                    int64_t* status, double* mu, double* tau, int64_t* nf, uint8_t* upd, void* stream) {
+    if (W < 0 || !prm) return fail(ATO_ERR_ARG, "ato_ipm_barrier: arguments");
+    if (W == 0) return 0;
+    if (!Emu || !mu_act || !force || !act || !status || !mu || !tau || !nf || !upd)
+        return fail(ATO_ERR_ARG, "ato_ipm_barrier: arguments");
+    const BarrierPrm o{prm[0], prm[1], prm[2], prm[3], prm[4]};
+    hipLaunchKernelGGL(k_barrier, dim3((W + CB - 1) / CB), dim3(CB), 0, static_cast<hipStream_t>(stream), W, o, Emu,
+                       mu_act, force, act, reinterpret_cast<long long*>(status), mu, tau,
+                       reinterpret_cast<long long*>(nf), upd);
+    return check_launch("ato_ipm_barrier");
 }
 
 }  // extern "C"

@@ -312,6 +312,8 @@ ATO_HD void qnormalize(const T* q, T* qh, T& inv_norm) {
 //                 contracts the orthonormality error quadratically, so the Gauss-Legendre
 //                 collocation, which conserves R^T R inside an interval, keeps every interval on
 //                 SO(3) -- the analogue of the quaternion's normalisation, with no extra rows.
+//                 (Round 5 measured the alternative of P at the closure only, identity continuity
+//                 rows: fewer DCM instances converge)
 //   others (NO = 0): the identity.
 // v[a] = op(r)_a, jac(a, m) = d op(r)_a / d r_m (every (a, m) is structural).
 template <class M, class T, int KIND = M::HAS_QUAT ? 1 : (M::HAS_DCM ? 2 : 0)>

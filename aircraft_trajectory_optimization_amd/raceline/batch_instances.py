@@ -111,13 +111,12 @@ def corridor_batch(B: int, device=None, seeds=None, progress: int = 0, **kw):
         psolver.kkt.close()
     del psolver
     spec = make_spec(**{**kw, 'model': 'drone'})
-    if spec.vehicle.use_quat and not spec.use_dcm:
-        raise NotImplementedError('corridor_batch: one closure sign per batch (DCM or Euler poses)')
-    W, LBW, UBW, _, wraps = drone_guess_batch(spec, pspec, XP)
-    if np.any(wraps != wraps[0]):
-        raise NotImplementedError('corridor_batch: Euler wraps differ between instances')
-    if wraps[0]:
-        spec = make_spec(**{**kw, 'model': 'drone', 'euler_wraps': float(wraps[0])})
+    W, LBW, UBW, flips, wraps = drone_guess_batch(spec, pspec, XP)
+    if np.any(flips != flips[0]) or np.any(wraps != wraps[0]):
+        # the closure sign / Euler wraps are structural constants of the NLP: one per batch
+        raise NotImplementedError('corridor_batch: closure signs or Euler wraps differ between instances')
+    if flips[0] or wraps[0]:
+        spec = make_spec(**{**kw, 'model': 'drone', 'quat_flip': bool(flips[0]), 'euler_wraps': float(wraps[0])})
     LBW, UBW = corridor_bounds(spec, seeds, LBW, UBW)
     W = np.clip(W, LBW, UBW)
     return spec, W, LBW, UBW, list(pres.status), XP[:, :pspec.N].sum(1)

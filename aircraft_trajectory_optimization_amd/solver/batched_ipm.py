@@ -963,17 +963,21 @@ class BatchedInteriorPoint:
                 stp = act & (own > 0) & stop_check(x, s)
                 status = torch.where(stp, torch.full_like(status, STOPPED), status)
                 act = act & ~stp
-            conv = act & (E0 <= o.tol) & (du / sf <= o.dual_inf_tol) & (pr_uns <= o.constr_viol_tol) & \
-                (co <= o.compl_inf_tol)
-            status = torch.where(conv, torch.full_like(status, OPTIMAL), status)
-            act = act & ~conv
-            n_acc = torch.where(act & (E0 <= o.acceptable_tol), n_acc + 1, torch.zeros_like(n_acc))
-            accd = act & (n_acc >= o.acceptable_iter)
-            status = torch.where(accd, torch.full_like(status, ACCEPTABLE), status)
-            act = act & ~accd
-            mx = act & (own >= self.lim)
-            status = torch.where(mx, torch.full_like(status, MAX_ITER), status)
-            act = act & ~mx
+            if self.vk is not None:        # one launch (ato_ipm_status), on private copies
+                act, n_acc, status = act.clone(), n_acc.clone(), status.clone()
+                self.vk.status(o, E0, du, pr_uns, co, sf, own, self.lim, act, n_acc, status)
+            else:
+                conv = act & (E0 <= o.tol) & (du / sf <= o.dual_inf_tol) & (pr_uns <= o.constr_viol_tol) & \
+                    (co <= o.compl_inf_tol)
+                status = torch.where(conv, torch.full_like(status, OPTIMAL), status)
+                act = act & ~conv
+                n_acc = torch.where(act & (E0 <= o.acceptable_tol), n_acc + 1, torch.zeros_like(n_acc))
+                accd = act & (n_acc >= o.acceptable_iter)
+                status = torch.where(accd, torch.full_like(status, ACCEPTABLE), status)
+                act = act & ~accd
+                mx = act & (own >= self.lim)
+                status = torch.where(mx, torch.full_like(status, MAX_ITER), status)
+                act = act & ~mx
             n_step, n_wt = torch.stack([act.sum(), waiting.sum()]).tolist()     # one synchronisation
             any_act, any_wait = n_step > 0, n_wt > 0
             if not any_act and not any_wait and not inflight:
@@ -996,26 +1000,31 @@ class BatchedInteriorPoint:
                 tiny_flag = tiny_flag & False
                 mu_act = act if resto_init is None else act & (own > 0)
                 force = force & mu_act
+                if self.vk is not None:            # the update runs in place (ato_ipm_barrier): private copies
+                    mu_act, act, status, mu, tau, nf = (t.clone() for t in (mu_act, act, status, mu, tau, nf))
                 for _ in range(100):
                     if self.vk is not None:
                         Emu = self.vk.errors(self._bd(), x, s, g, self.c_rhs, sg, y, zl, zu, vl, vu, dual_x, mu,
                                              self.n_bounds, o.s_max)[0]
+                        upd = self.vk.barrier(o, Emu, mu_act, force, act, status, mu, tau, nf)
+                        if not bool(upd.any()):
+                            break
                     else:
                         Emu = self._errors(dual_x, g, x, s, y, zl, zu, vl, vu, mu)[0]
-                    want = mu_act & ((Emu <= o.kappa_eps * mu) | force)
-                    mu_new = torch.clamp(torch.minimum(o.kappa_mu * mu, mu ** o.theta_mu), min=o.mu_min)
-                    same = mu_new == mu
-                    tstop = want & force & same
-                    status = torch.where(tstop, torch.full_like(status, TINY_STEP), status)
-                    act = act & ~tstop
-                    mu_act = mu_act & ~tstop
-                    upd = want & ~same
-                    force = force & False
-                    if not bool(upd.any()):
-                        break
-                    mu = torch.where(upd, mu_new, mu)
-                    tau = torch.where(upd, torch.clamp(1.0 - mu, min=o.tau_min), tau)
-                    nf = torch.where(upd, torch.zeros_like(nf), nf)
+                        want = mu_act & ((Emu <= o.kappa_eps * mu) | force)
+                        mu_new = torch.clamp(torch.minimum(o.kappa_mu * mu, mu ** o.theta_mu), min=o.mu_min)
+                        same = mu_new == mu
+                        tstop = want & force & same
+                        status = torch.where(tstop, torch.full_like(status, TINY_STEP), status)
+                        act = act & ~tstop
+                        mu_act = mu_act & ~tstop
+                        upd = want & ~same
+                        force = force & False
+                        if not bool(upd.any()):
+                            break
+                        mu = torch.where(upd, mu_new, mu)
+                        tau = torch.where(upd, torch.clamp(1.0 - mu, min=o.tau_min), tau)
+                        nf = torch.where(upd, torch.zeros_like(nf), nf)
                     if hasattr(self.ev, 'set_mu'):
                         # the restoration objective depends on the barrier parameter (proximity weight
                         # sqrt(mu), solver/ipm.py): f and its gradient at the current point for the new mu

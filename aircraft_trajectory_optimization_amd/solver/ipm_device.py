@@ -202,3 +202,43 @@ class DeviceIPMKernels:
                                              _p(inertia), _p(dw_out), _p(dc_out), _p(tosolve), _p(fin),
                                              self._stream()), 'ato_ipm_perturb')
         return pend
+
+    def _host_prm(self, key):
+        prm = self._prm.get(key)
+        if prm is None:
+            prm = self._prm[key] = np.array(key[1:], dtype=np.float64)
+        return prm
+
+    def _own(self, t, dtype, W, what):
+        if t.dtype != dtype or t.shape != (W,) or not t.is_contiguous() or t.device != self.device:
+            raise ValueError(f'{what}: expected a contiguous {dtype} [{W}] tensor on {self.device}')
+        return t
+
+    def status(self, o, E0, du, pr_uns, co, sf, own, lim, act, n_acc, status):
+        ''' termination tests (ato_ipm_status), in place on act (bool), n_acc and status (int64) '''
+        W = E0.shape[0]
+        prm = self._host_prm(('status', o.tol, o.dual_inf_tol, o.constr_viol_tol, o.compl_inf_tol,
+                              o.acceptable_tol, o.acceptable_iter))
+        cols = [self._c(t, W) for t in (E0, du, pr_uns, co, sf)]
+        ints = [self._own(t, torch.int64, W, 'status') for t in (own, lim)]
+        self._own(act, torch.bool, W, 'status act')
+        for t in (n_acc, status):
+            self._own(t, torch.int64, W, 'status')
+        self._check(self.lib.ato_ipm_status(W, prm.ctypes.data, *[_p(t) for t in cols], *[_p(t) for t in ints],
+                                            _p(act), _p(n_acc), _p(status), self._stream()), 'ato_ipm_status')
+
+    def barrier(self, o, Emu, mu_act, force, act, status, mu, tau, nf):
+        ''' one monotone barrier-update pass (ato_ipm_barrier), in place; returns upd (bool [W]) '''
+        W = Emu.shape[0]
+        prm = self._host_prm(('barrier', o.kappa_eps, o.kappa_mu, o.theta_mu, o.mu_min, o.tau_min))
+        for t in (mu_act, force, act):
+            self._own(t, torch.bool, W, 'barrier mask')
+        for t in (status, nf):
+            self._own(t, torch.int64, W, 'barrier')
+        for t in (mu, tau):
+            self._own(t, torch.float64, W, 'barrier')
+        upd = torch.empty(W, dtype=torch.bool, device=self.device)
+        self._check(self.lib.ato_ipm_barrier(W, prm.ctypes.data, _p(self._c(Emu, W)), _p(mu_act), _p(force), _p(act),
+                                             _p(status), _p(mu), _p(tau), _p(nf), _p(upd), self._stream()),
+                    'ato_ipm_barrier')
+        return upd

@@ -124,6 +124,24 @@ int ato_ipm_perturb(int32_t op, int32_t W, int32_t m, const double* prm, int64_t
                     int64_t* diters, int64_t* test, double* dx, double* dc, double* dx_last, double* dc_last,
                     const double* mu, uint8_t* pend, const int32_t* inertia, double* dw_out, double* dc_out,
                     uint8_t* tosolve, const uint8_t* fin, void* stream);
+/* Termination tests of a lockstep iteration (batched_ipm.py solve; IPOPT's ConvergenceCheck with the
+ * acceptable-level counter), one thread per column, in place: act [W] bytes; n_acc, status [W] int64
+ * (1 optimal, 2 acceptable, 3 max_iter; others unchanged). A column still active is optimal when
+ * E0 <= tol, du / sf <= dual_inf_tol, pr_uns <= constr_viol_tol and co <= compl_inf_tol; otherwise its
+ * n_acc counts consecutive E0 <= acceptable_tol and acceptable_iter of them make it acceptable; then
+ * own >= lim ends it at max_iter. prm = HOST {tol, dual_inf_tol, constr_viol_tol, compl_inf_tol,
+ * acceptable_tol, acceptable_iter}. E0, du, pr_uns, co, sf fp64 [W]; own, lim int64 [W]. */
+int ato_ipm_status(int32_t W, const double* prm, const double* E0, const double* du, const double* pr_uns,
+                   const double* co, const double* sf, const int64_t* own, const int64_t* lim, uint8_t* act,
+                   int64_t* n_acc, int64_t* status, void* stream);
+
+/* One pass of the monotone barrier update (IPOPT MonotoneMuUpdate; batched_ipm.py solve), in place:
+ * a column of mu_act wants a decrease when Emu <= kappa_eps mu or force; mu_new = max(min(kappa_mu mu,
+ * mu^theta_mu), mu_min). A forced column whose mu cannot fall ends (status 8 tiny step, act = mu_act = 0);
+ * otherwise a wanted change sets mu, tau = max(1 - mu, tau_min), nf = 0 and upd = 1 (else upd = 0);
+ * force is cleared. prm = HOST {kappa_eps, kappa_mu, theta_mu, mu_min, tau_min}. */
+int ato_ipm_barrier(int32_t W, const double* prm, const double* Emu, uint8_t* mu_act, uint8_t* force, uint8_t* act,
+                    int64_t* status, double* mu, double* tau, int64_t* nf, uint8_t* upd, void* stream);
 #ifdef __cplusplus
 }
 #endif

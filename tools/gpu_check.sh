@@ -134,6 +134,9 @@ for s in $STEPS; do
                    ATO_KKT_S16_MIN=$v run solve_s16min${v}_$i 600 python tools/solve_batched.py --batch 512 --max-iter 200 --cold --no-host --out "$OUT/solve_s16min${v}_$i.json"
                done ;;
         opcount) run opcount_device 300 python tools/diag/ipm_opcount.py --device -v ;;
+        c5ab)  run c5_dcm 600 python -u tools/solve_config5.py --batch ${B5:-1024} --out "$OUT/c5_dcm.json"
+               ATO_LIB_PATH=$PWD/tools/diag/_lib/libato_dcmPm.so run c5_dcm_Pmodel 600 python -u tools/solve_config5.py --batch ${B5:-1024} --out "$OUT/c5_dcm_Pmodel.json" ;;
+        c5esp) run c5_esp 600 python -u tools/solve_config5.py --batch ${B5:-1024} --pose esp --out "$OUT/c5_esp.json" ;;
         listpmc) run listpmc 120 rocprofv3 -L ;;
         mb)    run mb_store 120 ./tools/mb_store ;;
         tileab) for t in 0 8 16 4; do

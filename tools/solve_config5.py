@@ -1,0 +1,63 @@
+'''
+Config 5's batched DCM solve on one GPU (raceline/batch_instances.py corridor_batch: per-instance
+corridors, each warm-started from its own point-mass raceline), as a standalone run for A/B work:
+
+    python tools/solve_config5.py --batch 1024 [--pose dcm|esp] [--out FILE.json]
+    ATO_LIB_PATH=tools/diag/_lib/libato_dcmP.so python tools/solve_config5.py ...   (a library variant)
+'''
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--batch', type=int, default=1024)
+    ap.add_argument('--pose', choices=['dcm', 'esp'], default='dcm')
+    ap.add_argument('--max-iter', type=int, default=1000)
+    ap.add_argument('--seed0', type=int, default=0)
+    ap.add_argument('--out', default=None)
+    a = ap.parse_args()
+    from aircraft_trajectory_optimization_amd.raceline.batch_instances import corridor_batch
+    from aircraft_trajectory_optimization_amd.solver.batched_ipm import device_solver
+    from aircraft_trajectory_optimization_amd.solver.ipm import IPMOptions
+    B = a.batch
+    kw = dict(track='fig8', frame='parametric', N=50, K=4, use_quat=a.pose == 'esp', global_r=True,
+              use_dcm=a.pose == 'dcm')
+    if a.pose == 'esp':
+        kw['use_quat'] = True
+    t0 = time.time()
+    spec, W, LBW, UBW, pst, plap = corridor_batch(B, seeds=range(a.seed0, a.seed0 + B), **kw)
+    t_point = time.time() - t0
+    print(f'point-mass solves {t_point:.1f} s', {s: pst.count(s) for s in set(pst)}, flush=True)
+    t0 = time.time()
+    solver = device_solver(spec, B, LBW, UBW, IPMOptions(max_iter=a.max_iter))
+    res = solver.solve(W, progress=20)
+    torch.cuda.synchronize()
+    t = time.time() - t0
+    st = list(res.status)
+    ok = [b for b, s in enumerate(st) if s in ('optimal', 'acceptable')]
+    laps = res.x[:spec.N].sum(0).cpu().numpy()
+    out = {'batch': B, 'pose': a.pose, 'library': os.environ.get('ATO_LIB_PATH', 'in-tree'),
+           'statuses': {s: st.count(s) for s in sorted(set(st))}, 'solve_s': t, 'point_solve_s': t_point,
+           'iterations_median': float(np.median(res.iters)), 'instance_iterations': int(np.sum(res.iters)),
+           'iterations_per_s': float(np.sum(res.iters)) / t, 'lockstep_iterations': len(solver.history),
+           'restorations': res.stats.get('restorations'),
+           'lap_converged': [float(laps[ok].min()), float(np.median(laps[ok])), float(laps[ok].max())] if ok else None,
+           'point_lap': [float(plap.min()), float(plap.max())],
+           'status_list': st}
+    print(json.dumps({k: v for k, v in out.items() if k != 'status_list'}), flush=True)
+    if a.out:
+        with open(a.out, 'w') as f:
+            json.dump(out, f)
+
+
+if __name__ == '__main__':
+    main()
