@@ -179,40 +179,9 @@ struct AttYPR {
 // with the kinematics R' = R [w]x. R(r) is the identity map, so every force / pose term the ESP
 // model builds from R(q) is reused unchanged. Orthonormality is carried by the continuity operator
 // (ato_program.hpp AttOp: the analogue of the reference's quaternion normalisation).
-#ifndef ATO_DCM_MODEL_P
-#define ATO_DCM_MODEL_P 0
-#endif
 struct AttDCM {
     static constexpr int NR = 9;
 
-#if ATO_DCM_MODEL_P
-    // DIAGNOSTIC build: the model's rotation is P(r) = r (3 I - r^T r) / 2 instead of r
-    template <class T>
-    ATO_HD static void R(const T* r, T* Rm) {
-        T S[9];
-        for (int i = 0; i < 3; ++i)
-            for (int j = 0; j < 3; ++j) S[i * 3 + j] = r[i] * r[j] + r[3 + i] * r[3 + j] + r[6 + i] * r[6 + j];
-        for (int i = 0; i < 3; ++i)
-            for (int j = 0; j < 3; ++j)
-                Rm[i * 3 + j] = T(1.5) * r[i * 3 + j] -
-                                T(0.5) * (r[i * 3] * S[j] + r[i * 3 + 1] * S[3 + j] + r[i * 3 + 2] * S[6 + j]);
-    }
-
-    template <class T>
-    ATO_HD static void dR(const T* r, const T*, int m, T* out) {
-        const int a = m / 3, b = m % 3;
-        for (int i = 0; i < 3; ++i)
-            for (int j = 0; j < 3; ++j) {
-                T acc = r[i * 3 + b] * r[a * 3 + j];
-                if (i == a) acc += r[b] * r[j] + r[3 + b] * r[3 + j] + r[6 + b] * r[6 + j];
-                if (j == b) acc += r[3 * i] * r[3 * a] + r[3 * i + 1] * r[3 * a + 1] + r[3 * i + 2] * r[3 * a + 2];
-                T o = T(-0.5) * acc;
-                if (i == a && j == b) o += T(1.5);
-                out[i * 3 + j] = o;
-            }
-    }
-    static constexpr bool R_dep(int, int, int) { return true; }
-#else
     template <class T>
     ATO_HD static void R(const T* r, T* Rm) {
         for (int i = 0; i < 9; ++i) Rm[i] = r[i];
@@ -223,7 +192,6 @@ struct AttDCM {
         for (int i = 0; i < 9; ++i) out[i] = T(i == m ? 1 : 0);
     }
     static constexpr bool R_dep(int row, int col, int m) { return m == row * 3 + col; }
-#endif
 
     // (R [w]x)_i0 = R_i1 w2 - R_i2 w1, _i1 = R_i2 w0 - R_i0 w2, _i2 = R_i0 w1 - R_i1 w0
     template <class T>
