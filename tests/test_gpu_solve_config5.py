@@ -28,6 +28,8 @@ CFG = dict(track='fig8', model='drone', frame='parametric', N=50, K=4, use_quat=
 
 
 def _corridor_solve(use_dcm, progress):
+    import os
+    import threading
     import time
     from aircraft_trajectory_optimization_amd.raceline.batch_instances import corridor_batch
     from aircraft_trajectory_optimization_amd.solver.batched_ipm import device_solver
@@ -39,10 +41,17 @@ def _corridor_solve(use_dcm, progress):
     assert pst.count('optimal') == B
     t0 = time.time()
     solver = device_solver(spec, B, LBW, UBW, IPMOptions(max_iter=1000))
+    # a heartbeat on file descriptor 2 (not captured by pytest's sys capture): a runner that takes
+    # minutes of silence for a hang sees the solve alive
+    stop = threading.Event()
+    beat = threading.Thread(target=lambda: [os.write(2, b'[config 5 test] solving\n') for _ in iter(
+        lambda: stop.wait(30), True)], daemon=True)
+    beat.start()
     try:
         res = solver.solve(W, progress=progress)
         torch.cuda.synchronize()
     finally:
+        stop.set()
         solver.kkt.close()
         del solver
         torch.cuda.empty_cache()
