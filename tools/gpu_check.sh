@@ -137,6 +137,8 @@ for s in $STEPS; do
         c5ab)  run c5_dcm 600 python -u tools/solve_config5.py --batch ${B5:-1024} --out "$OUT/c5_dcm.json"
                ATO_LIB_PATH=$PWD/tools/diag/_lib/libato_dcmPm.so run c5_dcm_Pmodel 600 python -u tools/solve_config5.py --batch ${B5:-1024} --out "$OUT/c5_dcm_Pmodel.json" ;;
         c5esp) run c5_esp 600 python -u tools/solve_config5.py --batch ${B5:-1024} --pose esp --out "$OUT/c5_esp.json" ;;
+        cpcsolve) run cpc_dcm 500 python -u tools/solve_cpc.py --batch ${BC:-64} --out "$OUT/cpc_dcm.json"
+               run cpc_esp 500 python -u tools/solve_cpc.py --batch ${BC:-64} --pose esp --out "$OUT/cpc_esp.json" ;;
         listpmc) run listpmc 120 rocprofv3 -L ;;
         mb)    run mb_store 120 ./tools/mb_store ;;
         tileab) for t in 0 8 16 4; do

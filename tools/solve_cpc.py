@@ -1,0 +1,65 @@
+'''
+Config 5's CPC gate-progress formulation (build-side, Foehn et al. 2021; parity UNPINNED: the reference
+only displays a CPC CSV, utils/cpc_utils.py) as a batched solve on one GPU: the fig-8 drone in the global
+frame, progress variables lambda / mu / nu per node and waypoint with the relaxed complementarity of the
+formulation (mu_j |p - p_j|^2 <= nu_j, nu_j in [0, tol^2]: raceline/problem.py _cpc_block), from the
+spec's cold-start guess with seeded step-size perturbations (h * U[0.95, 1.05], seed 0 unperturbed).
+
+    python tools/solve_cpc.py --batch 64 [--pose dcm|esp] [--out FILE.json]
+'''
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--batch', type=int, default=64)
+    ap.add_argument('--pose', choices=['dcm', 'esp'], default='dcm')
+    ap.add_argument('--N', type=int, default=56)
+    ap.add_argument('--max-iter', type=int, default=1000)
+    ap.add_argument('--out', default=None)
+    a = ap.parse_args()
+    from aircraft_trajectory_optimization_amd.solver.batched_ipm import device_solver
+    from aircraft_trajectory_optimization_amd.solver.ipm import IPMOptions
+    from aircraft_trajectory_optimization_amd.tracks import make_spec
+    B = a.batch
+    spec = make_spec(track='fig8', model='drone', frame='global', N=a.N, K=4, use_quat=True, global_r=True,
+                     use_dcm=a.pose == 'dcm', cpc={'waypoints': None, 'tol': 0.3})
+    W = np.repeat(spec.w0[None], B, axis=0)
+    for b in range(1, B):
+        W[b, :spec.N] *= np.random.default_rng(b).uniform(0.95, 1.05, spec.N)
+    W = np.clip(W, spec.lbw, spec.ubw)
+    t0 = time.time()
+    solver = device_solver(spec, B, spec.lbw, spec.ubw, IPMOptions(max_iter=a.max_iter))
+    res = solver.solve(W, progress=50)
+    torch.cuda.synchronize()
+    t = time.time() - t0
+    st = list(res.status)
+    ok = [b for b, s in enumerate(st) if s in ('optimal', 'acceptable')]
+    x = res.x.cpu().numpy()
+    laps = x[:spec.N].sum(0)
+    out = {'batch': B, 'pose': a.pose, 'N': spec.N, 'waypoints': spec.cpc_m, 'nw': spec.nw,
+           'statuses': {s: st.count(s) for s in sorted(set(st))}, 'solve_s': t,
+           'iterations_median': float(np.median(res.iters)), 'restorations': res.stats.get('restorations'),
+           'lap_converged': [float(laps[ok].min()), float(np.median(laps[ok])), float(laps[ok].max())] if ok else None}
+    if ok:      # complementarity residual of the converged instances: max_j mu_j * |p - p_j|^2 - nu_j <= 0
+        M, P = spec.cpc_m, spec.P
+        b = ok[0]
+        prog = x[spec.cpc_off:, b].reshape(P, 3, M)
+        out['first_converged'] = {'instance': b, 'lambda_end': prog[-1, 0].tolist(), 'nu_max': float(prog[:, 2].max())}
+    print(json.dumps(out), flush=True)
+    if a.out:
+        with open(a.out, 'w') as f:
+            json.dump(out, f)
+
+
+if __name__ == '__main__':
+    main()
