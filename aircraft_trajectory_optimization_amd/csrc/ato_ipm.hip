@@ -529,7 +529,8 @@ __device__ __forceinline__ double tpow(double x, double e) {
 }
 
 struct FilterPrm {
-    double s_phi, s_theta, delta, eta_phi, gamma_theta, gamma_phi, obj_max_inc;
+    double s_phi, s_theta, delta, eta_phi, gamma_theta, gamma_phi, obj_max_inc, compare_tol;
+    long long max_filter_resets, filter_reset_trigger;
 };
 
 __global__ __launch_bounds__(CB) void k_filter_accept(int W, int fmax, const double* __restrict__ theta,
@@ -537,11 +538,13 @@ __global__ __launch_bounds__(CB) void k_filter_accept(int W, int fmax, const dou
                                                       const double* __restrict__ gphi_d,
                                                       const double* __restrict__ alpha,
                                                       const double* __restrict__ tht, const double* __restrict__ pht,
-                                                      const double* __restrict__ F, const int64_t* __restrict__ nf,
+                                                      const double* __restrict__ F, int64_t* __restrict__ nf,
                                                       const double* __restrict__ theta_max,
                                                       const double* __restrict__ theta_min,
                                                       const uint8_t* __restrict__ pend,
                                                       const uint8_t* __restrict__ first, FilterPrm o,
+                                                      int64_t* __restrict__ fr_n, int64_t* __restrict__ fr_cnt,
+                                                      uint8_t* __restrict__ fr_last,
                                                       uint8_t* __restrict__ ok_out, uint8_t* __restrict__ arm_out,
                                                       uint8_t* __restrict__ soc_out) {
     const int b = blockIdx.x * CB + threadIdx.x;
@@ -558,8 +561,12 @@ __global__ __launch_bounds__(CB) void k_filter_accept(int W, int fmax, const dou
     const double mgd = ngd != ngd ? ngd : (ngd < 0.0 ? 0.0 : ngd);      // torch.clamp(min=0): NaN stays
     const bool switching = (gd < 0.0) && (al * tpow(mgd, o.s_phi) > o.delta * tpow(th, o.s_theta));
     const bool arm_case = (th <= theta_min[b]) && switching;
-    const bool ok_arm = pt <= ph + (o.eta_phi * al) * gd;
-    const bool ok_suf = (tt <= (1.0 - o.gamma_theta) * th) || (pt <= ph - o.gamma_phi * th);
+    // IpUtils Compare_le(lhs, rhs, base): lhs - rhs <= compare_tol |base| (ArmijoHolds,
+    // IsAcceptableToCurrentIterate)
+    const double dp = pt - ph;
+    const bool ok_arm = dp - (o.eta_phi * al) * gd <= o.compare_tol * fabs(ph);
+    const bool ok_suf = (tt - (1.0 - o.gamma_theta) * th <= o.compare_tol * fabs(th)) ||
+                        (dp - (-o.gamma_phi * th) <= o.compare_tol * fabs(ph));
     // obj_max_inc (FilterLSAcceptor::CheckAcceptabilityOfTrialPoint): the barrier objective may not
     // grow by more than 10^obj_max_inc of its magnitude
     bool inc = false;
@@ -568,10 +575,41 @@ __global__ __launch_bounds__(CB) void k_filter_accept(int W, int fmax, const dou
         inc = log10(pt - ph) > o.obj_max_inc + base;
     }
     const bool pd = pend[b] != 0;
-    const bool ok = pd && !rej && !inc && !in_f && (arm_case ? ok_arm : ok_suf);
+    const bool it_ok = !inc && (arm_case ? ok_arm : ok_suf);
+    const bool ok = pd && !rej && it_ok && !in_f;
     ok_out[b] = ok ? 1 : 0;
     arm_out[b] = (ok && arm_case) ? 1 : 0;
     soc_out[b] = (pd && !ok && first[b] != 0 && tt >= th) ? 1 : 0;
+    // the filter reset heuristic of CheckAcceptabilityOfTrialPoint: a rejection by the current-iterate
+    // test clears "last rejection due to the filter", a rejection by the filter sets it (theta_max
+    // leaves it); an acceptance after filter_reset_trigger successive iterations whose last rejection
+    // was the filter's clears the filter (at most max_filter_resets times)
+    if (fr_n && pd && !rej) {
+        bool last = fr_last[b] != 0;
+        if (!it_ok) {
+            last = false;
+        } else if (in_f) {
+            last = true;
+        } else {
+            long long n = fr_n[b], c = fr_cnt[b];
+            if (o.max_filter_resets > 0 && n < o.max_filter_resets) {
+                if (last) {
+                    ++c;
+                    if (c >= o.filter_reset_trigger) {
+                        nf[b] = 0;
+                        ++n;
+                        c = 0;
+                    }
+                } else {
+                    c = 0;
+                }
+            }
+            fr_n[b] = n;
+            fr_cnt[b] = c;
+            last = false;
+        }
+        fr_last[b] = last ? 1 : 0;
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -732,6 +770,7 @@ enum { ST_OPTIMAL = 1, ST_ACCEPTABLE = 2, ST_MAX_ITER = 3, ST_TINY_STEP = 8 };
 struct StatusPrm {
     double tol, dual_inf_tol, constr_viol_tol, compl_inf_tol, acceptable_tol;
     long long acceptable_iter;
+    double acceptable_dual_inf_tol, acceptable_constr_viol_tol, acceptable_compl_inf_tol;
 };
 
 __global__ __launch_bounds__(CB) void k_status(int W, StatusPrm o, const double* __restrict__ E0,
@@ -745,12 +784,16 @@ __global__ __launch_bounds__(CB) void k_status(int W, StatusPrm o, const double*
     bool a = act[b] != 0;
     long long st = status[b], na = n_acc[b];
     const double e = E0[b];
-    if (a && e <= o.tol && du[b] / sf[b] <= o.dual_inf_tol && pr_uns[b] <= o.constr_viol_tol &&
-        co[b] <= o.compl_inf_tol) {
+    // OptimalityErrorConvergenceCheck: the dual and complementarity tests on unscaled quantities (/ sf)
+    const double du_u = du[b] / sf[b], co_u = co[b] / sf[b], pu = pr_uns[b];
+    if (a && e <= o.tol && du_u <= o.dual_inf_tol && pu <= o.constr_viol_tol && co_u <= o.compl_inf_tol) {
         st = ST_OPTIMAL;
         a = false;
     }
-    na = (a && e <= o.acceptable_tol) ? na + 1 : 0;
+    // CurrentIsAcceptable
+    const bool acc = e <= o.acceptable_tol && du_u <= o.acceptable_dual_inf_tol && pu <= o.acceptable_constr_viol_tol &&
+                     co_u <= o.acceptable_compl_inf_tol;
+    na = (a && acc) ? na + 1 : 0;
     if (a && na >= o.acceptable_iter) {
         st = ST_ACCEPTABLE;
         a = false;
@@ -915,18 +958,20 @@ int ato_ipm_multipliers(const ato_ipm_dims* d, const ato_ipm_bounds* bd, const d
 
 int ato_ipm_filter_accept(int32_t W, int32_t fmax, const double* theta, const double* phi, const double* gphi_d,
                           const double* alpha, const double* tht, const double* pht, const double* F,
-                          const int64_t* nf, const double* theta_max, const double* theta_min,
-                          const uint8_t* pend, const uint8_t* first, const double* prm, uint8_t* ok,
-                          uint8_t* arm, uint8_t* soc, void* stream) {
+                          int64_t* nf, const double* theta_max, const double* theta_min,
+                          const uint8_t* pend, const uint8_t* first, const double* prm, int64_t* fr_n,
+                          int64_t* fr_cnt, uint8_t* fr_last, uint8_t* ok, uint8_t* arm, uint8_t* soc, void* stream) {
     if (W < 0 || fmax < 0 || !prm) return fail(ATO_ERR_ARG, "ato_ipm_filter_accept: arguments");
     if (W == 0) return 0;
     if (!theta || !phi || !gphi_d || !alpha || !tht || !pht || (fmax && !F) || !nf || !theta_max || !theta_min ||
-        !pend || !first || !ok || !arm || !soc)
+        !pend || !first || !ok || !arm || !soc || (fr_n && (!fr_cnt || !fr_last)))
         return fail(ATO_ERR_ARG, "ato_ipm_filter_accept: arguments");
-    const FilterPrm o{prm[0], prm[1], prm[2], prm[3], prm[4], prm[5], prm[6]};   // prm: host array (ato_ipm.h)
+    // prm: host array (ato_ipm.h)
+    const FilterPrm o{prm[0], prm[1], prm[2], prm[3], prm[4], prm[5], prm[6], prm[7], (long long)prm[8],
+                      (long long)prm[9]};
     hipLaunchKernelGGL(k_filter_accept, dim3((W + CB - 1) / CB), dim3(CB), 0, static_cast<hipStream_t>(stream), W,
-                       fmax, theta, phi, gphi_d, alpha, tht, pht, F, nf, theta_max, theta_min, pend, first, o, ok,
-                       arm, soc);
+                       fmax, theta, phi, gphi_d, alpha, tht, pht, F, nf, theta_max, theta_min, pend, first, o,
+                       reinterpret_cast<int64_t*>(fr_n), reinterpret_cast<int64_t*>(fr_cnt), fr_last, ok, arm, soc);
     return check_launch("ato_ipm_filter_accept");
 }
 
@@ -937,7 +982,7 @@ int ato_ipm_status(int32_t W, const double* prm, const double* E0, const double*
     if (W == 0) return 0;
     if (!E0 || !du || !pr_uns || !co || !sf || !own || !lim || !act || !n_acc || !status)
         return fail(ATO_ERR_ARG, "ato_ipm_status: arguments");
-    const StatusPrm o{prm[0], prm[1], prm[2], prm[3], prm[4], (long long)prm[5]};
+    const StatusPrm o{prm[0], prm[1], prm[2], prm[3], prm[4], (long long)prm[5], prm[6], prm[7], prm[8]};
     hipLaunchKernelGGL(k_status, dim3((W + CB - 1) / CB), dim3(CB), 0, static_cast<hipStream_t>(stream), W, o, E0, du,
                        pr_uns, co, sf, reinterpret_cast<const long long*>(own),
                        reinterpret_cast<const long long*>(lim), act, reinterpret_cast<long long*>(n_acc),

@@ -142,6 +142,7 @@ struct Plan {
     const int2* sad_txy;          // [F] saddle fronts: trailing rows [0, tx) coupled to X, [T - ty, T) to Y
     long long l_size, cb_size;
     int sc_size;
+    int cap;                      // reserved storage slots: listed instances at or past it are skipped
     // saddle fronts fall back to Bunch-Kaufman when max |H_XX diagonal| > sad_tau max|J_YX|^2 (0: never):
     // G = -E^T H E carries the barrier diagonal (up to 1e10 near active bounds) through J^-1, where
     // Bunch-Kaufman would take those entries first as 1 x 1 pivots
@@ -343,10 +344,11 @@ __device__ __forceinline__ void extract_column(const double (&a)[T * (T + 1) / 2
     }
 }
 
-__global__ void k_inertia_zero(int batch, const int* __restrict__ list, int* __restrict__ inertia) {
+__global__ void k_inertia_zero(int batch, int cap, const int* __restrict__ list, int* __restrict__ inertia) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= batch) return;
     const int b = list ? list[i] : i;
+    if (b < 0 || b >= cap) return;
     inertia[3 * b + 0] = 0;
     inertia[3 * b + 1] = 0;
     inertia[3 * b + 2] = 0;
@@ -380,6 +382,7 @@ __global__ __launch_bounds__(FTT) __attribute__((amdgpu_waves_per_eu(W))) void k
     const int bi = blockIdx.y;
     if (bi >= batch) return;
     const int b = list ? __builtin_amdgcn_readfirstlane(list[bi]) : bi;
+    if (list && b >= P.cap) return;            // a listed slot past the reserved storage: nothing is touched
     if (P.n_sad && P.n_sad[f] > 0 && sinfo[(long long)b * P.F + f].x != SAD_FALLBACK) return;
     const int tid = threadIdx.x;
     const int ti = tid & 31, tj = tid >> 5;
@@ -771,6 +774,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void k
     const int bi = blockIdx.y;
     if (bi >= batch) return;
     const int b = list ? __builtin_amdgcn_readfirstlane(list[bi]) : bi;
+    if (list && b >= P.cap) return;            // a listed slot past the reserved storage: nothing is touched
     if (P.n_sad && P.n_sad[f] > 0 && sinfo[(long long)b * P.F + f].x != SAD_FALLBACK) return;
     const int tid = threadIdx.x;
     const int ti = tid & 15, tj = tid >> 4;
@@ -1140,6 +1144,7 @@ __global__ __launch_bounds__(SAD_NT) void k_front_saddle(Plan P, Vals V, int f0,
     const int bi = blockIdx.y;
     if (bi >= batch) return;
     const int b = list ? __builtin_amdgcn_readfirstlane(list[bi]) : bi;
+    if (list && b >= P.cap) return;            // a listed slot past the reserved storage: nothing is touched
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int p0 = P.pos_ptr[f];
     const int A = P.pos_ptr[f + 1] - p0;
@@ -1462,6 +1467,7 @@ __global__ __launch_bounds__(ST) void k_front_fwd(Plan P, int f0, int batch, con
     const int bi = blockIdx.y;
     if (bi >= batch) return;
     const int b = list ? __builtin_amdgcn_readfirstlane(list[bi]) : bi;
+    if (list && b >= P.cap) return;            // a listed slot past the reserved storage: nothing is touched
     const FrontSolve F = front_solve_setup(P, f0 + blockIdx.x, b, Lst, piv, dinv, sinfo, x, sb);
     const int tid = threadIdx.x;
     if (P.n_sad && P.n_sad[F.f] > 0 && sinfo[(long long)b * P.F + F.f].x == SAD_DONE) {
@@ -1595,6 +1601,7 @@ __global__ __launch_bounds__(ST) void k_front_bwd(Plan P, int f0, int batch, con
     const int bi = blockIdx.y;
     if (bi >= batch) return;
     const int b = list ? __builtin_amdgcn_readfirstlane(list[bi]) : bi;
+    if (list && b >= P.cap) return;            // a listed slot past the reserved storage: nothing is touched
     const FrontSolve F = front_solve_setup(P, f0 + blockIdx.x, b, Lst, piv, dinv, sinfo, x, sb);
     const int tid = threadIdx.x;
     if (P.n_sad && P.n_sad[F.f] > 0 && sinfo[(long long)b * P.F + F.f].x == SAD_DONE) {
@@ -1962,6 +1969,7 @@ Plan make_plan(const ato_kkt* h) {
     P.sc_off = h->d_sc_off;
     P.forder = h->d_forder;
     P.n_sad = h->d_n_sad;
+    P.cap = h->cap;
     P.sad_txy = reinterpret_cast<const int2*>(h->d_sad_txy);
     P.l_size = h->l_size;
     P.cb_size = h->cb_size;
@@ -2190,15 +2198,35 @@ int ato_kkt_reserve(ato_kkt* h, int32_t max_batch) {
     if (max_batch <= h->cap) return ATO_OK;
     if (h->d_L) KKT_HIP(hipDeviceSynchronize());    // queued factor / solve kernels may still use the old storage
     free_storage(h);
+    // transactional: either every buffer of the new capacity is allocated, or none is kept and the
+    // handle is left without storage (d_L == nullptr, cap == 0), which factor / solve refuse. (A
+    // failure part-way through used to leave d_L set with later buffers null and cap 0, which a
+    // listed factorisation did not catch.)
     const size_t B = (size_t)max_batch;
-    KKT_HIP(hipMalloc((void**)&h->d_L, sizeof(double) * std::max<size_t>(1, (size_t)h->l_size * B)));
-    KKT_HIP(hipMalloc((void**)&h->d_cb, sizeof(double) * std::max<size_t>(1, (size_t)h->cb_size * B)));
-    KKT_HIP(hipMalloc((void**)&h->d_sc, sizeof(double) * std::max<size_t>(1, (size_t)h->sc_size * B)));
-    KKT_HIP(hipMalloc((void**)&h->d_piv, sizeof(int2) * (size_t)h->dim * B));
-    KKT_HIP(hipMalloc((void**)&h->d_dinv, sizeof(double) * 3 * (size_t)h->dim * B));
-    KKT_HIP(hipMalloc((void**)&h->d_sinfo, sizeof(int2) * (size_t)h->F * B));
-    KKT_HIP(hipMalloc((void**)&h->d_spec, sizeof(int32_t) * (size_t)h->dim * B));
-    KKT_HIP(hipMemset(h->d_spec, 0xFF, sizeof(int32_t) * (size_t)h->dim * B));     // -1: no guess
+    const size_t bytes[7] = {sizeof(double) * std::max<size_t>(1, (size_t)h->l_size * B),
+                             sizeof(double) * std::max<size_t>(1, (size_t)h->cb_size * B),
+                             sizeof(double) * std::max<size_t>(1, (size_t)h->sc_size * B),
+                             sizeof(int2) * std::max<size_t>(1, (size_t)h->dim * B),
+                             sizeof(double) * 3 * std::max<size_t>(1, (size_t)h->dim * B),
+                             sizeof(int2) * std::max<size_t>(1, (size_t)h->F * B),
+                             sizeof(int32_t) * std::max<size_t>(1, (size_t)h->dim * B)};
+    void* p[7] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    hipError_t e = hipSuccess;
+    for (int i = 0; i < 7 && e == hipSuccess; ++i) e = hipMalloc(&p[i], bytes[i]);
+    if (e == hipSuccess) e = hipMemset(p[6], 0xFF, bytes[6]);     // -1: no guess
+    if (e != hipSuccess) {
+        for (void* q : p) (void)hipFree(q);
+        (void)hipGetLastError();
+        return fail(ATO_ERR_HIP, std::string("ato_kkt_reserve: ") + hipGetErrorString(e) + " (" +
+                                     std::to_string(max_batch) + " instances; the handle keeps no storage)");
+    }
+    h->d_L = static_cast<double*>(p[0]);
+    h->d_cb = static_cast<double*>(p[1]);
+    h->d_sc = static_cast<double*>(p[2]);
+    h->d_piv = static_cast<int2*>(p[3]);
+    h->d_dinv = static_cast<double*>(p[4]);
+    h->d_sinfo = static_cast<int2*>(p[5]);
+    h->d_spec = static_cast<int32_t*>(p[6]);
     h->cap = max_batch;
     return ATO_OK;
 }
@@ -2207,13 +2235,13 @@ int ato_kkt_factor(ato_kkt* h, int32_t batch, const int32_t* list, int64_t se, i
                    const double* J, const double* dx, const double* dr, int32_t* inertia, void* stream) {
     if (!h || !inertia || batch < 0) return fail(ATO_ERR_ARG, "bad argument");
     if (batch == 0) return ATO_OK;
-    if (!list && batch > h->cap) return fail(ATO_ERR_STATE, "ato_kkt_reserve() too small for this batch");
-    if (!h->d_L) return fail(ATO_ERR_STATE, "call ato_kkt_reserve() first");
+    if (!h->d_L || h->cap == 0) return fail(ATO_ERR_STATE, "call ato_kkt_reserve() first");
+    if (batch > h->cap) return fail(ATO_ERR_STATE, "ato_kkt_reserve() too small for this batch");
     if (batch > 65535) return fail(ATO_ERR_UNSUPPORTED, "KKT batch above 65535 instances per call");
     const Plan P = make_plan(h);
     const Vals V{H, J, dx, dr, se, sb};
     hipStream_t st = static_cast<hipStream_t>(stream);
-    hipLaunchKernelGGL(k_inertia_zero, dim3((batch + 255) / 256), dim3(256), 0, st, batch, list, inertia);
+    hipLaunchKernelGGL(k_inertia_zero, dim3((batch + 255) / 256), dim3(256), 0, st, batch, h->cap, list, inertia);
     KKT_HIP(hipGetLastError());
     for (int l = 0; l < h->L; ++l) {
         const int rc = factor_level(h, P, V, l, batch, list, inertia, st);
@@ -2226,8 +2254,8 @@ int ato_kkt_solve(ato_kkt* h, int32_t batch, const int32_t* list, int64_t se, in
                   void* stream) {
     if (!h || !x || batch < 0) return fail(ATO_ERR_ARG, "bad argument");
     if (batch == 0) return ATO_OK;
-    if (!h->d_L) return fail(ATO_ERR_STATE, "call ato_kkt_reserve() first");
-    if (!list && batch > h->cap) return fail(ATO_ERR_STATE, "ato_kkt_reserve() too small for this batch");
+    if (!h->d_L || h->cap == 0) return fail(ATO_ERR_STATE, "call ato_kkt_reserve() first");
+    if (batch > h->cap) return fail(ATO_ERR_STATE, "ato_kkt_reserve() too small for this batch");
     if (batch > 65535) return fail(ATO_ERR_UNSUPPORTED, "KKT batch above 65535 instances per call");
     const Plan P = make_plan(h);
     hipStream_t st = static_cast<hipStream_t>(stream);

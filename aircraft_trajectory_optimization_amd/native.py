@@ -168,7 +168,7 @@ def declare(lib: ctypes.CDLL, prefix: str = 'ato') -> ctypes.CDLL:
         lib.ato_ipm_direction.argtypes = [dp, bp] + [vp] * 12 + [vp] * 4 + [vp, vp, vp]
         lib.ato_ipm_measures.argtypes = [dp, bp] + [vp] * 6 + [d, vp, vp, vp]
         lib.ato_ipm_multipliers.argtypes = [dp, bp, vp, vp, vp, vp, d] + [vp] * 8 + [vp]
-        lib.ato_ipm_filter_accept.argtypes = [ctypes.c_int32, ctypes.c_int32] + [vp] * 16 + [vp]
+        lib.ato_ipm_filter_accept.argtypes = [ctypes.c_int32, ctypes.c_int32] + [vp] * 19 + [vp]
         lib.ato_ipm_kkt_diag.argtypes = [dp] + [vp] * 7 + [vp]
         lib.ato_ipm_perturb.argtypes = [ctypes.c_int32] * 3 + [vp] * 16 + [vp]
         lib.ato_ipm_status.argtypes = [ctypes.c_int32] + [vp] * 11 + [vp]

@@ -86,22 +86,34 @@ def summarize_records(rec) -> Dict:
 def window_timer(warmup: int, steps: int, sync: Callable[[], None]) -> Tuple[Callable, Dict]:
     '''
     on_iteration hook that times lockstep iterations [warmup, warmup + steps) of a solve: the
-    device is synchronised at both ends; instance-iterations in the window are the instances
-    that took a step in each of those iterations
+    device is synchronised at both ends. Instance-iterations in the window ('count') are those of
+    the solve's StepCounter between the two ends: the instances that took a step in each of the
+    window's lockstep iterations ('count_main') plus the iterations of the restoration phases that ran
+    meanwhile ('count_resto'; IPOPT's iteration counter runs through the restoration phase, and so do
+    max_iter and sqp_full's instance_iterations)
     '''
     import time
-    st: Dict = {'t0': None, 't1': None, 'count': 0, 'timed': 0}
+    st: Dict = {'t0': None, 't1': None, 'count': 0, 'count_main': 0, 'count_resto': 0, 'timed': 0}
+    base = {}
 
-    def hook(it, n_step):
+    def hook(it, n_step, counter=None):
         if n_step >= 0 and it == warmup and st['t0'] is None:
             sync()
             st['t0'] = time.perf_counter()
+            if counter is not None:       # this iteration's own steps are already in the counter
+                base['v'], base['r'] = counter.value - n_step, counter.resto
         if st['t0'] is not None and st['t1'] is None:
             if n_step < 0 or it == warmup + steps:
                 sync()
                 st['t1'] = time.perf_counter()
+                if counter is not None:
+                    end = counter.value - max(n_step, 0)
+                    st['count'] = end - base['v']
+                    st['count_resto'] = counter.resto - base['r']
+                else:
+                    st['count'] = st['count_main']
             else:
-                st['count'] += n_step
+                st['count_main'] += n_step
                 st['timed'] += 1
     return hook, st
 

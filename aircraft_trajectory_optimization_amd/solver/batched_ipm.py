@@ -50,6 +50,7 @@ STATUS_NAMES = {RUNNING: 'running', OPTIMAL: 'optimal', ACCEPTABLE: 'acceptable'
 # watchdog point and direction of every column (stored while the column's watchdog is active)
 WD_VECS = ('x', 's', 'y', 'zl', 'zu', 'vl', 'vu', 'dx', 'ds', 'dy', 'dzl', 'dzu', 'dvl', 'dvu')
 WD_SCAL = ('alpha_max', 'alpha_z', 'theta', 'phi', 'gphi_d')
+CSTAT = ('watchdog_started', 'watchdog_reverted', 'soft_resto_steps', 'resto_iterations', 'kkt_failures')
 FILTER_MAX = 256
 
 
@@ -71,10 +72,13 @@ class BatchedIPMResult:
 class BatchedDeviceEvaluator:
     ''' the evaluation library (ato_eval, ato_hess_eval) over B instances, interleaved layout '''
 
-    def __init__(self, spec, batch: int, device: Optional[torch.device] = None):
+    def __init__(self, spec, batch: int, device: Optional[torch.device] = None, jac32: bool = False):
         from aircraft_trajectory_optimization_amd.raceline.batched import BatchedNLP
         from aircraft_trajectory_optimization_amd.raceline.evaluator import variable_stages
         self.spec = spec
+        # config 5's fp32 leg: the Jacobian from the fp32 kernel (ato_eval_f32), widened to fp64; g, f,
+        # grad f and the Hessian stay fp64 (the residuals the termination test reads at tol 1e-8)
+        self.jac32 = bool(jac32)
         self.bn = BatchedNLP(spec, batch, device=device, buffers=False)
         self.device = self.bn.device
         self.batch = batch
@@ -114,7 +118,7 @@ class BatchedDeviceEvaluator:
     # the caching allocator orders any reuse of these blocks after the launch on the same stream)
     def eval(self, X: torch.Tensor):
         t = self._tic()
-        out = _eval_into(self.bn.problem, self.bn, self.batch, X, self.n, self.m, self.nnz, True)
+        out = _eval_into(self.bn.problem, self.bn, self.batch, X, self.n, self.m, self.nnz, True, self.jac32)
         self.counts['eval'] += 1
         self._toc(t)
         return out
@@ -148,24 +152,33 @@ class BatchedDeviceEvaluator:
 
     def fork(self) -> 'BatchedDeviceEvaluator':
         ''' the same problem on a second library handle (a handle serves one thread at a time) '''
-        ev = BatchedDeviceEvaluator(self.spec, self.batch, self.device)
+        ev = BatchedDeviceEvaluator(self.spec, self.batch, self.device, self.jac32)
         if getattr(self, 'tables', None) is not None:
             ev.set_instance_spheres(self.tables)
         return ev
 
 
-def _eval_into(problem, binder, B, X, n, m, nnz, jac):
-    ''' one ato_eval of the batch X [n, B] into new tensors: (f, g, grad f, J or None) '''
+def _eval_into(problem, binder, B, X, n, m, nnz, jac, jac32=False):
+    ''' one ato_eval of the batch X [n, B] into new tensors: (f, g, grad f, J or None). jac32: the
+    Jacobian comes from a second, fp32 evaluation (ato_eval_f32 with only J written), widened to fp64 '''
     X = X.contiguous()
     dev = X.device
     f = torch.empty(B, dtype=torch.float64, device=dev)
     g = torch.empty((m, B), dtype=torch.float64, device=dev)
     gf = torch.zeros((n, B), dtype=torch.float64, device=dev)     # (sparse grad f mode: zeros stay)
-    J = torch.empty((nnz, B), dtype=torch.float64, device=dev) if jac else None
+    J = torch.empty((nnz, B), dtype=torch.float64, device=dev) if jac and not jac32 else None
     st = torch.cuda.current_stream(dev)
     binder._bind_spheres()
-    problem.eval_ptrs(B, X.data_ptr(), g=g.data_ptr(), jac=J.data_ptr() if jac else 0, f=f.data_ptr(),
+    problem.eval_ptrs(B, X.data_ptr(), g=g.data_ptr(), jac=J.data_ptr() if J is not None else 0, f=f.data_ptr(),
                       grad_f=gf.data_ptr(), stream=st.cuda_stream)
+    if jac and jac32:
+        # (g is written too, into scratch: the J-producing launches of the evaluation library are the
+        # g + J passes, paired stores included)
+        X32 = X.float()
+        J32 = torch.empty((nnz, B), dtype=torch.float32, device=dev)
+        G32 = torch.empty((m, B), dtype=torch.float32, device=dev)
+        problem.eval_ptrs(B, X32.data_ptr(), g=G32.data_ptr(), jac=J32.data_ptr(), stream=st.cuda_stream, fp32=True)
+        J = J32.double()
     return f, g, gf, J
 
 
@@ -211,7 +224,7 @@ class _SubsetDeviceEvaluator:
             self.problem.set_instance_spheres(self.isph.data_ptr() if self.isph is not None else 0, self.batch)
 
     def eval(self, X: torch.Tensor):
-        return _eval_into(self.problem, self, self.batch, X, self.n, self.m, self.nnz, True)
+        return _eval_into(self.problem, self, self.batch, X, self.n, self.m, self.nnz, True, self.base.jac32)
 
     def eval_fg(self, X: torch.Tensor):
         f, g, _, _ = _eval_into(self.problem, self, self.batch, X, self.n, self.m, self.nnz, False)
@@ -224,18 +237,40 @@ class _SubsetDeviceEvaluator:
         return _hess_into(self.problem, self, self.batch, X, lam, sigma, len(self.h_col))
 
 
-def device_solver(spec, batch: int, lbx, ubx, options: Optional[IPMOptions] = None, device=None):
-    ''' BatchedInteriorPoint over the HIP evaluation library and the device KKT factorisation '''
+def device_solver(spec, batch: int, lbx, ubx, options: Optional[IPMOptions] = None, device=None,
+                  jac32: bool = False):
+    ''' BatchedInteriorPoint over the HIP evaluation library and the device KKT factorisation (jac32: the
+    Jacobian from the fp32 evaluation kernel, BatchedDeviceEvaluator) '''
     from aircraft_trajectory_optimization_amd.solver.kkt_device import DeviceKKT
-    from aircraft_trajectory_optimization_amd.solver.kkt_plan import build_plan, collocation_saddle
-    ev = BatchedDeviceEvaluator(spec, batch, device)
+    from aircraft_trajectory_optimization_amd.solver.kkt_plan import build_plan, collocation_saddle, cpc_node_groups
+    ev = BatchedDeviceEvaluator(spec, batch, device, jac32)
     # saddle fronts (the collocation states and their ODE defect rows: structured elimination) with
     # ATO_KKT_SADDLE=1; by default every front is factorised by Bunch-Kaufman
     sad = None if os.environ.get('ATO_KKT_SADDLE', '0') == '0' else \
         collocation_saddle(spec.N, spec.K1, spec.nv, spec.nz, ev.m, ev.j_row_ptr, ev.j_col)
-    plan = build_plan(ev.n, ev.m, ev.var_stage, ev.j_row_ptr, ev.j_col, ev.h_row_ptr, ev.h_col, saddle=sad)
+    # config 5's CPC progress variables: a chain of node fronts below every leaf (kkt_plan.cpc_node_groups)
+    plan = build_plan(ev.n, ev.m, ev.var_stage, ev.j_row_ptr, ev.j_col, ev.h_row_ptr, ev.h_col, saddle=sad,
+                      node_groups=cpc_node_groups(spec))
     kkt = DeviceKKT(plan, batch, ev.device)
     return BatchedInteriorPoint(ev, kkt, lbx, ubx, options)
+
+
+class StepCounter:
+    ''' instance-iterations taken so far by a solve and every restoration phase nested in it (shared with
+    the phases' solvers, which may run in worker threads): IPOPT's iteration counter runs through the
+    restoration phase, and the benchmark window counts both '''
+
+    def __init__(self):
+        import threading
+        self._lock = threading.Lock()
+        self.value = 0
+        self.resto = 0
+
+    def add(self, n: int, resto: bool = False):
+        with self._lock:
+            self.value += int(n)
+            if resto:
+                self.resto += int(n)
 
 
 class _Laps:
@@ -299,6 +334,11 @@ def _structure(ev, dev) -> Dict[str, torch.Tensor]:
     pw = np.argsort(w_row, kind='stable')
     d['w_src'], d['w_col'] = t(w_src[pw], torch.long), t(w_col[pw], torch.long)
     d['w_len'] = t(np.bincount(w_row, minlength=n), torch.long)
+    # entry counts of the segment sums (python ints): every length vector sums to its operand's rows
+    d['n_j'], d['n_w'] = int(len(jc_np)), int(len(w_src))
+    if int(np.diff(ev.j_row_ptr).sum()) != d['n_j'] or int(np.bincount(jc_np, minlength=n).sum()) != d['n_j'] or \
+            int(np.bincount(w_row, minlength=n).sum()) != d['n_w'] or len(np.diff(ev.j_row_ptr)) != m:
+        raise ValueError('sparse product structure: segment lengths do not cover the entries')
     try:
         holder._ipm_structure = {**d, '_dev': str(dev)}
     except AttributeError:
@@ -422,6 +462,8 @@ class BatchedInteriorPoint:
             setattr(self, k_, v_)
         self.stats = {'factorizations': 0, 'solves': 0, 'evals': 0, 'hess': 0, 'compactions': 0}
         self.laps = _Laps(dev)
+        self.step_counter = StepCounter()
+        self.in_resto_phase = False          # a restoration phase's nested solver (its steps count as such)
         self.compact = True             # carry only the live columns once half of them have finished
         self.async_restoration = True   # restoration phases in a worker thread (device backends with fork())
         # fused column kernels of the iteration's vector algebra on the device (libato, ato_ipm.h);
@@ -449,17 +491,23 @@ class BatchedInteriorPoint:
 
     # ------------------------------------------------------------------ sparse products
     @staticmethod
-    def _segsum(vals, lengths):
+    def _segsum(vals, lengths, total):
+        # unsafe=True skips segment_reduce's own validation (a device synchronisation per call); the
+        # lengths are structural and sum to `total` (checked once in _structure), so the operand's
+        # leading dimension is checked here on the host instead (gpurun_out r05h: a SIGSEGV inside
+        # this call in a B = 8192 solve, beside two restoration threads in the KKT factorisation)
+        if vals.shape[0] != total:
+            raise ValueError(f'segment sum over {vals.shape[0]} entries, the structure has {total}')
         return torch.segment_reduce(vals, 'sum', lengths=lengths, axis=0, unsafe=True)
 
     def _Jx(self, Js, v):
-        return self._segsum(Js * v[self.jc], self.j_len)
+        return self._segsum(Js * v[self.jc], self.j_len, self.n_j)
 
     def _JTy(self, Js, y):
-        return self._segsum(Js[self.jt_src] * y[self.jt_row], self.jt_len)
+        return self._segsum(Js[self.jt_src] * y[self.jt_row], self.jt_len, self.n_j)
 
     def _Wx(self, H, v):
-        return self._segsum(H[self.w_src] * v[self.w_col], self.w_len)
+        return self._segsum(H[self.w_src] * v[self.w_col], self.w_len, self.n_w)
 
     def _Kmul(self, H, Js, dx, dr, v):
         vx, vy = v[:self.n], v[self.n:]
@@ -587,23 +635,55 @@ class BatchedInteriorPoint:
             return self.vk.measures(self._bd(), x, s, g, self.c_rhs, f, mu, self.o.kappa_d)
         return self._resid(g, s).abs().sum(0), self._phi(f, x, s, mu)
 
-    def _accept(self, theta, phi, gphi_d, alpha, tht, pht, F, nf, theta_min=None):
-        ''' filter acceptance per instance (solver/ipm.py _accept): (accepted, is_armijo_step) '''
+    def _accept(self, theta, phi, gphi_d, alpha, tht, pht, F, nf, theta_min=None, pend=None, frs=None):
+        ''' filter acceptance per instance (solver/ipm.py _accept): (accepted, is_armijo_step). With
+        pend, only those columns are tested (accepted is False elsewhere); with frs = (fr_n, fr_cnt,
+        fr_last) the filter reset heuristic runs on the tested columns, in place on frs and nf
+        (the torch formulation of ato_ipm_filter_accept) '''
         o = self.o
         theta_min = self.theta_min if theta_min is None else theta_min
         rej = ~(tht <= self.theta_max)
         base = torch.where(phi.abs() > 10.0, torch.log10(phi.abs()), torch.ones_like(phi))
-        rej = rej | ((pht > phi) & (torch.log10(torch.clamp(pht - phi, min=1e-300)) > o.obj_max_inc + base))
+        inc = (pht > phi) & (torch.log10(torch.clamp(pht - phi, min=1e-300)) > o.obj_max_inc + base)
         k = torch.arange(F.shape[1], device=self.dev)
         valid = k[None, :] < nf[:, None]
         in_f = (valid & (tht[:, None] >= F[:, :, 0]) & (pht[:, None] >= F[:, :, 1])).any(1)
         mgd = torch.clamp(-gphi_d, min=0.0)
         switching = (gphi_d < 0) & (alpha * mgd ** o.s_phi > o.delta * theta ** o.s_theta)
         arm_case = (theta <= theta_min) & switching
-        ok_arm = pht <= phi + o.eta_phi * alpha * gphi_d
-        ok_suf = (tht <= (1 - o.gamma_theta) * theta) | (pht <= phi - o.gamma_phi * theta)
-        ok = ~rej & ~in_f & torch.where(arm_case, ok_arm, ok_suf)
+        # IpUtils Compare_le(lhs, rhs, base): lhs - rhs <= compare_tol |base|
+        dp = pht - phi
+        ok_arm = dp - (o.eta_phi * alpha) * gphi_d <= o.compare_tol * phi.abs()
+        ok_suf = (tht - (1 - o.gamma_theta) * theta <= o.compare_tol * theta.abs()) | \
+            (dp - (-o.gamma_phi * theta) <= o.compare_tol * phi.abs())
+        it_ok = ~inc & torch.where(arm_case, ok_arm, ok_suf)
+        ok = ~rej & it_ok & ~in_f
+        if pend is not None:
+            ok = ok & pend
+        if frs is not None:
+            fr_n, fr_cnt, fr_last = frs
+            ev = pend & ~rej
+            acc = ev & it_ok & ~in_f
+            elig = acc & (fr_n < o.max_filter_resets) if o.max_filter_resets > 0 else torch.zeros_like(acc)
+            up = elig & fr_last
+            cnt = torch.where(up, fr_cnt + 1, torch.where(elig, torch.zeros_like(fr_cnt), fr_cnt))
+            reset = up & (cnt >= o.filter_reset_trigger)
+            nf.masked_fill_(reset, 0)
+            fr_n.add_(reset.long())
+            fr_cnt.copy_(torch.where(reset, torch.zeros_like(cnt), cnt))
+            fr_last.copy_(torch.where((ev & ~it_ok) | acc, torch.zeros_like(fr_last),
+                                      torch.where(ev & it_ok & in_f, torch.ones_like(fr_last), fr_last)))
         return ok, ok & arm_case
+
+    def _filter_test(self, theta, phi, gphi_d, alpha, tht, pht, F, nf, pend, first, frs, theta_min=None):
+        ''' one trial's filter test for the pend columns (FilterLSAcceptor::CheckAcceptabilityOfTrialPoint with
+        its reset heuristic): (ok, arm, soc candidates); the fused kernel on the device '''
+        tmin = self.theta_min if theta_min is None else theta_min
+        if self.vk is not None:
+            return self.vk.filter_accept(theta, phi, gphi_d, alpha, tht, pht, F, nf, self.theta_max, tmin, pend,
+                                         first, self.o, frs=frs)
+        ok, arm = self._accept(theta, phi, gphi_d, alpha, tht, pht, F, nf, theta_min=tmin, pend=pend, frs=frs)
+        return ok, arm, pend & ~ok & first & (tht >= theta)
 
     def _solve(self, rhs, mask, H, Js, dx, dr, idx=None):
         ''' K x = rhs for the masked instances with their current factors, iterative refinement
@@ -619,6 +699,8 @@ class BatchedInteriorPoint:
         self.kkt.solve(x, idx)
         self.laps.lap('kkt_solve')
         self.stats['solves'] += 1
+        if self.o.refine_ipopt:
+            return self._refine(rhs, x, mask, idx, H, Js, dx, dr)
         scale = rhs.abs().amax(0) + 1e-300
         # residuals only for the columns whose x changed since the last one (comp): the others
         # keep their last rmax, bitwise what a full residual would give them again
@@ -641,6 +723,46 @@ class BatchedInteriorPoint:
             rmax = torch.where(comp, self._residual(H, Js, dx, dr, x, rhs, ridx).abs().amax(0), rmax)
         # IPOPT (residual_ratio_singular): unrefinable solves count as singular matrices
         self.last_solve_ok = torch.isfinite(rmax) & (rmax <= 1e-5 * scale)
+        self.laps.lap('kkt_refine')
+        return x
+
+    def _refine(self, rhs, x, mask, idx, H, Js, dx, dr):
+        ''' PDFullSpaceSolver's iterative refinement per column (solver/ipm.py refine): residual ratio
+        |r| / (min(|x|, 1e6 |rhs|) + |rhs|), at least min_refinement_steps, until residual_ratio_max, at most
+        max_refinement_steps, or until the ratio stops improving; last_solve_ok is False where the
+        refinement stopped above residual_ratio_singular (or the ratio is not finite) '''
+        o = self.o
+        nr = rhs.abs().amax(0)
+
+        def ratio(res, x_):
+            nres, nx = res.abs().amax(0), x_.abs().amax(0)
+            return torch.where(nr + nx == 0, nres, nres / (torch.minimum(nx, 1e6 * nr) + nr))
+        res = self._residual(H, Js, dx, dr, x, rhs, idx)
+        rr = torch.where(mask, ratio(res, x), torch.zeros_like(nr))
+        old = rr
+        bad = torch.zeros_like(mask)
+        refine = mask.clone()
+        k = 0
+        while True:
+            need = refine & torch.isfinite(rr) & ((rr > o.residual_ratio_max) if k >= o.min_refinement_steps
+                                                  else torch.ones_like(refine))
+            if not bool(need.any()):
+                break
+            nidx = _idx(need)
+            self.laps.lap('kkt_refine')
+            self.kkt.solve(res, nidx)
+            self.laps.lap('kkt_solve')
+            self.stats['solves'] += 1
+            x = torch.where(need[None, :], x + res, x)
+            res = self._residual(H, Js, dx, dr, x, rhs, nidx)
+            rr = torch.where(need, ratio(res, x), rr)
+            k += 1
+            quit_ = need & (((rr > o.residual_ratio_max) & (k > o.max_refinement_steps)) |
+                            ((rr > old) & (k > o.min_refinement_steps)))
+            bad = bad | (quit_ & (rr > o.residual_ratio_singular))
+            refine = need & ~quit_
+            old = torch.where(need, rr, old)
+        self.last_solve_ok = torch.isfinite(rr) & ~bad
         self.laps.lap('kkt_refine')
         return x
 
@@ -693,6 +815,9 @@ class BatchedInteriorPoint:
         pidx = _idx(pend)
         npass = 0
         tosolve = torch.zeros(B, dtype=torch.bool, device=self.dev)
+        # PDFullSpaceSolver: an unrefinable solve is treated as singular once per step; after that the
+        # solution is taken as it is (a non-finite one never is)
+        pretended = torch.zeros(B, dtype=torch.bool, device=self.dev)
         # The solves are deferred until the inertia-correction passes are done: an instance whose
         # inertia is right keeps its factors in its own storage slot while the others refactorise,
         # so all of them are solved (and refined) in one batched call instead of one per pass. Each
@@ -733,7 +858,12 @@ class BatchedInteriorPoint:
             ry = rhs_y.clone()
             ry[self.iin] += rhs_s / Ds_used
             xs = self._solve(torch.cat([rhs_x, ry]), tosolve, W, Js, dx_used, dr_used, idx=sidx)
-            fin = torch.isfinite(xs).all(0) & self.last_solve_ok
+            finite = torch.isfinite(xs).all(0)
+            if self.o.refine_ipopt:
+                fin = finite & (self.last_solve_ok | pretended)
+                pretended = pretended | (tosolve & finite & ~fin)
+            else:
+                fin = finite & self.last_solve_ok
             okd = tosolve & fin
             sol = torch.where(okd[None, :], xs, sol)
             ok_all = ok_all | okd
@@ -761,9 +891,10 @@ class BatchedInteriorPoint:
         X0 [n, B] (or [B, n]). active: instances to iterate (default all); mu0: initial barrier
         per instance; stop_check(x, s) -> [B] bool ends an instance with status 'stopped' (the
         restoration phase's return test, from an instance's second iteration on). on_iteration(it,
-        n_step): called once per lockstep iteration with the number of instances taking a step in
-        it (host value already fetched by the iteration's own synchronisation), and once more as
-        on_iteration(it, -1) when the loop ends (benchmark windows). resto_init (the restoration
+        n_step, counter): called once per lockstep iteration with the number of instances taking a step in
+        it (host value already fetched by the iteration's own synchronisation) and the solve's StepCounter
+        (instance-iterations so far, restoration phases included), and once more as on_iteration(it, -1,
+        counter) when the loop ends (benchmark windows). resto_init (the restoration
         phase's own solve, solver/ipm.py): starting slacks 's', bound multipliers 'zl', 'zu', 'vl',
         'vu', 'theta_max_fact' and per-instance iteration limits 'max_iter' [B].
         '''
@@ -849,6 +980,18 @@ class BatchedInteriorPoint:
         soft_count = torch.zeros(B, dtype=torch.long, device=dev)
         wd = {}
         wd_on = o.watchdog_shortened_iter_trigger > 0
+        # FilterLSAcceptor's filter reset heuristic per column: resets so far, successive iterations whose
+        # last rejection was the filter's, and whether the last rejection was the filter's
+        fr_n = torch.zeros(B, dtype=torch.long, device=dev)
+        fr_cnt = torch.zeros(B, dtype=torch.long, device=dev)
+        fr_last = torch.zeros(B, dtype=torch.bool, device=dev)
+        last_mu = torch.full((B,), -1.0, dtype=torch.float64, device=dev)   # mu of the last line search
+        # the last acceptable iterate of every column (BacktrackingLineSearch::StoreAcceptablePoint)
+        has_acc = torch.zeros(B, dtype=torch.bool, device=dev)
+        accp = {}
+        # per-instance counters (diagnostics: where an instance's iterations go): watchdog starts, watchdog
+        # reverts, soft restoration steps, iterations inside restoration phases, KKT failures (no direction)
+        cst = torch.zeros((len(CSTAT), B), dtype=torch.long, device=dev)
         wdst = torch.zeros(7, dtype=torch.long, device=dev)  # watchdog started / succeeded / reverted, tiny, soft
         own = torch.zeros(B, dtype=torch.long, device=dev)          # iterations done per instance
         waiting = torch.zeros(B, dtype=torch.bool, device=dev)      # frozen until the next restoration batch
@@ -879,7 +1022,9 @@ class BatchedInteriorPoint:
                'lam_x': torch.zeros((n, B0), dtype=torch.float64, device=dev),
                'status': torch.zeros(B0, dtype=torch.long, device=dev),
                'iters': torch.zeros(B0, dtype=torch.long, device=dev),
-               'n_resto': torch.zeros(B0, dtype=torch.long, device=dev)}
+               'n_resto': torch.zeros(B0, dtype=torch.long, device=dev),
+               'fr_n': torch.zeros(B0, dtype=torch.long, device=dev),
+               'cst': torch.zeros((len(CSTAT), B0), dtype=torch.long, device=dev)}
         hist_row = torch.zeros((6, B0), dtype=torch.float64, device=dev)
         e0_stale = torch.zeros(B0, dtype=torch.bool, device=dev)   # x moved after the last history row
         # ---- asynchronous restoration: a restoration phase runs in a worker thread on its own
@@ -893,8 +1038,10 @@ class BatchedInteriorPoint:
         use_async = (self.async_restoration and stop_check is None and self.vk is not None and can_compact
                      and hasattr(keep['ev'], 'fork') and hasattr(keep['kkt'], 'fork') and B0 <= self.ASYNC_MAX_BATCH)
 
-        def save(cols_, x_, s_, y_, zl_, zu_, status_, iters_, n_resto_):
+        def save(cols_, x_, s_, y_, zl_, zu_, status_, iters_, n_resto_, fr_n_, cst_):
             out['n_resto'][cols_] = n_resto_
+            out['fr_n'][cols_] = fr_n_
+            out['cst'][:, cols_] = cst_
             out['x'][:, cols_] = x_
             out['s'][:, cols_] = s_
             out['lam_g'][:, cols_] = y_ * self.sg / self.sf
@@ -932,14 +1079,17 @@ class BatchedInteriorPoint:
                 live = act | waiting | infl
                 n_live = int(live.sum())
                 if 0 < n_live <= B // 2:
-                    save(cols, x, s, y, zl, zu, status, iters, n_resto)
+                    save(cols, x, s, y, zl, zu, status, iters, n_resto, fr_n, cst)
                     sel = torch.nonzero(live).reshape(-1)
                     (x, s, f, g, gf, jv, y, zl, zu, vl, vu, mu, tau, nf, n_acc, status, n_resto, own, waiting,
-                     iters, act, infl, ws_short, in_wd, wd_trial, tiny_flag, in_soft, soft_count) = self._compact(
+                     iters, act, infl, ws_short, in_wd, wd_trial, tiny_flag, in_soft, soft_count, fr_n, fr_cnt,
+                     fr_last, last_mu, has_acc, cst) = self._compact(
                         sel, (x, s, f, g, gf, jv, y, zl, zu, vl, vu, mu, tau, nf, n_acc, status, n_resto, own,
-                              waiting, iters, act, infl, ws_short, in_wd, wd_trial, tiny_flag, in_soft, soft_count))
+                              waiting, iters, act, infl, ws_short, in_wd, wd_trial, tiny_flag, in_soft, soft_count,
+                              fr_n, fr_cnt, fr_last, last_mu, has_acc, cst))
                     pert.take(sel)
                     wd = dict(zip(wd.keys(), self._compact(sel, tuple(wd.values()))))
+                    accp = dict(zip(accp.keys(), self._compact(sel, tuple(accp.values()))))
                     F = F.index_select(0, sel).contiguous()
                     cols = cols.index_select(0, sel)
                     self.ev = keep['ev'].subset(n_live, cols)
@@ -968,22 +1118,35 @@ class BatchedInteriorPoint:
                 self.vk.status(o, E0, du, pr_uns, co, sf, own, self.lim, act, n_acc, status)
             else:
                 conv = act & (E0 <= o.tol) & (du / sf <= o.dual_inf_tol) & (pr_uns <= o.constr_viol_tol) & \
-                    (co <= o.compl_inf_tol)
+                    (co / sf <= o.compl_inf_tol)
                 status = torch.where(conv, torch.full_like(status, OPTIMAL), status)
                 act = act & ~conv
-                n_acc = torch.where(act & (E0 <= o.acceptable_tol), n_acc + 1, torch.zeros_like(n_acc))
+                acc_ = (E0 <= o.acceptable_tol) & (du / sf <= o.acceptable_dual_inf_tol) & \
+                    (pr_uns <= o.acceptable_constr_viol_tol) & (co / sf <= o.acceptable_compl_inf_tol)
+                n_acc = torch.where(act & acc_, n_acc + 1, torch.zeros_like(n_acc))
                 accd = act & (n_acc >= o.acceptable_iter)
                 status = torch.where(accd, torch.full_like(status, ACCEPTABLE), status)
                 act = act & ~accd
                 mx = act & (own >= self.lim)
                 status = torch.where(mx, torch.full_like(status, MAX_ITER), status)
                 act = act & ~mx
-            n_step, n_wt = torch.stack([act.sum(), waiting.sum()]).tolist()     # one synchronisation
+            # OptimalityErrorConvergenceCheck::CurrentIsAcceptable of the columns that take a step: their
+            # iterate is stored as the backup acceptable point (BacktrackingLineSearch::StoreAcceptablePoint)
+            cur_acc = act & (E0 <= o.acceptable_tol) & (du / sf <= o.acceptable_dual_inf_tol) & \
+                (pr_uns <= o.acceptable_constr_viol_tol) & (co / sf <= o.acceptable_compl_inf_tol)
+            n_step, n_wt, n_ac = torch.stack([act.sum(), waiting.sum(), cur_acc.sum()]).tolist()   # one synchronisation
             any_act, any_wait = n_step > 0, n_wt > 0
+            if n_ac:
+                cur_pt = {'x': x, 's': s, 'y': y, 'zl': zl, 'zu': zu, 'vl': vl, 'vu': vu}
+                if not accp:
+                    accp = {k_: torch.zeros_like(v_) for k_, v_ in cur_pt.items()}
+                accp = {k_: torch.where(cur_acc[None, :], cur_pt[k_], v_) for k_, v_ in accp.items()}
+                has_acc = has_acc | cur_acc
             if not any_act and not any_wait and not inflight:
                 break
+            self.step_counter.add(n_step, self.in_resto_phase)
             if on_iteration is not None:
-                on_iteration(it, int(n_step))
+                on_iteration(it, int(n_step), self.step_counter)
             laps.lap('check')
             stepping = act.clone()
             resto = torch.zeros(B, dtype=torch.bool, device=dev)
@@ -1034,6 +1197,13 @@ class BatchedInteriorPoint:
                         gf = torch.where(upd[None, :], gfe, gf)
                         dual_x = gf + jty - zl + zu
                 laps.lap('barrier')
+                if o.watchdog_ipopt_counter:
+                    # FindAcceptableTrialPoint: mu changed since the last line search -> the watchdog is
+                    # dropped (not reverted) and its shortened-step counter cleared
+                    chg = act & (mu != last_mu)
+                    in_wd = in_wd & ~chg
+                    ws_short = torch.where(chg, torch.zeros_like(ws_short), ws_short)
+                    last_mu = torch.where(act, mu, last_mu)
                 # ---- Newton step
                 W = self.ev.hess(x, y * sg, sf)
                 if _DEBUG_HESS:                   # diagnostic: instances with a non-finite Hessian
@@ -1059,6 +1229,7 @@ class BatchedInteriorPoint:
                 dx, ds, dy, ok, ctx = self._kkt_step(W, Js, Sx, Ss, rhs_x, rhs_s, rhs_y, mu, act, pert)
                 laps.lap('kkt_other')
                 kfail = act & ~ok
+                cst[4] += kfail.long()
                 # IPOPT: no direction inside the watchdog -> back to the watchdog point (below)
                 kwd = kfail & in_wd
                 kfail = kfail & ~in_wd
@@ -1126,6 +1297,7 @@ class BatchedInteriorPoint:
                         in_wd = in_wd | start
                         wd_trial = torch.where(start, torch.zeros_like(wd_trial), wd_trial)
                         wdst[0] += start.sum()
+                        cst[0] += start.long()
 
                 def revert(msk):
                     # stop the watchdog of the masked columns: their iterate and direction go back to the
@@ -1148,6 +1320,7 @@ class BatchedInteriorPoint:
                     f, g = torch.where(msk, fe_, f), torch.where(m2, ge_, g)
                     gf, jv = torch.where(m2, gfe_, gf), torch.where(m2, jve_, jv)
                     wdst[2] += msk.sum()
+                    cst[1] += msk.long()
 
                 def alpha_min_of(theta_, gphi_):
                     neg = gphi_ < 0
@@ -1174,20 +1347,28 @@ class BatchedInteriorPoint:
                 xn, sn = x.clone(), s.clone()
                 an, dyn = torch.zeros_like(alpha), dy.clone()
                 armn = torch.zeros(B, dtype=torch.bool, device=dev)
+                # columns at their line search's first trial (IPOPT's n_steps == 0: tried even below alpha_min;
+                # a column accepted there restarts the watchdog's shortened-step counter)
+                fresh = pend.clone()
+                accf = torch.zeros(B, dtype=torch.bool, device=dev)
+                frs = (fr_n, fr_cnt, fr_last)
 
                 def take(mask, al, xt, st, arm, dyt):
-                    nonlocal xn, sn, an, dyn, armn
+                    nonlocal xn, sn, an, dyn, armn, accf
                     m2 = mask[None, :]
                     xn = torch.where(m2, xt, xn)
                     sn = torch.where(m2, st, sn)
                     an = torch.where(mask, al, an)
                     dyn = torch.where(m2, dyt, dyn)
                     armn = torch.where(mask, arm, armn)
+                    accf = torch.where(mask, fresh, accf)
 
                 laps.lap('direction')
                 lsfail = torch.zeros_like(act)
                 for _ls in range(200):
                     failed = pend & ~(alpha > alpha_min)
+                    if o.ls_first_trial:
+                        failed = failed & ~fresh
                     # one host synchronisation per trial for both tests
                     any_failed, any_left = torch.stack([failed.any(), (pend & ~failed).any()]).tolist()
                     if any_failed:
@@ -1206,13 +1387,10 @@ class BatchedInteriorPoint:
                         gd_r, al_r = torch.where(wdm, wd['gphi_d'], gphi_d), torch.where(wdm, wd['alpha_max'], alpha)
                     else:
                         th_r, ph_r, gd_r, al_r = theta, phi, gphi_d, alpha
-                    if self.vk is not None:          # one launch: the filter test and the SOC candidates
-                        okt, armt, soc = self.vk.filter_accept(th_r, ph_r, gd_r, al_r, tht, pht, F, nf,
-                                                               self.theta_max, self.theta_min, pend, first, o)
-                    else:
-                        okt, armt = self._accept(th_r, ph_r, gd_r, al_r, tht, pht, F, nf)
-                        okt = okt & pend
-                        soc = pend & ~okt & first & (tht >= th_r)
+                    # one launch: the filter test (tiny steps are taken untested), its reset heuristic and the
+                    # SOC candidates
+                    okt, armt, soc = self._filter_test(th_r, ph_r, gd_r, al_r, tht, pht, F, nf,
+                                                       pend & ~tiny if _ls == 0 else pend, first, frs)
                     soc = soc & ~nosoc & ~wdm & ~tiny
                     take(okt, alpha, xt, st, armt, dy)
                     pend = pend & ~okt
@@ -1243,10 +1421,12 @@ class BatchedInteriorPoint:
                         if slk is None:
                             slk = self._slacks(x, s)
                         got = self._soc(soc, ctx, rhs_x, rhs_s, x, s, alpha, r, self._resid(gt, st), theta, phi,
-                                        gphi_d, F, nf, tau, slk, mu, take)
+                                        gphi_d, F, nf, tau, slk, mu, take, frs)
                         pend = pend & ~got
                         laps.lap('soc')
                     first = first & False
+                    # the next trial is a first one only for the columns whose watchdog was just reverted
+                    fresh = rev if (_ls == 0 and any_wd) else torch.zeros_like(fresh)
                     alpha = torch.where(pend, alpha * 0.5, alpha)
                 laps.lap('ls_logic')
                 # ---- soft restoration steps: the columns in the phase, and the columns whose line search
@@ -1260,9 +1440,10 @@ class BatchedInteriorPoint:
                     add_filter(enter, theta, phi)
                     al_soft = torch.minimum(alpha_max, alpha_z)
                     soft_ok, soft_sat = self._soft_steps(soft_cand, al_soft, x, s, y, zl, zu, vl, vu, gf, jv, g, dx,
-                                                         ds, dy, dzl, dzu, dvl, dvu, theta, phi, F, nf, mu, take)
+                                                         ds, dy, dzl, dzu, dvl, dvu, theta, phi, F, nf, mu, take, frs)
                     wdst[4] += (enter & soft_ok).sum()
                     wdst[5] += soft_ok.sum()
+                    cst[2] += soft_ok.long()
                     wdst[6] += (soft_sat & in_soft).sum()
                     in_soft = torch.where(soft_ok, ~soft_sat, in_soft)
                     soft_count = torch.where(soft_ok & soft_sat, torch.zeros_like(soft_count),
@@ -1270,6 +1451,21 @@ class BatchedInteriorPoint:
                 failed_all = (lsfail & ~soft_ok) | soft_over | (soft_try & ~soft_ok)
                 if allow_restoration:
                     resto = failed_all | kresto
+                    if o.resto_feasible_fact > 0:
+                        # restoration called at an almost feasible point: the stored acceptable iterate is
+                        # returned (ACCEPTABLE_POINT_REACHED), else the instance fails (RESTORATION_FAILED)
+                        near = resto & (theta <= o.resto_feasible_fact * o.tol)
+                        back = near & has_acc
+                        status = torch.where(back, torch.full_like(status, ACCEPTABLE),
+                                             torch.where(near, torch.full_like(status, LS_FAILED), status))
+                        act = act & ~near
+                        resto = resto & ~near
+                        e0_stale[cols[back]] = True          # returned point: the stored one, not the last row
+                        if accp:
+                            b2 = back[None, :]
+                            x, s, y = (torch.where(b2, accp[k_], v_) for k_, v_ in (('x', x), ('s', s), ('y', y)))
+                            zl, zu, vl, vu = (torch.where(b2, accp[k_], v_) for k_, v_ in
+                                              (('zl', zl), ('zu', zu), ('vl', vl), ('vu', vu)))
                 else:
                     status = torch.where(failed_all, torch.full_like(status, LS_FAILED), status)
                     act = act & ~failed_all
@@ -1287,7 +1483,8 @@ class BatchedInteriorPoint:
                     # watchdog trigger: consecutive accepted steps shorter than the fraction-to-the-boundary
                     # step (soft restoration steps leave the counter alone)
                     normal = upd & ~tiny & ~wd_cols & ~soft_ok
-                    ws_short = torch.where(normal, torch.where(an < alpha_max, ws_short + 1, torch.zeros_like(ws_short)),
+                    short = ~accf if o.watchdog_ipopt_counter else an < alpha_max
+                    ws_short = torch.where(normal, torch.where(short, ws_short + 1, torch.zeros_like(ws_short)),
                                            torch.where(upd & ~soft_ok, torch.zeros_like(ws_short), ws_short))
                 wdst[3] += tiny.sum()
                 m2 = upd[None, :]
@@ -1343,10 +1540,12 @@ class BatchedInteriorPoint:
                     theta_w, phi_w = self._measures(x, s, g, f, mu)
                     add_filter(can, theta_w, phi_w)
                     state = (x, s, g, zl, zu, vl, vu, mu, own)
-                    if use_async and n_act >= 8:
-                        inflight.append(self._resto_launch(can, state, theta_w, F, nf, cols, keep, inflight))
+                    job = self._resto_launch(can, state, theta_w, F, nf, cols, keep, inflight) \
+                        if use_async and n_act >= 8 else None
+                    if job is not None:
+                        inflight.append(job)
                         infl = infl | can
-                    else:
+                    else:                    # synchronous (also when a phase's own storage cannot be reserved)
                         done = self._restore(can, state, theta_w, F, nf)
             if done is not None:
                 can, xr, sr, okr, hitm, kr = done
@@ -1354,6 +1553,7 @@ class BatchedInteriorPoint:
                 resto_ran = True
                 laps.lap('resto')
                 own = own + torch.where(can, kr, torch.zeros_like(kr))
+                cst[3] += torch.where(can, kr, torch.zeros_like(kr))
                 bad = can & ~okr & ~hitm
                 status = torch.where(bad, torch.full_like(status, LS_FAILED), status)
                 status = torch.where(hitm, torch.full_like(status, MAX_ITER), status)
@@ -1390,7 +1590,7 @@ class BatchedInteriorPoint:
             # after their last history row
             e0_stale[cols[stepping]] = True
         if on_iteration is not None:
-            on_iteration(it, -1)
+            on_iteration(it, -1, self.step_counter)
         for j in inflight:                           # (the lockstep bound ended the loop first)
             R, xr, sr, okr, hitm, kr = self._resto_collect(j, cols, x, s, B0)
             e0_stale[cols[R]] = True
@@ -1404,8 +1604,12 @@ class BatchedInteriorPoint:
         if getattr(self, '_async_pool', None) is not None:
             self._async_pool.shutdown(wait=True)
             self._async_pool = None
-        save(cols, x, s, y, zl, zu, status, iters, n_resto)
+        save(cols, x, s, y, zl, zu, status, iters, n_resto, fr_n, cst)
+        self.per_instance = {k: out['cst'][i].cpu().numpy() for i, k in enumerate(CSTAT)}
+        self.per_instance['restorations'] = out['n_resto'].cpu().numpy()
+        self.per_instance['filter_resets'] = out['fr_n'].cpu().numpy()
         self.stats['restorations'] = self.stats.get('restorations', 0) + int(out['n_resto'].sum())
+        self.stats['filter_resets'] = self.stats.get('filter_resets', 0) + int(out['fr_n'].sum())
         wv = wdst.tolist()
         prev = self.stats.get('watchdog', {})
         self.stats['watchdog'] = {k: prev.get(k, 0) + v for k, v in
@@ -1463,7 +1667,7 @@ class BatchedInteriorPoint:
         return tot / (self.n + self.mi + self.m + self.n_bounds)
 
     def _soft_steps(self, mask, al, x, s, y, zl, zu, vl, vu, gf, jv, g, dx, ds, dy, dzl, dzu, dvl, dvu, theta, phi,
-                    F, nf, mu, take):
+                    F, nf, mu, take, frs=None):
         '''
         BacktrackingLineSearch::TrySoftRestoStep for the masked columns (solver/ipm.py _soft_step):
         primal and dual variables take the step al = min(alpha_primal_max, alpha_dual_max);
@@ -1478,8 +1682,9 @@ class BatchedInteriorPoint:
         ft, gt, gft, jvt = self._eval(xt)
         tht, pht = self._measures(xt, st, gt, ft, mu)
         zero = torch.zeros_like(al)
-        sat, _ = self._accept(theta, phi, zero, zero, tht, pht, F, nf, theta_min=torch.full_like(al, -1.0))
-        sat = sat & mask
+        # CheckAcceptabilityOfTrialPoint(0): alpha test 0, never the Armijo case (and the reset heuristic)
+        sat, _, _ = self._filter_test(theta, phi, zero, zero, tht, pht, F, nf, mask, torch.zeros_like(mask), frs,
+                                      theta_min=torch.full_like(al, -1.0))
         sg = self.sg
         e_cur = self._pd_error(gf, jv * sg[self.jr], g, x, s, y, zl, zu, vl, vu, mu)
         e_tr = self._pd_error(gft, jvt * sg[self.jr], gt, xt, st, yt, zlt, zut, vlt, vut, mu)
@@ -1507,7 +1712,8 @@ class BatchedInteriorPoint:
         reset = big > self.o.bound_mult_reset_threshold
         return tuple(torch.where(reset[None, :], h.double(), z) for z, h in zip(new, hs))
 
-    def _soc(self, mask, ctx, rhs_x, rhs_s, x, s, alpha, r, rt, theta, phi, gphi_d, F, nf, tau, slk, mu, take):
+    def _soc(self, mask, ctx, rhs_x, rhs_s, x, s, alpha, r, rt, theta, phi, gphi_d, F, nf, tau, slk, mu, take,
+             frs=None):
         ''' second-order corrections (IPOPT A-5.5 - A-5.10) for the masked instances; returns the
         mask of instances whose corrected trial point was accepted '''
         o = self.o
@@ -1532,12 +1738,7 @@ class BatchedInteriorPoint:
             ft, gt = self._eval_fg(xt)
             rt2 = self._resid(gt, st)
             tht, pht = self._measures(xt, st, gt, ft, mu)
-            if self.vk is not None:
-                ok, arm, _ = self.vk.filter_accept(theta, phi, gphi_d, alpha, tht, pht, F, nf, self.theta_max,
-                                                   self.theta_min, cur, torch.zeros_like(cur), o)
-            else:
-                ok, arm = self._accept(theta, phi, gphi_d, alpha, tht, pht, F, nf)
-                ok = ok & cur
+            ok, arm, _ = self._filter_test(theta, phi, gphi_d, alpha, tht, pht, F, nf, cur, torch.zeros_like(cur), frs)
             take(ok, am, xt, st, arm, dys)
             got = got | ok
             cur = cur & ~ok & ~(tht > o.kappa_soc * theta_old)
@@ -1638,6 +1839,7 @@ class BatchedInteriorPoint:
         ubx = torch.cat([view.ubx0, torch.full((2 * m, Br), np.inf, dtype=torch.float64, device=dev)])
         ro = IPMOptions(**{**o.__dict__, 'nlp_scaling': False})
         sub = BatchedInteriorPoint(rev, _RestorationKKT(kkt_r, rev), lbx.cpu().numpy(), ubx.cpu().numpy(), ro)
+        sub.step_counter, sub.in_resto_phase = self.step_counter, True
         accept = self._resto_accept(view, job['F'], job['nf'], job['theta'], job['mu'])
         res = sub.solve(Xr0, mu0=job['mu_r'], stop_check=accept, allow_restoration=False, progress=self._progress,
                         resto_init=job['init'])
@@ -1685,6 +1887,16 @@ class BatchedInteriorPoint:
             # built here, on the calling thread, before any worker can need it
             self._resto_structure = _RestorationStructure(keep['ev'])
         job = self._resto_prepare(R, state, theta, F, nf)
+        # the phase's factor storage is reserved here, on the calling thread (ato_kkt_reserve drains the
+        # device; in the worker it would wait for every other phase in flight). If it cannot be allocated
+        # the phase runs synchronously on the main storage instead (returns None)
+        from aircraft_trajectory_optimization_amd.solver.kkt_device import KKTReserveError
+        try:
+            res['kkt'].ensure(job['R'])
+        except KKTReserveError as exc:
+            self.stats['async_reserve_failed'] = self.stats.get('async_reserve_failed', 0) + 1
+            self.last_reserve_error = str(exc)
+            return None
         job['orig'] = cols.index_select(0, job['sel'])
         self.stats['async_phases'] = self.stats.get('async_phases', 0) + 1
         ready = torch.cuda.Event()
@@ -1747,6 +1959,7 @@ class BatchedInteriorPoint:
         ubx = torch.cat([self.ubx0, torch.full((2 * m, B), np.inf, dtype=torch.float64, device=dev)])
         ro = IPMOptions(**{**o.__dict__, 'nlp_scaling': False})
         sub = BatchedInteriorPoint(rev, _RestorationKKT(self.kkt, rev), lbx.cpu().numpy(), ubx.cpu().numpy(), ro)
+        sub.step_counter, sub.in_resto_phase = self.step_counter, True
         accept = self._resto_accept(self, F, nf, theta, mu)
         res = sub.solve(Xr0, mu0=mu_r, active=R, stop_check=accept, allow_restoration=False,
                         progress=self._progress, resto_init=init)

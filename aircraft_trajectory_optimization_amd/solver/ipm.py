@@ -69,6 +69,9 @@ class IPMOptions:
     max_iter: int = 3000
     acceptable_tol: float = 1e-6
     acceptable_iter: int = 15
+    acceptable_dual_inf_tol: float = 1e10
+    acceptable_constr_viol_tol: float = 1e-2
+    acceptable_compl_inf_tol: float = 1e-2
     dual_inf_tol: float = 1.0
     constr_viol_tol: float = 1e-4
     compl_inf_tol: float = 1e-4
@@ -100,6 +103,31 @@ class IPMOptions:
     theta_max_fact: float = 1e4
     theta_min_fact: float = 1e-4
     obj_max_inc: float = 5.0
+    # FilterLSAcceptor's filter reset heuristic: after filter_reset_trigger successive iterations whose
+    # last rejected trial was rejected by the filter, the filter is cleared (at most max_filter_resets times)
+    max_filter_resets: int = 5
+    filter_reset_trigger: int = 5
+    # IpUtils Compare_le: the sufficient-decrease and Armijo tests hold up to 10 eps of the reference value
+    # (round-off tolerance; 0 restates the exact comparisons)
+    compare_tol: float = 10 * 2.220446049250313e-16
+    # BacktrackingLineSearch: at least one trial point per line search (alpha > alpha_min || n_steps == 0)
+    ls_first_trial: bool = True
+    # the watchdog is dropped (not reverted) and its shortened-step counter cleared when mu has changed
+    # since the last line search; the counter counts line searches that needed a second trial (n_steps > 0)
+    watchdog_ipopt_counter: bool = True
+    # restoration requested at an almost feasible point (theta <= resto_feasible_fact * tol): the last
+    # acceptable iterate is returned ('acceptable') if one was stored, else 'restoration_failed'
+    resto_feasible_fact: float = 1e-2
+    # PDFullSpaceSolver's iterative refinement: residual ratio |r| / (min(|x|, 1e6 |rhs|) + |rhs|), at least
+    # min_refinement_steps, stop at residual_ratio_max, after max_refinement_steps or when the ratio stops
+    # improving; a solve that stops above residual_ratio_singular is treated as singular once per step
+    # (the retry's solution is then taken as it is). False: round 5's refinement (|r| / |rhs| <= 1e-10, every
+    # unrefinable solve singular)
+    refine_ipopt: bool = True
+    min_refinement_steps: int = 1
+    max_refinement_steps: int = 10
+    residual_ratio_max: float = 1e-10
+    residual_ratio_singular: float = 1e-5
     # inertia correction (PDPerturbationHandler)
     delta_w_0: float = 1e-4                 # first_hessian_perturbation
     delta_w_min: float = 1e-20              # min_hessian_perturbation
@@ -476,6 +504,9 @@ class InteriorPointSolver:
         soft_count = 0
         first_resto_iter = in_resto
         self.wd_stats = {'started': 0, 'succeeded': 0, 'reverted': 0, 'tiny_steps': 0}
+        self.fr = {'n': 0, 'count': 0, 'last_filter': False, 'resets': 0}   # filter reset heuristic
+        last_mu = -1.0            # mu of the previous line search (BacktrackingLineSearch::last_mu_)
+        acc_point = None          # the last acceptable iterate (StoreAcceptablePoint)
         self.soft_stats = {'entered': 0, 'steps': 0, 'left': 0}
         resto_accept = None if resto_init is None else resto_init.get('accept')
         while True:
@@ -497,10 +528,13 @@ class InteriorPointSolver:
                     status = 'stopped'
                     break
             if E0 <= o.tol and du / self.sf <= o.dual_inf_tol and pr_uns <= o.constr_viol_tol and \
-                    co <= o.compl_inf_tol:
+                    co / self.sf <= o.compl_inf_tol:
                 status = 'optimal'
                 break
-            n_acc = n_acc + 1 if E0 <= o.acceptable_tol else 0
+            # OptimalityErrorConvergenceCheck::CurrentIsAcceptable
+            cur_acc = (E0 <= o.acceptable_tol and du / self.sf <= o.acceptable_dual_inf_tol and
+                       pr_uns <= o.acceptable_constr_viol_tol and co / self.sf <= o.acceptable_compl_inf_tol)
+            n_acc = n_acc + 1 if cur_acc else 0
             if n_acc >= o.acceptable_iter:
                 status = 'acceptable'
                 break
@@ -531,6 +565,13 @@ class InteriorPointSolver:
             first_resto_iter = False
             if status == 'tiny_step':
                 break
+            if o.watchdog_ipopt_counter and mu != last_mu:
+                # FindAcceptableTrialPoint: "Mu has changed in line search - resetting watchdog counters"
+                wd = None
+                ws_short = 0
+            last_mu = mu
+            if cur_acc:               # backup acceptable point (restored if restoration is called at a feasible point)
+                acc_point = (x, s, y, zl, zu, vl, vu)
             # ---- Newton step
             W = _lower_to_full(n, self.ev.h_row_ptr, self.ev.h_col, self.ev.hess(x, y * self.sg, self.sf))
             self.evals['hess'] += 1
@@ -573,6 +614,7 @@ class InteriorPointSolver:
                 phi = phi_of(f, x, s, mu)
                 gphi_d = gx @ dx + gs @ ds
             accepted = None
+            ls_steps = 0              # n_steps of the accepted line-search trial
             soft = None               # an accepted soft-restoration step: (x, s, y, zl, zu, vl, vu, f, g, gf, jv, S)
             skip_first = False
             tiny = False
@@ -649,7 +691,8 @@ class InteriorPointSolver:
                 alpha_min = o.alpha_min_frac * amin
                 alpha = alpha_max * (0.5 if skip_first else 1.0)
                 first = not skip_first
-                while alpha > alpha_min:
+                n_steps = 0
+                while alpha > alpha_min or (o.ls_first_trial and n_steps == 0):
                     xt, st = x + alpha * dx, s + alpha * ds
                     ft, gt, gft, jvt = self._eval(xt)
                     tht, rt = theta_of(gt, st)
@@ -657,6 +700,7 @@ class InteriorPointSolver:
                     ok, armijo_step = self._accept(theta, phi, gphi_d, alpha, tht, pht, filt, theta_max, theta_min)
                     if ok:
                         accepted = (alpha, xt, st, ft, gt, gft, jvt, armijo_step, dy)
+                        ls_steps = n_steps
                         break
                     if first and tht >= theta and solve is not None:
                         # second-order corrections (IPOPT A-5.7 ... A-5.10)
@@ -664,9 +708,11 @@ class InteriorPointSolver:
                                         theta_min, theta_of, phi_of, tau, a, b, c, d, hxl, hxu, hsl, hsu, mu)
                         if soc is not None:
                             accepted = soc
+                            ls_steps = n_steps
                             break
                     first = False
                     alpha *= 0.5
+                    n_steps += 1
                 if accepted is None and o.soft_resto_pderror_reduction_factor > 0:
                     # ---- the line search failed: try the soft restoration phase first (the current
                     # point is abandoned: its filter entry is added as before a restoration)
@@ -697,6 +743,15 @@ class InteriorPointSolver:
                 # ---- feasibility restoration (MinC_1NrmRestorationPhase)
                 if in_resto or n_resto >= o.max_resto:
                     status = 'restoration_failed'
+                    break
+                if o.resto_feasible_fact > 0 and theta <= o.resto_feasible_fact * o.tol:
+                    # BacktrackingLineSearch: restoration called at an almost feasible point -- the stored
+                    # acceptable iterate is returned (ACCEPTABLE_POINT_REACHED), else RESTORATION_FAILED
+                    if acc_point is not None:
+                        x, s, y, zl, zu, vl, vu = acc_point
+                        status = 'acceptable'
+                    else:
+                        status = 'restoration_failed'
                     break
                 n_resto += 1
                 self._last_step = 'R'
@@ -732,8 +787,12 @@ class InteriorPointSolver:
             if not armijo_step:
                 filt.append(((1 - o.gamma_theta) * theta, phi - o.gamma_phi * theta))
             if wd is None and not tiny:
-                # watchdog trigger: consecutive steps shorter than the fraction-to-the-boundary step
-                ws_short = ws_short + 1 if alpha < alpha_max else 0
+                # watchdog trigger: consecutive line searches that needed more than one trial (IPOPT counts
+                # n_steps > 0; round 5 counted steps shorter than the fraction-to-the-boundary step)
+                if o.watchdog_ipopt_counter:
+                    ws_short = ws_short + 1 if ls_steps > 0 else 0
+                else:
+                    ws_short = ws_short + 1 if alpha < alpha_max else 0
             else:
                 ws_short = 0
             x, s, f, g, gf, jv = xt, st, ft, gt, gft, jvt
@@ -754,6 +813,7 @@ class InteriorPointSolver:
         stats['restorations'] = n_resto
         stats['watchdog'] = dict(self.wd_stats)
         stats['soft_resto'] = dict(self.soft_stats)
+        stats['filter_resets'] = self.fr['resets']
         stats['degenerate'] = (pert.hdeg, pert.jdeg)
         return IPMResult(x=x, f=float(fu), g=gu, lam_g=lam_g, lam_x=lam_x, status=status, success=success,
                          iters=it, stats=stats, history=history)
@@ -785,8 +845,7 @@ class InteriorPointSolver:
         return None
 
     # ------------------------------------------------------------------ feasibility restoration
-    @staticmethod
-    def _post_resto_bound_mults(x, s, xr, sr, zl, zu, vl, vu, mu, tau, slacks, hxl, hxu, hsl, hsu):
+    def _post_resto_bound_mults(self, x, s, xr, sr, zl, zu, vl, vu, mu, tau, slacks, hxl, hxu, hsl, hsu):
         '''
         MinC_1NrmRestorationPhase after a successful phase: the whole primal move is taken as one
         primal-dual Newton step of the bound multipliers (ComputeBoundMultiplierStep:
@@ -800,7 +859,7 @@ class InteriorPointSolver:
         dz = [np.where(h, ((sc - st) * z + mu) / sc - z, 0.0) for z, sc, st, h in zip(zs, cur, tri, hs)]
         adual = min(InteriorPointSolver._ftb(z, d_, h, tau) for z, d_, h in zip(zs, dz, hs))
         new = [z + adual * d_ for z, d_ in zip(zs, dz)]
-        if max(np.abs(z).max(initial=0) for z in new) > 1000.0:
+        if max(np.abs(z).max(initial=0) for z in new) > self.o.bound_mult_reset_threshold:
             new = [np.where(h, 1.0, 0.0) for h in hs]
         return tuple(new)
 
@@ -907,6 +966,8 @@ class InteriorPointSolver:
 
         def solve(rhs):
             x = base(rhs)
+            if self.o.refine_ipopt:
+                return refine(rhs, x)
             scale = np.abs(rhs).max(initial=0) + 1e-300
             for _ in range(10):
                 res = rhs - Kc @ x
@@ -917,6 +978,29 @@ class InteriorPointSolver:
             # IPOPT (residual_ratio_singular): a solve refinement cannot bring below 1e-5 of the
             # right-hand side is treated like a singular matrix (larger perturbation)
             self._last_solve_ok = bool(np.all(np.isfinite(res)) and np.abs(res).max(initial=0) <= 1e-5 * scale)
+            return x
+
+        def refine(rhs, x):
+            # PDFullSpaceSolver::Solve (ComputeResidualRatio, on the reduced system)
+            o = self.o
+            nr = np.abs(rhs).max(initial=0)
+
+            def ratio(res, x):
+                nres, nx = np.abs(res).max(initial=0), np.abs(x).max(initial=0)
+                return nres if nr + nx == 0 else nres / (min(nx, 1e6 * nr) + nr)
+            res = rhs - Kc @ x
+            rr = ratio(res, x)
+            old, k, bad = rr, 0, False
+            while np.isfinite(rr) and (k < o.min_refinement_steps or rr > o.residual_ratio_max):
+                x = x + base(res)
+                res = rhs - Kc @ x
+                rr = ratio(res, x)
+                k += 1
+                if (k > o.max_refinement_steps and rr > o.residual_ratio_max) or (k > o.min_refinement_steps and rr > old):
+                    bad = rr > o.residual_ratio_singular
+                    break
+                old = rr
+            self._last_solve_ok = bool(np.isfinite(rr) and np.all(np.isfinite(x)) and not bad)
             return x
         return solve, inertia
 
@@ -933,6 +1017,7 @@ class InteriorPointSolver:
         '''
         n, m = self.n, self.m
         d = pert.consider_new_system(mu)
+        pretended = False          # an unrefinable solve has been treated as singular in this step already
         while d is not None:
             delta_w, delta_c = d
             Ds_tot = Ss + delta_w
@@ -950,8 +1035,12 @@ class InteriorPointSolver:
                 r_y = rhs_y.copy()
                 r_y[iin] += rhs_s / Ds_tot
                 sol = solve_k(np.concatenate([rhs_x, r_y]))
-                if not (np.all(np.isfinite(sol)) and self._last_solve_ok):
+                finite = bool(np.all(np.isfinite(sol)))
+                if not finite or (not self._last_solve_ok and not (self.o.refine_ipopt and pretended)):
+                    # PDFullSpaceSolver: pretend singularity only once -- if it did not help, the solution is
+                    # taken as it is (a non-finite one never is)
                     singular = True
+                    pretended = pretended or finite
                 else:
                     dx, dy = sol[:n], sol[n:]
                     ds = (rhs_s + dy[iin]) / Ds_tot
@@ -970,23 +1059,46 @@ class InteriorPointSolver:
 
     def _accept(self, theta, phi, gphi_d, alpha, tht, pht, filt, theta_max, theta_min):
         ''' filter acceptance (FilterLSAcceptor::CheckAcceptabilityOfTrialPoint); returns
-        (accepted, is_armijo_step) '''
+        (accepted, is_armijo_step). Order of IPOPT's tests: theta_max; then the current iterate
+        (Armijo in the f-type case, else sufficient decrease of theta or phi, with Compare_le's
+        round-off tolerance, and obj_max_inc); then the filter. An accepted trial runs the filter
+        reset heuristic on the filter list `filt` (cleared in place). '''
         o = self.o
+        fr = self.fr
         if tht > theta_max:
             return False, False
+        ct = o.compare_tol
+        switching = alpha > 0 and gphi_d < 0 and alpha * (-gphi_d) ** o.s_phi > o.delta * theta ** o.s_theta
+        arm_case = theta <= theta_min and switching
+        if arm_case:
+            ok = (pht - phi) - o.eta_phi * alpha * gphi_d <= ct * abs(phi)
+        else:
+            ok = (tht - (1 - o.gamma_theta) * theta <= ct * abs(theta) or
+                  (pht - phi) - (-o.gamma_phi * theta) <= ct * abs(phi))
         if pht > phi:
             # obj_max_inc: the barrier objective may not grow by more than 10^5 of its magnitude
             base = np.log10(abs(phi)) if abs(phi) > 10.0 else 1.0
             if np.log10(pht - phi) > o.obj_max_inc + base:
-                return False, False
+                ok = False
+        if not ok:
+            fr['last_filter'] = False
+            return False, False
         for tf, pf in filt:
             if tht >= tf and pht >= pf:
+                fr['last_filter'] = True
                 return False, False
-        switching = alpha > 0 and gphi_d < 0 and alpha * (-gphi_d) ** o.s_phi > o.delta * theta ** o.s_theta
-        if theta <= theta_min and switching:
-            return pht <= phi + o.eta_phi * alpha * gphi_d, True
-        ok = tht <= (1 - o.gamma_theta) * theta or pht <= phi - o.gamma_phi * theta
-        return ok, False
+        if o.max_filter_resets > 0 and fr['n'] < o.max_filter_resets:
+            if fr['last_filter']:
+                fr['count'] += 1
+                if fr['count'] >= o.filter_reset_trigger:
+                    filt.clear()
+                    fr['n'] += 1
+                    fr['resets'] += 1
+                    fr['count'] = 0
+            else:
+                fr['count'] = 0
+        fr['last_filter'] = False
+        return True, arm_case
 
     def _soc(self, solve, rhs_x, rhs_s, x, s, alpha, r, rt, theta, phi, gphi_d, filt, theta_max, theta_min,
              theta_of, phi_of, tau, a, b, c, d, hxl, hxu, hsl, hsu, mu):

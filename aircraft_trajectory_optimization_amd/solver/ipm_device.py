@@ -152,24 +152,32 @@ class DeviceIPMKernels:
                     'ato_ipm_kkt_diag')
         return dx, dr, Ds
 
-    def filter_accept(self, theta, phi, gphi_d, alpha, tht, pht, F, nf, theta_max, theta_min, pend, first, o):
+    def filter_accept(self, theta, phi, gphi_d, alpha, tht, pht, F, nf, theta_max, theta_min, pend, first, o,
+                      frs=None):
         ''' (ok, arm, soc) bool [W]: the filter test of a trial point for the searching columns
-        (batched_ipm.py _accept, `& pend`) and the columns that try a second-order correction '''
+        (batched_ipm.py _accept, `& pend`) and the columns that try a second-order correction.
+        frs: the filter reset heuristic's state (fr_n, fr_cnt int64 [W], fr_last bool [W]), updated in
+        place together with nf (a reset filter gets nf = 0); None: no heuristic '''
         W = theta.shape[0]
         cols = [self._c(t, W) for t in (theta, phi, gphi_d, alpha, tht, pht, theta_max, theta_min)]
         if F.dtype != torch.float64 or F.shape[0] != W or F.dim() != 3 or F.shape[2] != 2:
             raise ValueError('filter: expected fp64 [W, fmax, 2]')
         F = F.contiguous()
-        nf = nf.to(torch.int64).contiguous()
+        self._own(nf, torch.int64, W, 'filter length')            # updated in place (filter resets)
         pend, first = pend.to(torch.bool).contiguous(), first.to(torch.bool).contiguous()
-        key = (o.s_phi, o.s_theta, o.delta, o.eta_phi, o.gamma_theta, o.gamma_phi, o.obj_max_inc)
-        prm = self._prm.get(key)
-        if prm is None:     # host array: the seven parameters are read on the host and passed by value
-            prm = self._prm[key] = np.array(key, dtype=np.float64)
+        if frs is not None:
+            self._own(frs[0], torch.int64, W, 'filter reset count')
+            self._own(frs[1], torch.int64, W, 'filter reset trigger count')
+            self._own(frs[2], torch.bool, W, 'filter rejection flag')
+        key = ('filter', o.s_phi, o.s_theta, o.delta, o.eta_phi, o.gamma_theta, o.gamma_phi, o.obj_max_inc,
+               o.compare_tol, o.max_filter_resets, o.filter_reset_trigger)
+        prm = self._host_prm(key)      # host array: the parameters are read on the host and passed by value
         out = torch.empty((3, W), dtype=torch.bool, device=self.device)
         th, ph, gd, al, tt, pt, tmax, tmin = cols
+        fr = (None, None, None) if frs is None else frs
         self._check(self.lib.ato_ipm_filter_accept(W, F.shape[1], _p(th), _p(ph), _p(gd), _p(al), _p(tt), _p(pt),
                                                    _p(F), _p(nf), _p(tmax), _p(tmin), _p(pend), _p(first), prm.ctypes.data,
+                                                   _p(fr[0]), _p(fr[1]), _p(fr[2]),
                                                    _p(out[0]), _p(out[1]), _p(out[2]), self._stream()),
                     'ato_ipm_filter_accept')
         return out[0], out[1], out[2]
@@ -190,7 +198,9 @@ class DeviceIPMKernels:
         for t in st:
             if t.dtype != torch.int64 or t.shape != (W,) or not t.is_contiguous():
                 raise ValueError('perturbation state: expected contiguous int64 [W]')
-        fl = [self._c(t, W) for t in fl]
+        # the handler state is updated in place by the kernel: a non-contiguous (copied) operand would
+        # lose the update, so every state tensor must be the solver's own contiguous storage
+        fl = [self._own(t, torch.float64, W, 'perturbation state') for t in fl]
         for t in (pend, tosolve):
             if t is not None and (t.dtype != torch.bool or t.shape != (W,) or not t.is_contiguous()):
                 raise ValueError('perturbation masks: expected contiguous bool [W]')
@@ -218,7 +228,8 @@ class DeviceIPMKernels:
         ''' termination tests (ato_ipm_status), in place on act (bool), n_acc and status (int64) '''
         W = E0.shape[0]
         prm = self._host_prm(('status', o.tol, o.dual_inf_tol, o.constr_viol_tol, o.compl_inf_tol,
-                              o.acceptable_tol, o.acceptable_iter))
+                              o.acceptable_tol, o.acceptable_iter, o.acceptable_dual_inf_tol,
+                              o.acceptable_constr_viol_tol, o.acceptable_compl_inf_tol))
         cols = [self._c(t, W) for t in (E0, du, pr_uns, co, sf)]
         ints = [self._own(t, torch.int64, W, 'status') for t in (own, lim)]
         self._own(act, torch.bool, W, 'status act')

@@ -19,6 +19,10 @@ _i32p = ctypes.POINTER(ctypes.c_int32)
 _i64p = ctypes.POINTER(ctypes.c_int64)
 
 
+class KKTReserveError(RuntimeError):
+    ''' the factor storage could not be allocated (the handle then holds no storage) '''
+
+
 class AtoKKTPlanDesc(ctypes.Structure):
     ''' mirror of ato_kkt_plan_desc '''
     _fields_ = [
@@ -166,10 +170,16 @@ class DeviceKKT:
         return DeviceKKT(self.plan, min(self.cap, 64), self.device)
 
     def ensure(self, count: int):
-        ''' grow the factor storage to `count` instances (the library drains the device first) '''
+        ''' grow the factor storage to `count` instances (the library drains the device first).
+        ato_kkt_reserve is transactional: when an allocation fails the handle keeps no storage at
+        all, so cap becomes 0 here (every factor / solve is then refused until a reserve succeeds)
+        and KKTReserveError is raised '''
         if count > self.cap:
             with torch.cuda.device(self.device):
-                self._check(self.lib.ato_kkt_reserve(self.handle, int(count)))
+                rc = self.lib.ato_kkt_reserve(self.handle, int(count))
+            if rc != 0:
+                self.cap = 0
+                raise KKTReserveError(f'libato KKT error {rc}: {self.lib.ato_last_error().decode()}')
             self.cap = int(count)
             self.inertia = torch.zeros((self.cap, 3), dtype=torch.int32, device=self.device)
 

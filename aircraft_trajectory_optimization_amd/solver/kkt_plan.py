@@ -202,7 +202,17 @@ def collocation_saddle(N, K1, nv, nz, m, j_row_ptr, j_col):
 HUB_MIN_ROWS = 3           # border rows of a hub reach this many distinct intervals (eliminated at the root)
 
 
-def _fronts_nd(n, var_stage, lo, hi, j_row_ptr, j_col, split_pairs=True, saddle=None):
+def cpc_node_groups(spec):
+    ''' the CPC progress variables (lambda, mu, nu per waypoint) of every collocation node, for the node
+    chain of build_plan (raceline/problem.py _cpc_block: laid out node by node after all node variables);
+    None without CPC '''
+    if getattr(spec, 'cpc', None) is None:
+        return None
+    w = 3 * spec.cpc_m
+    return [spec.cpc_off + q * w + np.arange(w) for q in range(spec.P)]
+
+
+def _fronts_nd(n, var_stage, lo, hi, j_row_ptr, j_col, split_pairs=True, saddle=None, node_groups=None):
     S = int(var_stage.max()) + 1
     m = len(lo)
     jr = np.repeat(np.arange(m), np.diff(np.asarray(j_row_ptr)))
@@ -263,6 +273,12 @@ def _fronts_nd(n, var_stage, lo, hi, j_row_ptr, j_col, split_pairs=True, saddle=
     # child front of the leaf: eliminated first, they leave a smaller leaf block (fewer register
     # tiles, cheaper pivot steps) and a short chain of small-front steps instead
     pre = [np.zeros(0, np.int64) for _ in range(S)]
+    # node groups (CPC progress variables of every node, cpc_node_groups): node of every grouped variable
+    gnode = np.full(n, -1, np.int64)
+    if node_groups is not None:
+        for q, g in enumerate(node_groups):
+            gnode[np.asarray(g, np.int64)] = q
+    npairs: Dict[int, List[tuple]] = {}             # pairs of a grouped variable: pre-front of its node front
     if split_pairs:
         cnt = np.bincount(jc, minlength=n)
         used = np.zeros(m, bool)
@@ -273,7 +289,10 @@ def _fronts_nd(n, var_stage, lo, hi, j_row_ptr, j_col, split_pairs=True, saddle=
             if anchor[v] or root_anchor[v] or used[r] or root_only[r] or not (interior[r] and lo[r] == st):
                 continue
             used[r] = True
-            pairs[st].append((v, r))
+            if gnode[v] >= 0:
+                npairs.setdefault(int(gnode[v]), []).append((v, r))
+            else:
+                pairs[st].append((v, r))
         for st in range(S):
             if pairs[st]:
                 pre[st] = np.concatenate([np.sort([v for v, _ in pairs[st]]), n + np.sort([r for _, r in pairs[st]])])
@@ -283,6 +302,53 @@ def _fronts_nd(n, var_stage, lo, hi, j_row_ptr, j_col, split_pairs=True, saddle=
             pre_id[st] = len(own)
             own.append(pre[st])
             children.append([])
+    # node chain (CPC, config 5): the progress variables of node q and the rows that touch progress
+    # variables only (order rows, progress rows lambda_{q+1} - lambda_q + mu_q = 0: they couple node q to
+    # q + 1 only) form a front of node q; inside an interval the node fronts are a chain, each the child
+    # of the next and the last the child of the leaf, with the node's (nu, complementarity row) pairs as a
+    # pre-front below it. In the leaf they would add ~200 positions (fig-8 56 x 4 with eight waypoints:
+    # 360, over the kernels' 288); as a chain each front holds ~31 own positions and trails the node
+    # positions of its interval and the next node's lambda.
+    chain_last: List[List[int]] = [[] for _ in range(S)]
+    in_chain = np.zeros(n + m, bool)
+    if node_groups is not None:
+        gvar = gnode >= 0
+        rmin = np.full(m, np.iinfo(np.int64).max)
+        np.minimum.at(rmin, jr, np.where(gvar[jc], gnode[jc], np.iinfo(np.int64).max))
+        n_non = np.bincount(jr[~gvar[jc]], minlength=m)           # entries on other variables
+        paired = np.zeros(m, bool)
+        for lst in npairs.values():
+            paired[[r for _, r in lst]] = True
+        crow = interior & ~anchor_only & ~root_only & (n_non == 0) & (rmin < len(node_groups)) & ~paired
+        rows_of: Dict[int, List[int]] = {}
+        for r in np.nonzero(crow)[0]:
+            rows_of.setdefault(int(rmin[r]), []).append(int(r))
+        pending: Dict[int, List[int]] = {}         # fronts of an interval waiting for the next chain front
+        for q, g in enumerate(node_groups):
+            g = np.asarray(g, np.int64)
+            st = int(var_stage[g[0]])
+            pv = {v for v, _ in npairs.get(q, [])}
+            vs = np.array([v for v in g if not anchor[v] and not root_anchor[v] and v not in pv], np.int64)
+            rs = np.array(sorted(r for r in rows_of.get(q, []) if lo[r] == st), np.int64)
+            kids = pending.pop(st, [])
+            if q in npairs:
+                pl = npairs[q]
+                kids.append(len(own))
+                own.append(np.concatenate([np.sort([v for v, _ in pl]), n + np.sort([r for _, r in pl])]))
+                children.append([])
+                for v, r in pl:
+                    in_chain[v] = True
+                    in_chain[n + r] = True
+            if len(vs) or len(rs):
+                pending[st] = [len(own)]
+                own.append(np.concatenate([vs, n + rs]))
+                children.append(kids)
+                in_chain[vs] = True
+                in_chain[n + rs] = True
+            else:
+                pending[st] = kids
+        for st, fl in pending.items():
+            chain_last[st] = fl
     # saddle fronts: the states of nodes 1..K and their ODE defect rows (collocation_saddle), when
     # every one of them lies inside the leaf (not an anchor, not in a pre-front pair)
     sad_id = [-1] * S
@@ -314,9 +380,10 @@ def _fronts_nd(n, var_stage, lo, hi, j_row_ptr, j_col, split_pairs=True, saddle=
             inner = inner[~np.isin(inner, pre[st])]
         if len(sad[st]):
             inner = inner[~np.isin(inner, sad[st])]
+        inner = inner[~in_chain[inner]]
         leaf_id.append(len(own))
         own.append(inner)
-        children.append([c for c in (pre_id[st], sad_id[st]) if c >= 0])
+        children.append([c for c in (pre_id[st], sad_id[st]) if c >= 0] + chain_last[st])
 
     def sep(j):
         return np.concatenate([np.nonzero((var_stage == j) & anchor)[0],
@@ -341,10 +408,12 @@ def _fronts_nd(n, var_stage, lo, hi, j_row_ptr, j_col, split_pairs=True, saddle=
 
 
 def build_plan(n: int, m: int, var_stage, j_row_ptr, j_col, h_row_ptr, h_col, ordering: str = 'nd',
-               split_pairs: bool = True, saddle=None) -> KKTPlan:
+               split_pairs: bool = True, saddle=None, node_groups=None) -> KKTPlan:
     '''
     saddle: optional (cols, rows) saddle pairs (collocation_saddle) for the 'nd' ordering: every
     interval's set becomes a saddle front, a child of the interval's leaf.
+    node_groups: optional per-node variable groups (cpc_node_groups) eliminated as a chain of node
+    fronts below every leaf ('nd' ordering).
     '''
     var_stage = np.asarray(var_stage, np.int64)
     j_row_ptr = np.asarray(j_row_ptr, np.int64)
@@ -357,7 +426,7 @@ def build_plan(n: int, m: int, var_stage, j_row_ptr, j_col, h_row_ptr, h_col, or
         raise ValueError('Hessian couples different stages; the staged KKT does not apply')
     lo, hi = row_span(n, m, var_stage, j_row_ptr, j_col)
     if ordering == 'nd':
-        own, children, n_sad = _fronts_nd(n, var_stage, lo, hi, j_row_ptr, j_col, split_pairs, saddle)
+        own, children, n_sad = _fronts_nd(n, var_stage, lo, hi, j_row_ptr, j_col, split_pairs, saddle, node_groups)
     elif ordering == 'chain':
         own, children = _fronts_chain(n, var_stage, lo, hi)
         n_sad = [0] * len(own)

@@ -277,7 +277,8 @@ def main():
         if win['t0'] is None or win['t1'] is None:
             raise RuntimeError('the solve ended before the timed window began')
         window_s = max_over_ranks(win['t1'] - win['t0'], dev)
-        counts = torch.tensor([float(win['count']), float(win['timed'])], dtype=torch.float64, device=dev)
+        counts = torch.tensor([float(win['count']), float(win['timed']), float(win['count_main']),
+                               float(win['count_resto'])], dtype=torch.float64, device=dev)
         timed_min = torch.tensor([float(win['timed'])], dtype=torch.float64, device=dev)
         if world > 1:
             dist.all_reduce(counts, op=dist.ReduceOp.SUM)
@@ -292,7 +293,11 @@ def main():
             summ = summarize_records(allrec)
             steps_timed = int(timed_min.item())
             value = float(counts[0].item()) / window_s
-            sqp_full = {'solve_s': solve_s, 'lockstep_iterations': lockstep,
+            sqp_full = {'window': {'instance_iterations': int(counts[0].item()),
+                                   'main_loop': int(counts[2].item()), 'restoration_phases': int(counts[3].item()),
+                                   'note': 'value counts both, as IPOPT\'s iteration counter (and max_iter, and '
+                                           'instance_iterations below) does'},
+                        'solve_s': solve_s, 'lockstep_iterations': lockstep,
                         'iterations_per_s': summ['instance_iterations'] / solve_s,
                         'converged_solves_per_s': summ['converged'] / solve_s, 'max_iter': args.max_iter,
                         'records_all_gathered': {'bytes_per_instance': RECORD_BYTES, 'instances': len(allrec),

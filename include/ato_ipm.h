@@ -96,15 +96,19 @@ int ato_ipm_multipliers(const ato_ipm_dims* d, const ato_ipm_bounds* bd, const d
  * derivative; alpha: trial step; tht, pht: measures of the trial point; F [W][fmax][2] the
  * filter entries (theta, phi) of every column, nf [W] (int64) how many are valid; theta_max,
  * theta_min [W]; pend, first [W] (bytes 0/1): columns still searching, first trial of the
- * search. prm = HOST array {s_phi, s_theta, delta, eta_phi, gamma_theta, gamma_phi, obj_max_inc} (read on the
- * host and passed to the kernel by value; every other pointer is a device array). Outputs (bytes 0/1,
- * [W]): ok = pend and accepted, arm = ok and the Armijo (f-type) case, soc = pend, not
- * accepted, first trial and tht >= theta (a second-order correction is tried). */
+ * search. prm = HOST array {s_phi, s_theta, delta, eta_phi, gamma_theta, gamma_phi, obj_max_inc, compare_tol,
+ * max_filter_resets, filter_reset_trigger} (read on the host and passed to the kernel by value; every other
+ * pointer is a device array). The sufficient-decrease and Armijo tests hold up to compare_tol |reference|
+ * (IpUtils Compare_le). Outputs (bytes 0/1, [W]): ok = pend and accepted, arm = ok and the Armijo (f-type)
+ * case, soc = pend, not accepted, first trial and tht >= theta (a second-order correction is tried).
+ * fr_n, fr_cnt [W] int64, fr_last [W] bytes (in/out; all NULL: no heuristic): FilterLSAcceptor's filter reset
+ * heuristic state of the pend columns (resets so far, successive iterations whose last rejection was the
+ * filter's, last rejection was the filter's); a column whose filter is reset gets nf = 0. */
 int ato_ipm_filter_accept(int32_t W, int32_t fmax, const double* theta, const double* phi, const double* gphi_d,
                           const double* alpha, const double* tht, const double* pht, const double* F,
-                          const int64_t* nf, const double* theta_max, const double* theta_min,
-                          const uint8_t* pend, const uint8_t* first, const double* prm, uint8_t* ok,
-                          uint8_t* arm, uint8_t* soc, void* stream);
+                          int64_t* nf, const double* theta_max, const double* theta_min,
+                          const uint8_t* pend, const uint8_t* first, const double* prm, int64_t* fr_n,
+                          int64_t* fr_cnt, uint8_t* fr_last, uint8_t* ok, uint8_t* arm, uint8_t* soc, void* stream);
 
 /* IPOPT's PDPerturbationHandler per column (IpPDPerturbationHandler: ConsiderNewSystem,
  * PerturbForSingularity, PerturbForWrongInertia with the structural-degeneracy test; batched_ipm.py
@@ -127,10 +131,12 @@ int ato_ipm_perturb(int32_t op, int32_t W, int32_t m, const double* prm, int64_t
 /* Termination tests of a lockstep iteration (batched_ipm.py solve; IPOPT's ConvergenceCheck with the
  * acceptable-level counter), one thread per column, in place: act [W] bytes; n_acc, status [W] int64
  * (1 optimal, 2 acceptable, 3 max_iter; others unchanged). A column still active is optimal when
- * E0 <= tol, du / sf <= dual_inf_tol, pr_uns <= constr_viol_tol and co <= compl_inf_tol; otherwise its
- * n_acc counts consecutive E0 <= acceptable_tol and acceptable_iter of them make it acceptable; then
- * own >= lim ends it at max_iter. prm = HOST {tol, dual_inf_tol, constr_viol_tol, compl_inf_tol,
- * acceptable_tol, acceptable_iter}. E0, du, pr_uns, co, sf fp64 [W]; own, lim int64 [W]. */
+ * E0 <= tol, du / sf <= dual_inf_tol, pr_uns <= constr_viol_tol and co / sf <= compl_inf_tol; otherwise
+ * its n_acc counts consecutive acceptable iterates (CurrentIsAcceptable: E0 <= acceptable_tol, du / sf <=
+ * acceptable_dual_inf_tol, pr_uns <= acceptable_constr_viol_tol, co / sf <= acceptable_compl_inf_tol) and
+ * acceptable_iter of them make it acceptable; then own >= lim ends it at max_iter. prm = HOST {tol,
+ * dual_inf_tol, constr_viol_tol, compl_inf_tol, acceptable_tol, acceptable_iter, acceptable_dual_inf_tol,
+ * acceptable_constr_viol_tol, acceptable_compl_inf_tol}. E0, du, pr_uns, co, sf fp64 [W]; own, lim int64 [W]. */
 int ato_ipm_status(int32_t W, const double* prm, const double* E0, const double* du, const double* pr_uns,
                    const double* co, const double* sf, const int64_t* own, const int64_t* lim, uint8_t* act,
                    int64_t* n_acc, int64_t* status, void* stream);

@@ -174,6 +174,59 @@ def test_asynchronous_restoration_matches_synchronous():
     assert torch.allclose(r0.x, r1.x, rtol=1e-9, atol=1e-9)
 
 
+def test_failed_fork_reserve_falls_back_to_synchronous_restoration(monkeypatch):
+    ''' the r05h crash path: a KKT storage reservation that cannot fit returns an
+    error code and leaves the handle without storage (ato_kkt_reserve is transactional), which factor
+    refuses instead of writing through half-allocated buffers; a later reservation that fits works.
+    In a batched solve whose restoration phases cannot reserve their own storage, every phase runs
+    synchronously on the main storage, and every instance ends as in the synchronous solve. '''
+    import ctypes
+    from aircraft_trajectory_optimization_amd.solver.batched_ipm import device_solver
+    from aircraft_trajectory_optimization_amd.solver.kkt_device import DeviceKKT, KKTReserveError
+    from aircraft_trajectory_optimization_amd.tracks import make_spec
+    spec = make_spec(track='race', N=5, K=2)
+    B = 24
+    sol0 = device_solver(spec, B, spec.lbw, spec.ubw, IPMOptions(max_iter=150))
+    fork = sol0.kkt.fork()
+    too_big = int(min(2 ** 31 - 1, 2e12 // (8 * max(1, fork.plan.l_size))))     # ~2 TB of factor storage
+    with pytest.raises(KKTReserveError):
+        fork.ensure(too_big)
+    assert fork.cap == 0
+    lib = fork.lib
+    rc = lib.ato_kkt_factor(fork.handle, 1, None, 1, 1, None, ctypes.c_void_p(8), ctypes.c_void_p(8),
+                            ctypes.c_void_p(8), ctypes.c_void_p(8), None)
+    assert rc != 0 and b'reserve' in lib.ato_last_error()
+    fork.ensure(8)                                  # fits again
+    assert fork.cap == 8
+    fork.close()
+
+    rng = np.random.default_rng(4)
+    W = np.repeat(spec.w0[None], B, axis=0)
+    for b in range(B):
+        W[b, :spec.N] *= 1 + 0.1 * rng.uniform(-1, 1, spec.N)
+    opts = IPMOptions(max_iter=150)
+    sync = device_solver(spec, B, spec.lbw, spec.ubw, opts)
+    sync.async_restoration = False
+    r0 = sync.solve(W)
+    real_fork, real_ensure = DeviceKKT.fork, DeviceKKT.ensure
+
+    def fork_(self):
+        k = real_fork(self)
+        k._fail_reserve = True
+        return k
+
+    def ensure_(self, count):                    # every reservation of a phase's own storage fails
+        return real_ensure(self, too_big if getattr(self, '_fail_reserve', False) else count)
+    monkeypatch.setattr(DeviceKKT, 'fork', fork_)
+    monkeypatch.setattr(DeviceKKT, 'ensure', ensure_)
+    r1 = device_solver(spec, B, spec.lbw, spec.ubw, opts).solve(W)
+    assert r1.stats.get('async_reserve_failed', 0) > 0 and r1.stats.get('async_phases', 0) == 0
+    assert r0.stats['restorations'] > 0 and r0.stats['restorations'] == r1.stats['restorations']
+    assert r0.status == r1.status
+    assert [int(i) for i in r0.iters] == [int(i) for i in r1.iters]
+    assert torch.allclose(r0.x, r1.x, rtol=1e-9, atol=1e-9)
+
+
 def test_trial_point_evaluation_matches_full_evaluation():
     ''' the line search evaluates trial points without the Jacobian (eval_fg); its f and g are
     those of the full evaluation (bitwise on this build; asserted to 1e-13 relative), on the full
@@ -214,9 +267,9 @@ def test_cold_start_batch_converges_to_oracle_kkt_points():
 def test_config3_full_size_cold_start_batch():
     '''
     Config 3 at its full size: racetrack 50 x 4 drone (parametric, ESP, global_r), seeded cold starts
-    0..63 (raceline/instances.py), IPOPT's max_iter 1000 -- the bench's workload on 64 of its 512
-    instances. At least 80 % of the instances converge (the full batch: 414 / 512 = 81 %); every converged
-    instance satisfies the oracle's constraints and every 8th converged one the full oracle KKT
+    0..127 (raceline/instances.py), IPOPT's max_iter 1000 -- the bench's workload on 128 of its 512
+    instances. At least 80 % of the instances converge (the full batch: 429 / 512 = 84 %); every converged
+    instance satisfies the oracle's constraints and every 16th converged one the full oracle KKT
     certificate (g, complex-step Lagrangian gradient; 5 s per instance on the host).
     Primal tolerance: IPOPT's test is |g - s| / s_g <= constr_viol_tol = 1e-4 in unscaled units, and the
     slacks live in bounds relaxed by bound_relax_factor 1e-8 in SCALED units, i.e. 1e-8 / s_g unscaled;
@@ -231,17 +284,18 @@ def test_config3_full_size_cold_start_batch():
     from aircraft_trajectory_optimization_amd.tracks import make_spec
     kw = dict(track='race', N=50, K=4)
     spec = make_spec(**kw)
-    B = 64
+    B = 128
     W, LBW, UBW = seeded_instances(spec, range(B))
     import time
     t0 = time.time()
     res = device_solver(spec, B, LBW, UBW, IPMOptions(max_iter=1000)).solve(W)
     torch.cuda.synchronize()
     ok = [b for b, st in enumerate(res.status) if st in ('optimal', 'acceptable')]
-    print(f'config 3, 64 cold starts: {time.time() - t0:.1f} s, statuses',
+    print(f'config 3, {B} cold starts: {time.time() - t0:.1f} s, statuses',
           {s: res.status.count(s) for s in sorted(set(res.status))}, 'watchdog', res.stats.get('watchdog'))
-    # round 5 (IPOPT-faithful perturbation handling and restoration): 54 / 64 here, 414 / 512 on the
-    # whole batch (gpurun_out r05d); round 4's restatement reached 482 / 512
+    # round 6 (IPOPT's filter reset heuristic, Compare_le tolerances, iterative refinement):
+    # 106 / 128 here, 429 / 512 on the whole batch (gpurun_out r06d; round 5: 414 / 512, round 4's
+    # restatement of another perturbation policy 482 / 512). The failures are classified in DESIGN 5.5.
     assert len(ok) >= 0.8 * B, res.status
     nlp = oracle_nlp(**kw)
     x = res.x.cpu().numpy()
@@ -255,7 +309,7 @@ def test_config3_full_size_cold_start_batch():
         viols.append(max(np.max(np.maximum(lbg - g, 0)), np.max(np.maximum(g - ubg, 0))))
     print('primal violation on the oracle: max %.2e, median %.2e' % (max(viols), float(np.median(viols))))
     assert max(viols) <= tol['primal'], viols
-    sub = [b for i, b in enumerate(ok) if i % 8 == 0]
+    sub = [b for i, b in enumerate(ok) if i % 16 == 0]
 
     class _Sub:
         status = [res.status[b] for b in sub]

@@ -21,8 +21,14 @@ sys.path.insert(0, ROOT)
 
 
 def _work(args):
-    seed, budget, spec_kw = args
+    seed, budget, spec_kw, core = args
+    if core is not None:
+        try:                                   # one worker per core: no migration between cores
+            os.sched_setaffinity(0, {core})
+        except (AttributeError, OSError):
+            pass
     import numpy as np
+    from threadpoolctl import threadpool_limits
     from aircraft_trajectory_optimization_amd.raceline.instances import seeded_instances
     from aircraft_trajectory_optimization_amd.solver.ipm import InteriorPointSolver, IPMOptions
     from aircraft_trajectory_optimization_amd.tracks import make_spec
@@ -30,24 +36,41 @@ def _work(args):
     spec = make_spec(**spec_kw)
     ev = HostEvaluator(spec)
     W, L, U = seeded_instances(spec, [seed])
-    t0 = time.perf_counter()
-    deadline = t0 + budget
-    r = InteriorPointSolver(ev, L[0], U[0], ev.lbg, ev.ubg, IPMOptions(max_iter=1000)).solve(
-        W[0], stop_check=lambda x: time.perf_counter() > deadline)
-    return {'seed': int(seed), 'iterations': int(r.iters), 'seconds': time.perf_counter() - t0,
-            'status': r.status, 'lap': float(np.sum(r.x[:spec.N]))}
+    with threadpool_limits(limits=1):
+        # set-up and a 3-iteration warm-up outside the timed solve, as the 1-core leg does (bench.py)
+        InteriorPointSolver(ev, L[0], U[0], ev.lbg, ev.ubg, IPMOptions(max_iter=3)).solve(W[0])
+        solver = InteriorPointSolver(ev, L[0], U[0], ev.lbg, ev.ubg, IPMOptions(max_iter=1000))
+        t0 = time.perf_counter()
+        deadline = t0 + budget
+        r = solver.solve(W[0], stop_check=lambda x: time.perf_counter() > deadline)
+        dt = time.perf_counter() - t0
+    return {'seed': int(seed), 'iterations': int(r.iters), 'seconds': dt, 'status': r.status,
+            'lap': float(np.sum(r.x[:spec.N])), 'core': core}
+
+
+def _cores(workers):
+    ''' distinct cores of this process's affinity set for the workers (None when there are too few) '''
+    try:
+        avail = sorted(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return [None] * workers
+    return avail[:workers] if len(avail) >= workers else [None] * workers
 
 
 def run(workers, budget, seeds, spec_kw):
     ctx = get_context('fork')
     t0 = time.perf_counter()
+    cores = _cores(len(seeds))
     with ctx.Pool(workers) as pool:
-        res = pool.map(_work, [(s, budget, spec_kw) for s in seeds])
+        res = pool.map(_work, [(s, budget, spec_kw, c) for s, c in zip(seeds, cores)], chunksize=1)
     wall = time.perf_counter() - t0
     iters = sum(r['iterations'] for r in res)
     secs = max(r['seconds'] for r in res)
+    per = [r['iterations'] / r['seconds'] for r in res]
     return {'workers': workers, 'budget_s': budget, 'wall_s': wall, 'iterations': iters,
-            'iterations_per_s': iters / secs, 'per_worker': res}
+            'iterations_per_s': iters / secs, 'per_worker_iterations_per_s': {'min': min(per), 'max': max(per),
+                                                                             'mean': sum(per) / len(per)},
+            'pinned': cores[0] is not None, 'per_worker': res}
 
 
 if __name__ == '__main__':
@@ -57,6 +80,7 @@ if __name__ == '__main__':
     ap.add_argument('--seeds', type=int, nargs='*', default=None)
     ap.add_argument('--spec', default='{}', help='make_spec keyword arguments (JSON)')
     a = ap.parse_args()
-    os.environ['OMP_NUM_THREADS'] = '1'          # one core per worker (BLAS inside the KKT blocks)
+    for k in ('OMP_NUM_THREADS', 'OPENBLAS_NUM_THREADS', 'MKL_NUM_THREADS', 'BLIS_NUM_THREADS'):
+        os.environ[k] = '1'                      # one core per worker (BLAS inside the KKT blocks, the C++ twin)
     seeds = a.seeds if a.seeds else list(range(a.workers))
     print(json.dumps(run(a.workers, a.budget, seeds, json.loads(a.spec))), flush=True)

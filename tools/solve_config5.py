@@ -23,6 +23,8 @@ def main():
     ap.add_argument('--pose', choices=['dcm', 'esp'], default='dcm')
     ap.add_argument('--max-iter', type=int, default=1000)
     ap.add_argument('--seed0', type=int, default=0)
+    ap.add_argument('--jac32', action='store_true', help='the Jacobian from the fp32 evaluation kernel')
+    ap.add_argument('--opts', default='{}', help='IPMOptions overrides (JSON)')
     ap.add_argument('--out', default=None)
     a = ap.parse_args()
     from aircraft_trajectory_optimization_amd.raceline.batch_instances import corridor_batch
@@ -38,7 +40,8 @@ def main():
     t_point = time.time() - t0
     print(f'point-mass solves {t_point:.1f} s', {s: pst.count(s) for s in set(pst)}, flush=True)
     t0 = time.time()
-    solver = device_solver(spec, B, LBW, UBW, IPMOptions(max_iter=a.max_iter))
+    solver = device_solver(spec, B, LBW, UBW, IPMOptions(**{**json.loads(a.opts), 'max_iter': a.max_iter}),
+                           jac32=a.jac32)
     res = solver.solve(W, progress=20)
     torch.cuda.synchronize()
     t = time.time() - t0
@@ -52,8 +55,9 @@ def main():
            'restorations': res.stats.get('restorations'),
            'lap_converged': [float(laps[ok].min()), float(np.median(laps[ok])), float(laps[ok].max())] if ok else None,
            'point_lap': [float(plap.min()), float(plap.max())],
-           'status_list': st}
-    print(json.dumps({k: v for k, v in out.items() if k != 'status_list'}), flush=True)
+           'status_list': st, 'laps': [float(v) for v in laps],
+           'final_e0': [float(v) for v in np.asarray(solver.final_e0)]}
+    print(json.dumps({k: v for k, v in out.items() if k not in ('status_list', 'laps', 'final_e0')}), flush=True)
     if a.out:
         with open(a.out, 'w') as f:
             json.dump(out, f)

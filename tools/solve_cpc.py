@@ -26,6 +26,7 @@ def main():
     ap.add_argument('--N', type=int, default=56)
     ap.add_argument('--max-iter', type=int, default=1000)
     ap.add_argument('--out', default=None)
+    ap.add_argument('--opts', default='{}', help='IPMOptions overrides (JSON)')
     a = ap.parse_args()
     from aircraft_trajectory_optimization_amd.solver.batched_ipm import device_solver
     from aircraft_trajectory_optimization_amd.solver.ipm import IPMOptions
@@ -38,7 +39,7 @@ def main():
         W[b, :spec.N] *= np.random.default_rng(b).uniform(0.95, 1.05, spec.N)
     W = np.clip(W, spec.lbw, spec.ubw)
     t0 = time.time()
-    solver = device_solver(spec, B, spec.lbw, spec.ubw, IPMOptions(max_iter=a.max_iter))
+    solver = device_solver(spec, B, spec.lbw, spec.ubw, IPMOptions(**{**json.loads(a.opts), 'max_iter': a.max_iter}))
     res = solver.solve(W, progress=50)
     torch.cuda.synchronize()
     t = time.time() - t0
