@@ -120,3 +120,73 @@ def corridor_batch(B: int, device=None, seeds=None, progress: int = 0, **kw):
     LBW, UBW = corridor_bounds(spec, seeds, LBW, UBW)
     W = np.clip(W, LBW, UBW)
     return spec, W, LBW, UBW, list(pres.status), XP[:, :pspec.N].sum(1)
+
+
+def cpc_warm_batch(B: int, device=None, seeds=None, use_dcm: bool = True, N: int = 56, K: int = 4,
+                   tol: float = 0.3, track: str = 'fig8'):
+    '''
+    Config 5's CPC instances (build-side gate-progress formulation, global frame; parity unpinned), warm
+    started the reference's way (use_ws, drone_raceline.py:158-274) from a point-mass raceline of the SAME
+    formulation: one point-mass CPC solve on the device (waypoints, one total time; from its own progress
+    guess), then the drone guess from its trajectory (attitude from thrust and velocity, body rates,
+    thrusts) with the point mass's progress variables (the node layout of both is the same). Instance
+    b > 0 perturbs that start as perturbed_warm_starts does. Returns (spec, W, LBW, UBW, point-mass lap).
+    (A drone raceline through the gates re-sampled on a uniform time grid is a worse start: the gate
+    rows let the path pass the waypoints by up to the gate opening, the complementarity rows do not.)
+    '''
+    from aircraft_trajectory_optimization_amd.raceline.warmstart import drone_guess
+    from aircraft_trajectory_optimization_amd.solver.batched_ipm import device_solver
+    from aircraft_trajectory_optimization_amd.solver.ipm import IPMOptions
+    from aircraft_trajectory_optimization_amd.tracks import make_spec
+    cpc = {'waypoints': None, 'tol': tol}
+    kw = dict(track=track, frame='global', N=N, K=K, use_quat=True, global_r=True, use_dcm=use_dcm)
+    pspec = make_spec(**{**kw, 'model': 'point', 'use_quat': False, 'use_dcm': False, 'cpc': cpc})
+    psolver = device_solver(pspec, 1, pspec.lbw[None], pspec.ubw[None], IPMOptions(max_iter=3000), device=device)
+    pres = psolver.solve(pspec.w0[None])
+    if pres.status[0] not in ('optimal', 'acceptable'):
+        raise RuntimeError(f'CPC warm start: point-mass solve {pres.status[0]}')
+    x = pres.x[:, 0].cpu().numpy()
+    p0 = make_spec(**{**kw, 'model': 'point', 'use_quat': False, 'use_dcm': False})
+    d0 = make_spec(**{**kw, 'model': 'drone'})
+    nx = p0.nw
+    w0, lbw, ubw, flip, wraps = drone_guess(d0, p0, x[:nx])
+    spec = make_spec(**{**kw, 'model': 'drone', 'quat_flip': flip, 'euler_wraps': wraps, 'cpc': cpc})
+    spec.w0 = np.concatenate([np.asarray(w0, float), x[nx:]])
+    spec.lbw = np.concatenate([np.asarray(lbw, float), pspec.lbw[nx:]])
+    spec.ubw = np.concatenate([np.asarray(ubw, float), pspec.ubw[nx:]])
+    W, LBW, UBW = perturbed_warm_starts(spec, B, seeds)
+    return spec, W, LBW, UBW, float(x[:pspec.N].sum())
+
+
+def resample_uniform_time(spec: ProblemSpec, w) -> np.ndarray:
+    '''
+    A collocation solution w of `spec` (global frame) re-sampled on a uniform time grid of the same N, K:
+    every step size becomes T / N (T = sum h, the lap time), and every node variable is interpolated in time
+    (linear between the old nodes, the lap closed periodically); quaternions are renormalised, DCM
+    attitudes projected back onto SO(3) (polar factor). The CPC formulation has one total time (all h
+    equal): a solution with phase-wise steps would violate its dynamics by O(h differences).
+    '''
+    w = np.asarray(w, float)
+    N, K1, nv, nz = spec.N, spec.K1, spec.nv, spec.nz
+    h = w[:N]
+    T = float(h.sum())
+    t0 = np.concatenate([[0.0], np.cumsum(h)[:-1]])
+    told = (t0[:, None] + spec.tau[None, :] * h[:, None]).reshape(-1)       # node times
+    Z = w[N:N + spec.P * nv].reshape(spec.P, nv)
+    hn = T / N
+    tnew = (np.arange(N)[:, None] * hn + spec.tau[None, :] * hn).reshape(-1)
+    # periodic extension: the closed lap's first node follows the last one at time T
+    tx = np.concatenate([told, [T]])
+    Zx = np.vstack([Z, Z[:1]])
+    Zn = np.stack([np.interp(tnew, tx, Zx[:, c]) for c in range(nv)], axis=1)
+    if spec.is_drone:
+        if nz == 18:                                   # DCM: rows 3..12, project on SO(3)
+            for q in range(spec.P):
+                U_, _, Vt = np.linalg.svd(Zn[q, 3:12].reshape(3, 3))
+                Zn[q, 3:12] = (U_ @ Vt).reshape(-1)
+        elif nz == 13:                                 # quaternion 3..7
+            Zn[:, 3:7] /= np.linalg.norm(Zn[:, 3:7], axis=1, keepdims=True)
+    out = w.copy()
+    out[:N] = hn
+    out[N:N + spec.P * nv] = Zn.reshape(-1)
+    return out

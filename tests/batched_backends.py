@@ -60,12 +60,23 @@ class HostBatchEvaluator:
 
 
 class HostBlockKKT:
+    # the refinement residual rhs - K x from the assembled matrix of each instance, as the single-instance
+    # solver computes it (scipy CSR product): both solvers then refine and decide identically
+    residual_lists = True
+
     def __init__(self, ev: HostBatchEvaluator):
         self.ev = ev
         self.bk = BlockKKT(ev.n, ev.m, ev.var_stage, ev.j_row_ptr, ev.j_col, ev.h_row_ptr, ev.h_col)
         self.jr = np.repeat(np.arange(ev.m), np.diff(ev.j_row_ptr))
         self.fac = [None] * ev.batch
+        self.K = [None] * ev.batch
         self.inertia = torch.zeros((ev.batch, 3), dtype=torch.int32)
+
+    def residual(self, H, J, dx, dr, x, rhs, instances=None):
+        out = torch.zeros_like(rhs)
+        for b in (range(self.ev.batch) if instances is None else instances):
+            out[:, b] = torch.as_tensor(rhs[:, b].numpy() - self.K[b] @ x[:, b].numpy())
+        return out
 
     def factor(self, H, J, dx, dr, instances):
         ev = self.ev
@@ -76,6 +87,7 @@ class HostBlockKKT:
             K = sp.bmat([[W + sp.diags(dx[:, b].numpy()), Jm.T], [Jm, sp.diags(dr[:, b].numpy())]], format='csr')
             f, inertia = self.bk.factor(K)
             self.fac[b] = f
+            self.K[b] = K
             self.inertia[b] = torch.as_tensor(inertia)
         return self.inertia
 

@@ -27,19 +27,29 @@ def main():
     ap.add_argument('--max-iter', type=int, default=1000)
     ap.add_argument('--out', default=None)
     ap.add_argument('--opts', default='{}', help='IPMOptions overrides (JSON)')
+    ap.add_argument('--warm', action='store_true', help='warm start from a point-mass raceline '
+                                                        '(raceline/batch_instances.py cpc_warm_batch)')
     a = ap.parse_args()
     from aircraft_trajectory_optimization_amd.solver.batched_ipm import device_solver
     from aircraft_trajectory_optimization_amd.solver.ipm import IPMOptions
     from aircraft_trajectory_optimization_amd.tracks import make_spec
     B = a.batch
-    spec = make_spec(track='fig8', model='drone', frame='global', N=a.N, K=4, use_quat=True, global_r=True,
-                     use_dcm=a.pose == 'dcm', cpc={'waypoints': None, 'tol': 0.3})
-    W = np.repeat(spec.w0[None], B, axis=0)
-    for b in range(1, B):
-        W[b, :spec.N] *= np.random.default_rng(b).uniform(0.95, 1.05, spec.N)
-    W = np.clip(W, spec.lbw, spec.ubw)
+    LBW = UBW = None
+    if a.warm:
+        from aircraft_trajectory_optimization_amd.raceline.batch_instances import cpc_warm_batch
+        spec, W, LBW, UBW, plap = cpc_warm_batch(B, use_dcm=a.pose == 'dcm', N=a.N)
+        print(f'point-mass warm start: lap {plap:.4f} s', flush=True)
+    else:
+        spec = make_spec(track='fig8', model='drone', frame='global', N=a.N, K=4, use_quat=True, global_r=True,
+                         use_dcm=a.pose == 'dcm', cpc={'waypoints': None, 'tol': 0.3})
+        W = np.repeat(spec.w0[None], B, axis=0)
+        for b in range(1, B):
+            W[b, :spec.N] *= np.random.default_rng(b).uniform(0.95, 1.05, spec.N)
+        W = np.clip(W, spec.lbw, spec.ubw)
+    LBW = spec.lbw if LBW is None else LBW
+    UBW = spec.ubw if UBW is None else UBW
     t0 = time.time()
-    solver = device_solver(spec, B, spec.lbw, spec.ubw, IPMOptions(**{**json.loads(a.opts), 'max_iter': a.max_iter}))
+    solver = device_solver(spec, B, LBW, UBW, IPMOptions(**{**json.loads(a.opts), 'max_iter': a.max_iter}))
     res = solver.solve(W, progress=50)
     torch.cuda.synchronize()
     t = time.time() - t0
