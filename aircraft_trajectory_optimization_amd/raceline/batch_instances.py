@@ -141,11 +141,17 @@ def cpc_warm_batch(B: int, device=None, seeds=None, use_dcm: bool = True, N: int
     cpc = {'waypoints': None, 'tol': tol}
     kw = dict(track=track, frame='global', N=N, K=K, use_quat=True, global_r=True, use_dcm=use_dcm)
     pspec = make_spec(**{**kw, 'model': 'point', 'use_quat': False, 'use_dcm': False, 'cpc': cpc})
-    psolver = device_solver(pspec, 1, pspec.lbw[None], pspec.ubw[None], IPMOptions(max_iter=3000), device=device)
-    pres = psolver.solve(pspec.w0[None])
-    if pres.status[0] not in ('optimal', 'acceptable'):
-        raise RuntimeError(f'CPC warm start: point-mass solve {pres.status[0]}')
-    x = pres.x[:, 0].cpu().numpy()
+    # a small batch of perturbed point-mass starts (the complementarity rows make single starts fragile):
+    # the converged one with the shortest lap is the warm start
+    PW, PL, PU = perturbed_warm_starts(pspec, 16)
+    psolver = device_solver(pspec, 16, PL, PU, IPMOptions(max_iter=3000), device=device)
+    pres = psolver.solve(PW)
+    ok = [b for b, st in enumerate(pres.status) if st in ('optimal', 'acceptable')]
+    if not ok:
+        raise RuntimeError(f'CPC warm start: no point-mass solve converged ({set(pres.status)})')
+    laps = pres.x[:pspec.N].sum(0).cpu().numpy()
+    x = pres.x[:, min(ok, key=lambda b: laps[b])].cpu().numpy()
+    cpc_warm_batch.point_statuses = list(pres.status)
     p0 = make_spec(**{**kw, 'model': 'point', 'use_quat': False, 'use_dcm': False})
     d0 = make_spec(**{**kw, 'model': 'drone'})
     nx = p0.nw

@@ -102,3 +102,76 @@ def test_config5_corridor_batch_quaternion_pose():
     kw, spec, LBW, UBW, res, ok = _corridor_solve(False, progress=0)
     assert len(ok) >= 0.99 * B, {s: res.status.count(s) for s in set(res.status)}
     _certify(kw, spec, LBW, UBW, res, ok, 128, False)
+
+
+@pytest.mark.timeout(300)
+def test_config5_fp32_jacobian_leg():
+    '''
+    Config 5's fp32 leg: the Jacobian of every iterate from the fp32 evaluation kernel (ato_eval_f32,
+    widened to fp64 for the KKT system), g, f, grad f and the Hessian in fp64 (BatchedDeviceEvaluator
+    jac32), on 256 corridor instances (quaternion pose). The fp32 Jacobian's rounding (~1e-7 relative) sits
+    in the dual residual grad f + J^T y, so IPOPT's tol 1e-8 is out of reach: the leg runs at tol 1e-6
+    (measured, gpurun_out r06e / r06i: 200 / 256 optimal, the fp64 solve 256 / 256). Its converged laps equal the
+    fp64 solve's within 1e-3 s (the north star's lap-time tolerance; measured 1.9e-4 s) and are KKT points of
+    the oracle's NLP at the fp32 level.
+    '''
+    from aircraft_trajectory_optimization_amd.raceline.batch_instances import corridor_batch
+    from aircraft_trajectory_optimization_amd.solver.batched_ipm import device_solver
+    from aircraft_trajectory_optimization_amd.solver.ipm import IPMOptions
+    from tests.helpers import kkt_certificate
+    B32 = 256
+    kw = dict(CFG, use_dcm=False)
+    spec, W, LBW, UBW, pst, _ = corridor_batch(B32, **{k: v for k, v in kw.items() if k != 'model'})
+    r64 = device_solver(spec, B32, LBW, UBW, IPMOptions(max_iter=1000)).solve(W)
+    r32 = device_solver(spec, B32, LBW, UBW, IPMOptions(max_iter=1000, tol=1e-6), jac32=True).solve(W)
+    ok64 = np.array([s == 'optimal' for s in r64.status])
+    ok32 = np.array([s in ('optimal', 'acceptable') for s in r32.status])
+    l64, l32 = (r.x[:spec.N].sum(0).cpu().numpy() for r in (r64, r32))
+    both = ok64 & ok32
+    print('fp32 Jacobian leg:', {s: r32.status.count(s) for s in set(r32.status)}, 'fp64:',
+          {s: r64.status.count(s) for s in set(r64.status)}, f'max lap difference {np.abs(l32 - l64)[both].max():.2e} s')
+    assert ok32.sum() >= 0.7 * B32
+    assert np.abs(l32 - l64)[both].max() <= 1e-3
+    nlp = oracle_nlp(**kw, quat_flip=spec.quat_flip)
+    for b in np.nonzero(ok32)[0][::64]:
+        c = kkt_certificate(nlp, r32.x[:, b].cpu().numpy(), r32.lam_g[:, b].cpu().numpy(),
+                            r32.lam_x[:, b].cpu().numpy(), LBW[b], UBW[b])
+        assert c['primal'] <= 1e-5 and c['dual'] <= 1e-4 and c['compl'] <= 1e-5, (b, c)
+
+
+@pytest.mark.timeout(600)
+def test_config5_cpc_solve():
+    '''
+    Config 5's CPC gate-progress formulation (build-side; parity UNPINNED: the reference only displays a
+    CPC CSV) solved as a batch: fig-8, global frame, 56 x 4, DCM pose, eight waypoints, 64 instances
+    warm-started from a point-mass CPC raceline (raceline/batch_instances.py cpc_warm_batch). The device
+    KKT runs the progress variables as a chain of node fronts (kkt_plan.cpc_node_groups; in the leaves they
+    made 360-position fronts, over the kernels' 288). The complementarity rows make this an MPCC, on which
+    the interior-point method converges rarely (measured 2 / 64, gpurun_out r06h): at least one instance
+    converges, and every converged one is a KKT point of the oracle's CPC NLP, passes every waypoint within
+    the tolerance and ends with all progress consumed.
+    '''
+    from aircraft_trajectory_optimization_amd.raceline.batch_instances import cpc_warm_batch
+    from aircraft_trajectory_optimization_amd.solver.batched_ipm import device_solver
+    from aircraft_trajectory_optimization_amd.solver.ipm import IPMOptions
+    from tests.helpers import kkt_certificate
+    Bc = 64
+    spec, W, LBW, UBW, _ = cpc_warm_batch(Bc, use_dcm=True)
+    res = device_solver(spec, Bc, LBW, UBW, IPMOptions(max_iter=1000)).solve(W, progress=50)   # (progress: a heartbeat)
+    ok = [b for b, s in enumerate(res.status) if s in ('optimal', 'acceptable')]
+    print('CPC solve:', {s: res.status.count(s) for s in set(res.status)})
+    assert len(ok) >= 1
+    kw = dict(track='fig8', model='drone', frame='global', N=spec.N, K=4, use_quat=True, global_r=True,
+              use_dcm=True)
+    nlp = oracle_nlp(**kw, quat_flip=spec.quat_flip, cpc=spec.cpc)
+    M, P = spec.cpc_m, spec.P
+    for b in ok:
+        x = res.x[:, b].cpu().numpy()
+        c = kkt_certificate(nlp, x, res.lam_g[:, b].cpu().numpy(), res.lam_x[:, b].cpu().numpy(), LBW[b], UBW[b])
+        assert c['primal'] <= 1e-5 and c['dual'] <= 1e-5 and c['compl'] <= 1e-5, (b, c)
+        prog = x[spec.cpc_off:].reshape(P, 3, M)
+        assert np.abs(prog[-1, 0]).max() <= 1e-6               # lambda = 0 at the end: every waypoint passed
+        pos = np.array([x[spec.col_z(q // spec.K1, q % spec.K1):spec.col_z(q // spec.K1, q % spec.K1) + 3]
+                        for q in range(P)])
+        d = np.sqrt(((pos[:, None] - spec.cpc['waypoints'][None]) ** 2).sum(-1)).min(0)
+        assert d.max() <= spec.cpc['tol'] + 1e-3, d

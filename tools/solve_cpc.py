@@ -38,7 +38,8 @@ def main():
     if a.warm:
         from aircraft_trajectory_optimization_amd.raceline.batch_instances import cpc_warm_batch
         spec, W, LBW, UBW, plap = cpc_warm_batch(B, use_dcm=a.pose == 'dcm', N=a.N)
-        print(f'point-mass warm start: lap {plap:.4f} s', flush=True)
+        print(f'point-mass warm start: lap {plap:.4f} s, point-mass statuses',
+              {k: cpc_warm_batch.point_statuses.count(k) for k in set(cpc_warm_batch.point_statuses)}, flush=True)
     else:
         spec = make_spec(track='fig8', model='drone', frame='global', N=a.N, K=4, use_quat=True, global_r=True,
                          use_dcm=a.pose == 'dcm', cpc={'waypoints': None, 'tol': 0.3})
