@@ -165,7 +165,20 @@ def _eval_into(problem, binder, B, X, n, m, nnz, jac, jac32=False):
     dev = X.device
     f = torch.empty(B, dtype=torch.float64, device=dev)
     g = torch.empty((m, B), dtype=torch.float64, device=dev)
-    gf = torch.zeros((n, B), dtype=torch.float64, device=dev)     # (sparse grad f mode: zeros stay)
+    # grad f: at an accepted point (jac) the kernels write every entry (ato_gradf_mode dense: no zero fill
+    # of a fresh buffer); a trial point needs only f, whose partials come with the gradient pass, so its
+    # sparse gradient goes to a scratch buffer of the binder (zero-filled once, never read)
+    sparse = not jac
+    if getattr(problem, '_gf_sparse', None) != sparse:
+        problem.gradf_mode(sparse)
+        problem._gf_sparse = sparse
+    if jac:
+        gf = torch.empty((n, B), dtype=torch.float64, device=dev)
+    else:
+        scratch = binder.__dict__.setdefault('_gf_scratch', {})
+        gf = scratch.get((B, dev))
+        if gf is None:
+            gf = scratch[(B, dev)] = torch.zeros((n, B), dtype=torch.float64, device=dev)
     J = torch.empty((nnz, B), dtype=torch.float64, device=dev) if jac and not jac32 else None
     st = torch.cuda.current_stream(dev)
     binder._bind_spheres()
@@ -1854,7 +1867,8 @@ class BatchedInteriorPoint:
                     iters=torch.as_tensor(res.iters, dtype=torch.long, device=dev), stats=stats,
                     laps=dict(sub.laps.t))
 
-    ASYNC_PHASES = 3                # restoration phases in flight at once (each: own handle, storage, stream)
+    # restoration phases in flight at once (each: own handle, storage, stream); ATO_ASYNC_PHASES overrides
+    ASYNC_PHASES = int(os.environ.get('ATO_ASYNC_PHASES', '3'))
     ASYNC_PHASE_BYTES = 4e9         # factor storage of one phase in flight (its columns are capped to fit)
     ASYNC_MAX_BATCH = 1 << 30       # (batches above it would restore synchronously, on the main storage)
 

@@ -204,6 +204,7 @@ def cpu_baseline(W, budget_s, spec_kw):
             'numpy_oracle_evals_per_s': r_np,
             'sqp_all_cores': None if allc is None or 'error' in allc else
             {'cores': allc['workers'], 'iterations_per_s': allc['iterations_per_s'], 'budget_s': allc['budget_s'],
+             'per_worker_iterations_per_s': allc.get('per_worker_iterations_per_s'), 'pinned': allc.get('pinned'),
              'sample': f"{allc['workers']} worker processes, one config-3 cold start each (seeds 0..), the same "
                        f"solver on the C++ twin + host block LDL^T, {allc['budget_s']:.0f} s each: "
                        f"{allc['iterations']} iterations"},
