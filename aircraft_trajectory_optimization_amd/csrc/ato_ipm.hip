@@ -533,6 +533,72 @@ struct FilterPrm {
     long long max_filter_resets, filter_reset_trigger;
 };
 
+// one trial's FilterLSAcceptor::CheckAcceptabilityOfTrialPoint: rejected by theta_max, the
+// current-iterate test (Armijo in the f-type case, else sufficient decrease; Compare_le tolerance;
+// obj_max_inc) or the filter
+struct TrialTest {
+    bool ok, arm_case, rej, it_ok, in_f;
+};
+
+__device__ __forceinline__ TrialTest filter_trial(const FilterPrm& o, double th, double ph, double gd, double al,
+                                                  double tt, double pt, const double* Fb, long long k1, int fmax,
+                                                  double tmax, double tmin) {
+    TrialTest r;
+    r.rej = !(tt <= tmax);
+    r.in_f = false;
+    const int kn = (int)(k1 < fmax ? k1 : fmax);
+    for (int k = 0; k < kn; ++k)
+        if (tt >= Fb[2 * k] && pt >= Fb[2 * k + 1]) r.in_f = true;
+    const double ngd = -gd;
+    const double mgd = ngd != ngd ? ngd : (ngd < 0.0 ? 0.0 : ngd);      // torch.clamp(min=0): NaN stays
+    const bool switching = (gd < 0.0) && (al * tpow(mgd, o.s_phi) > o.delta * tpow(th, o.s_theta));
+    r.arm_case = (th <= tmin) && switching;
+    // IpUtils Compare_le(lhs, rhs, base): lhs - rhs <= compare_tol |base| (ArmijoHolds,
+    // IsAcceptableToCurrentIterate)
+    const double dp = pt - ph;
+    const bool ok_arm = dp - (o.eta_phi * al) * gd <= o.compare_tol * fabs(ph);
+    const bool ok_suf = (tt - (1.0 - o.gamma_theta) * th <= o.compare_tol * fabs(th)) ||
+                        (dp - (-o.gamma_phi * th) <= o.compare_tol * fabs(ph));
+    // obj_max_inc (FilterLSAcceptor::CheckAcceptabilityOfTrialPoint): the barrier objective may not
+    // grow by more than 10^obj_max_inc of its magnitude
+    bool inc = false;
+    if (pt > ph) {
+        const double base = fabs(ph) > 10.0 ? log10(fabs(ph)) : 1.0;
+        inc = log10(pt - ph) > o.obj_max_inc + base;
+    }
+    r.it_ok = !inc && (r.arm_case ? ok_arm : ok_suf);
+    r.ok = !r.rej && r.it_ok && !r.in_f;
+    return r;
+}
+
+// the filter reset heuristic of CheckAcceptabilityOfTrialPoint for one tested trial: a rejection by
+// the current-iterate test clears "last rejection due to the filter", a rejection by the filter sets
+// it (theta_max leaves it); an acceptance after filter_reset_trigger successive iterations whose last
+// rejection was the filter's clears the filter (at most max_filter_resets times)
+__device__ __forceinline__ void filter_reset_step(const FilterPrm& o, const TrialTest& t, long long& n, long long& c,
+                                                  bool& last, long long& nf) {
+    if (t.rej) return;
+    if (!t.it_ok) {
+        last = false;
+    } else if (t.in_f) {
+        last = true;
+    } else {
+        if (o.max_filter_resets > 0 && n < o.max_filter_resets) {
+            if (last) {
+                ++c;
+                if (c >= o.filter_reset_trigger) {
+                    nf = 0;
+                    ++n;
+                    c = 0;
+                }
+            } else {
+                c = 0;
+            }
+        }
+        last = false;
+    }
+}
+
 __global__ __launch_bounds__(CB) void k_filter_accept(int W, int fmax, const double* __restrict__ theta,
                                                       const double* __restrict__ phi,
                                                       const double* __restrict__ gphi_d,
@@ -549,67 +615,73 @@ __global__ __launch_bounds__(CB) void k_filter_accept(int W, int fmax, const dou
                                                       uint8_t* __restrict__ soc_out) {
     const int b = blockIdx.x * CB + threadIdx.x;
     if (b >= W) return;
-    const double th = theta[b], ph = phi[b], gd = gphi_d[b], al = alpha[b], tt = tht[b], pt = pht[b];
-    const bool rej = !(tt <= theta_max[b]);
-    bool in_f = false;
-    const long long k1 = nf[b];
-    const double* Fb = F + (long long)b * fmax * 2;
-    const int kn = (int)(k1 < fmax ? k1 : fmax);
-    for (int k = 0; k < kn; ++k)
-        if (tt >= Fb[2 * k] && pt >= Fb[2 * k + 1]) in_f = true;
-    const double ngd = -gd;
-    const double mgd = ngd != ngd ? ngd : (ngd < 0.0 ? 0.0 : ngd);      // torch.clamp(min=0): NaN stays
-    const bool switching = (gd < 0.0) && (al * tpow(mgd, o.s_phi) > o.delta * tpow(th, o.s_theta));
-    const bool arm_case = (th <= theta_min[b]) && switching;
-    // IpUtils Compare_le(lhs, rhs, base): lhs - rhs <= compare_tol |base| (ArmijoHolds,
-    // IsAcceptableToCurrentIterate)
-    const double dp = pt - ph;
-    const bool ok_arm = dp - (o.eta_phi * al) * gd <= o.compare_tol * fabs(ph);
-    const bool ok_suf = (tt - (1.0 - o.gamma_theta) * th <= o.compare_tol * fabs(th)) ||
-                        (dp - (-o.gamma_phi * th) <= o.compare_tol * fabs(ph));
-    // obj_max_inc (FilterLSAcceptor::CheckAcceptabilityOfTrialPoint): the barrier objective may not
-    // grow by more than 10^obj_max_inc of its magnitude
-    bool inc = false;
-    if (pt > ph) {
-        const double base = fabs(ph) > 10.0 ? log10(fabs(ph)) : 1.0;
-        inc = log10(pt - ph) > o.obj_max_inc + base;
-    }
+    const double th = theta[b], tt = tht[b];
+    const TrialTest t = filter_trial(o, th, phi[b], gphi_d[b], alpha[b], tt, pht[b], F + (long long)b * fmax * 2,
+                                     nf[b], fmax, theta_max[b], theta_min[b]);
     const bool pd = pend[b] != 0;
-    const bool it_ok = !inc && (arm_case ? ok_arm : ok_suf);
-    const bool ok = pd && !rej && it_ok && !in_f;
+    const bool ok = pd && t.ok;
     ok_out[b] = ok ? 1 : 0;
-    arm_out[b] = (ok && arm_case) ? 1 : 0;
+    arm_out[b] = (ok && t.arm_case) ? 1 : 0;
     soc_out[b] = (pd && !ok && first[b] != 0 && tt >= th) ? 1 : 0;
-    // the filter reset heuristic of CheckAcceptabilityOfTrialPoint: a rejection by the current-iterate
-    // test clears "last rejection due to the filter", a rejection by the filter sets it (theta_max
-    // leaves it); an acceptance after filter_reset_trigger successive iterations whose last rejection
-    // was the filter's clears the filter (at most max_filter_resets times)
-    if (fr_n && pd && !rej) {
+    if (fr_n && pd) {
+        long long n = fr_n[b], c = fr_cnt[b], k = nf[b];
         bool last = fr_last[b] != 0;
-        if (!it_ok) {
-            last = false;
-        } else if (in_f) {
-            last = true;
-        } else {
-            long long n = fr_n[b], c = fr_cnt[b];
-            if (o.max_filter_resets > 0 && n < o.max_filter_resets) {
-                if (last) {
-                    ++c;
-                    if (c >= o.filter_reset_trigger) {
-                        nf[b] = 0;
-                        ++n;
-                        c = 0;
-                    }
-                } else {
-                    c = 0;
-                }
-            }
-            fr_n[b] = n;
-            fr_cnt[b] = c;
-            last = false;
-        }
+        filter_reset_step(o, t, n, c, last, k);
+        fr_n[b] = n;
+        fr_cnt[b] = c;
         fr_last[b] = last ? 1 : 0;
+        nf[b] = k;
     }
+}
+
+// K successive backtracking trials of each of P columns, evaluated together (trial k of column p at
+// alpha0[p] / 2^k; tht, pht [K][P]) and tested in order, exactly as K rounds of the lockstep line
+// search would (batched_ipm.py _multi_trials): a column stops at its first trial with alpha <= alpha_min
+// (failed) or at its first accepted trial (kacc = k, arm); the reset heuristic runs on every tested trial
+__global__ __launch_bounds__(CB) void k_filter_multi(int P, int K, int fmax, const double* __restrict__ theta,
+                                                     const double* __restrict__ phi,
+                                                     const double* __restrict__ gphi_d,
+                                                     const double* __restrict__ alpha0,
+                                                     const double* __restrict__ alpha_min,
+                                                     const double* __restrict__ tht, const double* __restrict__ pht,
+                                                     const double* __restrict__ F, int64_t* __restrict__ nf,
+                                                     const double* __restrict__ theta_max,
+                                                     const double* __restrict__ theta_min, FilterPrm o,
+                                                     int64_t* __restrict__ fr_n, int64_t* __restrict__ fr_cnt,
+                                                     uint8_t* __restrict__ fr_last, int32_t* __restrict__ kacc,
+                                                     uint8_t* __restrict__ fail_out, uint8_t* __restrict__ arm_out) {
+    const int p = blockIdx.x * CB + threadIdx.x;
+    if (p >= P) return;
+    const double th = theta[p], ph = phi[p], gd = gphi_d[p], amin = alpha_min[p];
+    const double tmax = theta_max[p], tmin = theta_min[p];
+    const double* Fb = F + (long long)p * fmax * 2;
+    long long n = fr_n[p], c = fr_cnt[p], k1 = nf[p];
+    bool last = fr_last[p] != 0;
+    int ka = -1;
+    bool fl = false, arm = false;
+    double al = alpha0[p];
+    for (int k = 0; k < K; ++k) {
+        if (!(al > amin)) {
+            fl = true;
+            break;
+        }
+        const TrialTest t = filter_trial(o, th, ph, gd, al, tht[(long long)k * P + p], pht[(long long)k * P + p], Fb,
+                                         k1, fmax, tmax, tmin);
+        filter_reset_step(o, t, n, c, last, k1);
+        if (t.ok) {
+            ka = k;
+            arm = t.arm_case;
+            break;
+        }
+        al = al * 0.5;
+    }
+    fr_n[p] = n;
+    fr_cnt[p] = c;
+    fr_last[p] = last ? 1 : 0;
+    nf[p] = k1;
+    kacc[p] = ka;
+    fail_out[p] = fl ? 1 : 0;
+    arm_out[p] = arm ? 1 : 0;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -973,6 +1045,24 @@ int ato_ipm_filter_accept(int32_t W, int32_t fmax, const double* theta, const do
                        fmax, theta, phi, gphi_d, alpha, tht, pht, F, nf, theta_max, theta_min, pend, first, o,
                        reinterpret_cast<int64_t*>(fr_n), reinterpret_cast<int64_t*>(fr_cnt), fr_last, ok, arm, soc);
     return check_launch("ato_ipm_filter_accept");
+}
+
+int ato_ipm_filter_multi(int32_t P, int32_t K, int32_t fmax, const double* theta, const double* phi,
+                         const double* gphi_d, const double* alpha0, const double* alpha_min, const double* tht,
+                         const double* pht, const double* F, int64_t* nf, const double* theta_max,
+                         const double* theta_min, const double* prm, int64_t* fr_n, int64_t* fr_cnt, uint8_t* fr_last,
+                         int32_t* kacc, uint8_t* failed, uint8_t* arm, void* stream) {
+    if (P < 0 || K < 1 || fmax < 0 || !prm) return fail(ATO_ERR_ARG, "ato_ipm_filter_multi: arguments");
+    if (P == 0) return 0;
+    if (!theta || !phi || !gphi_d || !alpha0 || !alpha_min || !tht || !pht || (fmax && !F) || !nf || !theta_max ||
+        !theta_min || !fr_n || !fr_cnt || !fr_last || !kacc || !failed || !arm)
+        return fail(ATO_ERR_ARG, "ato_ipm_filter_multi: arguments");
+    const FilterPrm o{prm[0], prm[1], prm[2], prm[3], prm[4], prm[5], prm[6], prm[7], (long long)prm[8],
+                      (long long)prm[9]};
+    hipLaunchKernelGGL(k_filter_multi, dim3((P + CB - 1) / CB), dim3(CB), 0, static_cast<hipStream_t>(stream), P, K,
+                       fmax, theta, phi, gphi_d, alpha0, alpha_min, tht, pht, F, nf, theta_max, theta_min, o, fr_n,
+                       fr_cnt, fr_last, kacc, failed, arm);
+    return check_launch("ato_ipm_filter_multi");
 }
 
 int ato_ipm_status(int32_t W, const double* prm, const double* E0, const double* du, const double* pr_uns,

@@ -648,14 +648,15 @@ class BatchedInteriorPoint:
             return self.vk.measures(self._bd(), x, s, g, self.c_rhs, f, mu, self.o.kappa_d)
         return self._resid(g, s).abs().sum(0), self._phi(f, x, s, mu)
 
-    def _accept(self, theta, phi, gphi_d, alpha, tht, pht, F, nf, theta_min=None, pend=None, frs=None):
+    def _accept(self, theta, phi, gphi_d, alpha, tht, pht, F, nf, theta_min=None, pend=None, frs=None,
+                theta_max=None):
         ''' filter acceptance per instance (solver/ipm.py _accept): (accepted, is_armijo_step). With
         pend, only those columns are tested (accepted is False elsewhere); with frs = (fr_n, fr_cnt,
         fr_last) the filter reset heuristic runs on the tested columns, in place on frs and nf
         (the torch formulation of ato_ipm_filter_accept) '''
         o = self.o
         theta_min = self.theta_min if theta_min is None else theta_min
-        rej = ~(tht <= self.theta_max)
+        rej = ~(tht <= (self.theta_max if theta_max is None else theta_max))
         base = torch.where(phi.abs() > 10.0, torch.log10(phi.abs()), torch.ones_like(phi))
         inc = (pht > phi) & (torch.log10(torch.clamp(pht - phi, min=1e-300)) > o.obj_max_inc + base)
         k = torch.arange(F.shape[1], device=self.dev)
@@ -687,6 +688,70 @@ class BatchedInteriorPoint:
             fr_last.copy_(torch.where((ev & ~it_ok) | acc, torch.zeros_like(fr_last),
                                       torch.where(ev & it_ok & in_f, torch.ones_like(fr_last), fr_last)))
         return ok, ok & arm_case
+
+    def _filter_multi(self, theta, phi, gphi_d, alpha0, alpha_min, tht, pht, F, nf, theta_max, theta_min, frs):
+        ''' K successive backtracking trials of P columns (tht, pht [K][P]; trial k at alpha0 / 2^k) tested in
+        order, as K rounds of the lockstep line search would: (kacc [P] (-1: none), failed [P], arm [P]); the
+        fused kernel on the device (ato_ipm_filter_multi), its torch formulation here '''
+        if self.vk is not None:
+            return self.vk.filter_multi(theta, phi, gphi_d, alpha0, alpha_min, tht, pht, F, nf, theta_max, theta_min,
+                                        self.o, frs)
+        K, P = tht.shape
+        kacc = torch.full((P,), -1, dtype=torch.int32, device=theta.device)
+        failed = torch.zeros(P, dtype=torch.bool, device=theta.device)
+        arm = torch.zeros_like(failed)
+        act = torch.ones_like(failed)
+        al = alpha0.clone()
+        for k in range(K):
+            inval = act & ~(al > alpha_min)
+            failed = failed | inval
+            act = act & ~inval
+            ok, armk = self._accept(theta, phi, gphi_d, al, tht[k], pht[k], F, nf, theta_min=theta_min, pend=act,
+                                    frs=frs, theta_max=theta_max)
+            kacc = torch.where(ok, torch.full_like(kacc, k), kacc)
+            arm = torch.where(ok, armk, arm)
+            act = act & ~ok
+            al = al * 0.5
+        return kacc, failed, arm
+
+    LS_MULTI_K = int(os.environ.get('ATO_LS_MULTI_K', '8'))   # trials per batched backtracking round (0: off)
+
+    def _multi_round(self, idx, P, K, x, s, dx, ds, alpha, alpha_min, mu, theta, phi, gphi_d, F, nf, frs):
+        '''
+        The next K backtracking trials of the P searching columns idx evaluated in ONE batch of K P instances
+        (trial k of column p at alpha / 2^k, k-major: column k P + p) and tested in order (_filter_multi):
+        the same trial points, tests and filter-heuristic updates as K more rounds of the lockstep loop, with
+        one evaluation, one measure and one test launch instead of K of each over the whole batch. Returns
+        (kacc, failed, arm) of the P columns; nf and frs are updated in place.
+        '''
+        import copy
+        cols = idx.repeat(K)
+        pw = torch.pow(torch.full((K,), 0.5, dtype=torch.float64, device=alpha.device),
+                       torch.arange(K, device=alpha.device, dtype=torch.float64))
+        ak = alpha.index_select(0, idx)[None, :] * pw[:, None]               # [K, P]: exact halvings
+        akf = ak.reshape(-1)
+        Xm = x.index_select(1, cols) + akf * dx.index_select(1, cols)
+        Sm = s.index_select(1, cols) + akf * ds.index_select(1, cols)
+        view = copy.copy(self)
+        view._compact(cols, ())
+        view.B = K * P
+        view.ev = self.ev.subset(K * P, cols)
+        fm, gm = view._eval_fg(Xm)
+        tht, pht = view._measures(Xm, Sm, gm, fm, mu.index_select(0, cols))
+        sel = lambda t: t.index_select(0, idx)                              # noqa: E731
+        nf_p = sel(nf)
+        frs_p = tuple(sel(t) for t in frs)
+        kacc, failed, arm = self._filter_multi(sel(theta), sel(phi), sel(gphi_d), sel(alpha), sel(alpha_min),
+                                               tht.reshape(K, P).contiguous(), pht.reshape(K, P).contiguous(),
+                                               F.index_select(0, idx), nf_p, sel(self.theta_max), sel(self.theta_min),
+                                               frs_p)
+        nf.index_copy_(0, idx, nf_p)
+        for t, tp in zip(frs, frs_p):
+            t.index_copy_(0, idx, tp)
+        lss = self.stats.setdefault('ls_multi', [0, 0])      # rounds, trial points evaluated
+        lss[0] += 1
+        lss[1] += K * P
+        return kacc, failed, arm
 
     def _filter_test(self, theta, phi, gphi_d, alpha, tht, pht, F, nf, pend, first, frs, theta_min=None):
         ''' one trial's filter test for the pend columns (FilterLSAcceptor::CheckAcceptabilityOfTrialPoint with
@@ -1363,6 +1428,7 @@ class BatchedInteriorPoint:
                 # columns at their line search's first trial (IPOPT's n_steps == 0: tried even below alpha_min;
                 # a column accepted there restarts the watchdog's shortened-step counter)
                 fresh = pend.clone()
+                fresh_any = True                 # (host flag: any column at its first trial)
                 accf = torch.zeros(B, dtype=torch.bool, device=dev)
                 frs = (fr_n, fr_cnt, fr_last)
 
@@ -1383,12 +1449,33 @@ class BatchedInteriorPoint:
                     if o.ls_first_trial:
                         failed = failed & ~fresh
                     # one host synchronisation per trial for both tests
-                    any_failed, any_left = torch.stack([failed.any(), (pend & ~failed).any()]).tolist()
+                    any_failed, n_left = torch.stack([failed.any(), (pend & ~failed).sum()]).tolist()
                     if any_failed:
                         lsfail = lsfail | failed
                         pend = pend & ~failed
-                    if not any_left:
+                    if not n_left:
                         break
+                    lss = self.stats.setdefault('ls_trials', [0, 0, 0])   # trials, pending columns, lockstep searches
+                    lss[0] += 1
+                    lss[1] += int(n_left)
+                    lss[2] += int(_ls == 0)
+                    K = self.LS_MULTI_K
+                    if K > 0 and _ls >= 1 and not fresh_any and hasattr(self.ev, 'subset'):
+                        # batched backtracking: the next K trials of the searching columns in one evaluation
+                        pidx = torch.nonzero(pend).reshape(-1)
+                        kacc, mfail, marm = self._multi_round(pidx, int(n_left), K, x, s, dx, ds, alpha, alpha_min,
+                                                              mu, theta, phi, gphi_d, F, nf, frs)
+                        acc_p = kacc >= 0
+                        a_p = alpha.index_select(0, pidx) * torch.pow(torch.full_like(alpha.index_select(0, pidx), 0.5),
+                                                                      torch.where(acc_p, kacc, K).double())
+                        acc = torch.zeros_like(pend).index_copy(0, pidx, acc_p)
+                        mf = torch.zeros_like(pend).index_copy(0, pidx, mfail)
+                        alpha = alpha.index_copy(0, pidx, a_p)      # accepted: its step; searching on: / 2^K
+                        take(acc, alpha, x + alpha * dx, s + alpha * ds, torch.zeros_like(pend).index_copy(0, pidx, marm),
+                             dy)
+                        lsfail = lsfail | mf
+                        pend = pend & ~acc & ~mf
+                        continue
                     xt = x + alpha * dx
                     st = s + alpha * ds
                     laps.lap('ls_logic')
@@ -1420,7 +1507,8 @@ class BatchedInteriorPoint:
                             take(blind, alpha, xt, st, torch.ones_like(blind), dy)   # accepted untested
                             rev = failw & ~blind
                             pend = pend & ~wdm
-                            if bool(rev.any()):
+                            fresh_any = bool(rev.any())
+                            if fresh_any:
                                 revert(rev)
                                 dx, ds, dy, dzl, dzu, dvl, dvu = (dirs[k] for k in ('dx', 'ds', 'dy', 'dzl',
                                                                                     'dzu', 'dvl', 'dvu'))
@@ -1439,7 +1527,10 @@ class BatchedInteriorPoint:
                         laps.lap('soc')
                     first = first & False
                     # the next trial is a first one only for the columns whose watchdog was just reverted
-                    fresh = rev if (_ls == 0 and any_wd) else torch.zeros_like(fresh)
+                    if _ls == 0 and any_wd:
+                        fresh = rev
+                    else:
+                        fresh, fresh_any = torch.zeros_like(fresh), False
                     alpha = torch.where(pend, alpha * 0.5, alpha)
                 laps.lap('ls_logic')
                 # ---- soft restoration steps: the columns in the phase, and the columns whose line search

@@ -182,6 +182,35 @@ class DeviceIPMKernels:
                     'ato_ipm_filter_accept')
         return out[0], out[1], out[2]
 
+    def filter_multi(self, theta, phi, gphi_d, alpha0, alpha_min, tht, pht, F, nf, theta_max, theta_min, o, frs):
+        ''' K successive trials of P columns tested in order (ato_ipm_filter_multi; batched_ipm.py
+        _filter_multi): (kacc int32 [P] (-1: none), failed bool [P], arm bool [P]); nf and the heuristic's
+        state frs = (fr_n, fr_cnt, fr_last) updated in place '''
+        P = theta.shape[0]
+        K = tht.shape[0]
+        cols = [self._c(t, P) for t in (theta, phi, gphi_d, alpha0, alpha_min, theta_max, theta_min)]
+        for t in (tht, pht):
+            if t.dtype != torch.float64 or t.shape != (K, P) or not t.is_contiguous():
+                raise ValueError('filter_multi: trial measures must be contiguous fp64 [K, P]')
+        if F.dtype != torch.float64 or F.shape[0] != P or F.dim() != 3 or F.shape[2] != 2:
+            raise ValueError('filter: expected fp64 [P, fmax, 2]')
+        F = F.contiguous()
+        self._own(nf, torch.int64, P, 'filter length')
+        self._own(frs[0], torch.int64, P, 'filter reset count')
+        self._own(frs[1], torch.int64, P, 'filter reset trigger count')
+        self._own(frs[2], torch.bool, P, 'filter rejection flag')
+        key = ('filter', o.s_phi, o.s_theta, o.delta, o.eta_phi, o.gamma_theta, o.gamma_phi, o.obj_max_inc,
+               o.compare_tol, o.max_filter_resets, o.filter_reset_trigger)
+        prm = self._host_prm(key)
+        kacc = torch.empty(P, dtype=torch.int32, device=self.device)
+        out = torch.empty((2, P), dtype=torch.bool, device=self.device)
+        th, ph, gd, a0, amin, tmax, tmin = cols
+        self._check(self.lib.ato_ipm_filter_multi(P, K, F.shape[1], _p(th), _p(ph), _p(gd), _p(a0), _p(amin), _p(tht),
+                                                  _p(pht), _p(F), _p(nf), _p(tmax), _p(tmin), prm.ctypes.data,
+                                                  _p(frs[0]), _p(frs[1]), _p(frs[2]), _p(kacc), _p(out[0]),
+                                                  _p(out[1]), self._stream()), 'ato_ipm_filter_multi')
+        return kacc, out[0], out[1]
+
     def perturb(self, op, pert, mu, pend, inertia=None, dw_out=None, dc_out=None, tosolve=None, fin=None, m=0):
         ''' one step of the per-column PDPerturbationHandler (ato_ipm_perturb, op 0 / 1 / 2 as in
         include/ato_ipm.h) on the handler state `pert` (batched_ipm.py BatchedPerturbation, updated in

@@ -110,6 +110,19 @@ int ato_ipm_filter_accept(int32_t W, int32_t fmax, const double* theta, const do
                           const uint8_t* pend, const uint8_t* first, const double* prm, int64_t* fr_n,
                           int64_t* fr_cnt, uint8_t* fr_last, uint8_t* ok, uint8_t* arm, uint8_t* soc, void* stream);
 
+/* K successive backtracking trials of P columns tested in order (the lockstep line search's next K rounds at
+ * once): trial k of column p has step alpha0[p] / 2^k and measures tht, pht [K][P]; theta, phi, gphi_d,
+ * alpha_min, theta_max, theta_min [P]; F [P][fmax][2], nf [P] (in/out), the filter reset heuristic's state
+ * fr_n, fr_cnt (int64), fr_last (bytes) [P] in/out, prm as ato_ipm_filter_accept's. A column stops at its first
+ * trial with alpha <= alpha_min (failed = 1) or at its first accepted trial (kacc = k, arm = its Armijo case);
+ * kacc = -1, failed = 0: none of the K trials decided. The heuristic runs on every tested trial, as K calls of
+ * ato_ipm_filter_accept would. */
+int ato_ipm_filter_multi(int32_t P, int32_t K, int32_t fmax, const double* theta, const double* phi,
+                         const double* gphi_d, const double* alpha0, const double* alpha_min, const double* tht,
+                         const double* pht, const double* F, int64_t* nf, const double* theta_max,
+                         const double* theta_min, const double* prm, int64_t* fr_n, int64_t* fr_cnt, uint8_t* fr_last,
+                         int32_t* kacc, uint8_t* failed, uint8_t* arm, void* stream);
+
 /* IPOPT's PDPerturbationHandler per column (IpPDPerturbationHandler: ConsiderNewSystem,
  * PerturbForSingularity, PerturbForWrongInertia with the structural-degeneracy test; batched_ipm.py
  * BatchedPerturbation) and the bookkeeping of an inertia-correction pass (batched_ipm.py _kkt_step),

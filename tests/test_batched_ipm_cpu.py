@@ -136,3 +136,28 @@ def test_kkt_failure_falls_back_to_restoration():
     assert res.iters[1] == ref.iters
     x = res.x.numpy()
     assert np.abs(x[:, 1] - ref.x).max() <= 1e-6 * max(1.0, np.abs(ref.x).max())
+
+
+def test_batched_backtracking_rounds_match_trial_by_trial():
+    ''' the line search's batched backtracking rounds (_multi_round: the next K trials of the searching
+    columns evaluated together and tested in order, filter reset heuristic included) against the
+    trial-by-trial lockstep loop (LS_MULTI_K = 0): identical statuses, iteration counts, solutions and
+    per-iteration histories on drone cold starts that backtrack (K = 8 and K = 2: rounds that leave columns
+    searching) '''
+    spec = product_spec(track='race', N=4, K=2)
+    B = 2
+    W = _instances(spec, B, seed=5)
+    runs = []
+    for k in (0, 8, 2):
+        ev = HostBatchEvaluator(spec, B)
+        solver = BatchedInteriorPoint(ev, HostBlockKKT(ev), spec.lbw, spec.ubw, IPMOptions(max_iter=25))
+        solver.LS_MULTI_K = k
+        runs.append((solver.solve(W), solver.history))
+    (r0, h0) = runs[0]
+    assert r0.stats.get('ls_multi') is None
+    for r, h in runs[1:]:
+        assert r.stats['ls_multi'][0] > 0
+        assert r.status == r0.status
+        assert [int(i) for i in r.iters] == [int(i) for i in r0.iters]
+        assert torch.equal(r.x, r0.x)
+        assert h.shape == h0.shape and np.array_equal(h, h0)
