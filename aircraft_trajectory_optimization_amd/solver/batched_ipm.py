@@ -206,7 +206,10 @@ def _hess_into(problem, binder, B, X, lam, sigma, nnz_h):
 
 class _SubsetDeviceEvaluator:
     def __init__(self, base, count: int, cols=None):
-        if not 0 < count <= base.batch:
+        # (with explicit columns a column may repeat: the line search's batched backtracking evaluates
+        # K trials of each searching column, so count may exceed the base's width; ato_eval grows its
+        # scratch to the batch it is given)
+        if not 0 < count or (cols is None and count > base.batch):
             raise ValueError('subset size out of range')
         if isinstance(base, _SubsetDeviceEvaluator):       # a subset of a subset: columns of the root
             if cols is not None:
@@ -716,6 +719,11 @@ class BatchedInteriorPoint:
 
     LS_MULTI_K = int(os.environ.get('ATO_LS_MULTI_K', '8'))   # trials per batched backtracking round (0: off)
 
+    @staticmethod
+    def _halvings(K, device):
+        ''' [2^0, 2^-1, ..., 2^-(K-1)] (fp64, exact) '''
+        return torch.tensor([0.5 ** k for k in range(K)], dtype=torch.float64, device=device)
+
     def _multi_round(self, idx, P, K, x, s, dx, ds, alpha, alpha_min, mu, theta, phi, gphi_d, F, nf, frs):
         '''
         The next K backtracking trials of the P searching columns idx evaluated in ONE batch of K P instances
@@ -726,9 +734,10 @@ class BatchedInteriorPoint:
         '''
         import copy
         cols = idx.repeat(K)
-        pw = torch.pow(torch.full((K,), 0.5, dtype=torch.float64, device=alpha.device),
-                       torch.arange(K, device=alpha.device, dtype=torch.float64))
-        ak = alpha.index_select(0, idx)[None, :] * pw[:, None]               # [K, P]: exact halvings
+        # 2^-k as exact host constants (a device pow need not be exact): alpha 2^-k is then bitwise the
+        # k-times-halved alpha of the trial-by-trial loop
+        pw = self._halvings(K + 1, alpha.device)[:K]
+        ak = alpha.index_select(0, idx)[None, :] * pw[:, None]               # [K, P]
         akf = ak.reshape(-1)
         Xm = x.index_select(1, cols) + akf * dx.index_select(1, cols)
         Sm = s.index_select(1, cols) + akf * ds.index_select(1, cols)
@@ -1466,8 +1475,8 @@ class BatchedInteriorPoint:
                         kacc, mfail, marm = self._multi_round(pidx, int(n_left), K, x, s, dx, ds, alpha, alpha_min,
                                                               mu, theta, phi, gphi_d, F, nf, frs)
                         acc_p = kacc >= 0
-                        a_p = alpha.index_select(0, pidx) * torch.pow(torch.full_like(alpha.index_select(0, pidx), 0.5),
-                                                                      torch.where(acc_p, kacc, K).double())
+                        a_p = alpha.index_select(0, pidx) * self._halvings(K + 1, dev).index_select(
+                            0, torch.where(acc_p, kacc, K).long())
                         acc = torch.zeros_like(pend).index_copy(0, pidx, acc_p)
                         mf = torch.zeros_like(pend).index_copy(0, pidx, mfail)
                         alpha = alpha.index_copy(0, pidx, a_p)      # accepted: its step; searching on: / 2^K
