@@ -742,9 +742,17 @@ class BatchedInteriorPoint:
         Xm = x.index_select(1, cols) + akf * dx.index_select(1, cols)
         Sm = s.index_select(1, cols) + akf * ds.index_select(1, cols)
         view = copy.copy(self)
-        view._compact(cols, ())
+        if self.vk is not None:
+            # the fused measures kernel reads only the bounds, the constraint constants and the scalings
+            # of the trial columns: gather those (7 of the 25 per-instance attributes)
+            for k in ('sf', 'sg', 'c_rhs', 'xL', 'xU', 'dL', 'dU'):
+                t = getattr(self, k)
+                if torch.is_tensor(t) and t.dim() >= 1 and t.shape[-1] == self.B:
+                    setattr(view, k, t.index_select(t.dim() - 1, cols).contiguous())
+        else:
+            view._compact(cols, ())
         view.B = K * P
-        view.ev = self.ev.subset(K * P, cols)
+        view.ev = getattr(self.ev, 'trial_subset', getattr(self.ev, 'subset', None))(K * P, cols)
         fm, gm = view._eval_fg(Xm)
         tht, pht = view._measures(Xm, Sm, gm, fm, mu.index_select(0, cols))
         sel = lambda t: t.index_select(0, idx)                              # noqa: E731
@@ -1469,7 +1477,8 @@ class BatchedInteriorPoint:
                     lss[1] += int(n_left)
                     lss[2] += int(_ls == 0)
                     K = self.LS_MULTI_K
-                    if K > 0 and _ls >= 1 and not fresh_any and hasattr(self.ev, 'subset'):
+                    if K > 0 and _ls >= 1 and not fresh_any and getattr(self.ev, 'trial_subset_ok',
+                                                                          hasattr(self.ev, 'subset')):
                         # batched backtracking: the next K trials of the searching columns in one evaluation
                         pidx = torch.nonzero(pend).reshape(-1)
                         kacc, mfail, marm = self._multi_round(pidx, int(n_left), K, x, s, dx, ds, alpha, alpha_min,
@@ -2148,6 +2157,22 @@ class _RestorationEvaluator:
         self.h_row_ptr, self.h_col, self.nnz_h = st.h_row_ptr, st.h_col, st.nnz_h
         self.h_map, self.h_diag, self.diag_new = st.h_map, st.h_diag, st.diag_new
         self.lbg, self.ubg = lbg_s, ubg_s
+        self.trial_subset_ok = hasattr(base, 'subset')
+
+    def trial_subset(self, count: int, cols) -> '_RestorationEvaluator':
+        ''' the restoration NLP of the columns cols, for eval_fg: the line search's batched backtracking
+        (a column may repeat; BatchedInteriorPoint._multi_round). Not `subset`: the restoration phase does
+        not compact its batch or nest another restoration. '''
+        import copy
+        cols = torch.as_tensor(cols, device=self.device).reshape(-1).long()
+        v = copy.copy(self)
+        v.base = self.base.subset(count, cols)
+        v.batch = int(count)
+        for k in ('sg', 'x_ref', 'dr2', 'zeta', 'rho', 'lbg', 'ubg'):
+            t = getattr(self, k)
+            if torch.is_tensor(t) and t.dim() >= 1 and t.shape[-1] == self.batch:
+                setattr(v, k, t.index_select(t.dim() - 1, cols).contiguous())
+        return v
 
     def eval(self, X):
         n, m, B = self.n0, self.m, self.batch

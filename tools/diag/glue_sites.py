@@ -1,0 +1,75 @@
+'''
+DIAGNOSTIC (GPU): torch operators (= device launches, copies included) of the batched interior-point solver
+per source line, on the real config-3 workload (B cold starts, max_iter iterations), counted by a torch
+dispatch mode on the main thread (the restoration phases' worker threads run the same code and are not
+counted). Prints the top lines and the total per lockstep iteration.
+    python tools/diag/glue_sites.py --batch 512 --max-iter 60 --out gpurun_out/glue.json
+'''
+import argparse
+import collections
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--batch', type=int, default=512)
+    ap.add_argument('--max-iter', type=int, default=60)
+    ap.add_argument('--top', type=int, default=60)
+    ap.add_argument('--out', default=None)
+    a = ap.parse_args()
+    import torch
+    from torch.utils._python_dispatch import TorchDispatchMode
+    from aircraft_trajectory_optimization_amd.raceline.batched_solve import solve_shard
+    from aircraft_trajectory_optimization_amd.solver.ipm import IPMOptions
+    from aircraft_trajectory_optimization_amd.tracks import make_spec
+    pkg = os.path.join(ROOT, 'aircraft_trajectory_optimization_amd')
+    sites = collections.Counter()
+    ops = collections.defaultdict(collections.Counter)
+    # operators that launch nothing on the device (views, metadata, host scalars)
+    free = ('aten.view', 'aten._unsafe_view', 'aten.t.', 'aten.alias', 'aten.detach', 'aten.unsqueeze', 'aten.squeeze',
+            'aten.expand', 'aten.reshape', 'aten.select.', 'aten.slice.', 'aten.as_strided.', 'aten.permute',
+            'aten.transpose', 'aten.empty', 'aten._local_scalar_dense', 'aten.size', 'aten.stride', 'aten.is_nonzero',
+            'aten.lift_fresh', 'aten.unbind', 'aten.split.', 'aten.chunk', 'aten.sym_')
+
+    class Count(TorchDispatchMode):
+        def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+            out = func(*args, **(kwargs or {}))
+            name = str(func)
+            dev = any(torch.is_tensor(t) and t.is_cuda for t in list(args) + list((kwargs or {}).values()))
+            if dev and not name.startswith(free):
+                f = sys._getframe(1)
+                site = None
+                while f is not None:
+                    fn = f.f_code.co_filename
+                    if fn.startswith(pkg) and 'python_dispatch' not in fn:
+                        site = f'{os.path.relpath(fn, ROOT)}:{f.f_lineno} {f.f_code.co_name}'
+                        break
+                    f = f.f_back
+                site = site or 'other'
+                sites[site] += 1
+                ops[site][name] += 1
+            return out
+
+    spec = make_spec(track='race', model='drone', frame='parametric', N=50, K=4, use_quat=True, global_r=True)
+    lock = {'n': 0}
+    with Count():
+        res, solver, _ = solve_shard(spec, list(range(a.batch)), IPMOptions(max_iter=a.max_iter),
+                                     on_iteration=lambda *x: lock.__setitem__('n', lock['n'] + 1))
+    torch.cuda.synchronize()
+    n = max(lock['n'], 1)
+    tot = sum(sites.values())
+    print(f'lockstep iterations {n}, device operators on the main thread {tot} ({tot / n:.0f} per iteration)')
+    for s, c in sites.most_common(a.top):
+        print(f'{c / n:8.1f}  {s}   {dict(ops[s].most_common(3))}')
+    if a.out:
+        json.dump({'lockstep': n, 'total': tot, 'sites': sites.most_common(),
+                   'ops': {k: dict(v) for k, v in ops.items()}}, open(a.out, 'w'), indent=1)
+
+
+if __name__ == '__main__':
+    main()
