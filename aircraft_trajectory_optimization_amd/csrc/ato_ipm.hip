@@ -913,6 +913,136 @@ __global__ __launch_bounds__(CB) void k_barrier(int W, BarrierPrm o, const doubl
     upd[b] = u ? 1 : 0;
 }
 
+
+// ------------------------------------------------------------------------------------------
+// Iterative refinement of the KKT solves (batched_ipm.py _refine, IPOPT's PDFullSpaceSolver):
+// k_refine_pass = one pass over the [N][W] vectors of a step (the update a += b of the refining
+// columns, column maxima of |a| and |c|: partials per row chunk), k_refine_decide = one workgroup
+// folding the partials into IPOPT's residual ratio and the per-column decisions, with the ordered
+// list of the columns that refine next (what torch.nonzero gave the host). Maxima are exact and
+// propagate NaN as torch.amax does, so the fold order does not matter.
+// ------------------------------------------------------------------------------------------
+constexpr int RF_THREADS = 256;                  // 4 waves: 64 columns x 4 row strides
+constexpr int RD_THREADS = 1024;                 // the decision workgroup
+
+__global__ __launch_bounds__(RF_THREADS) void k_refine_pass(int N, int W, int rows, double* __restrict__ a,
+                                                           const double* __restrict__ b,
+                                                           const uint8_t* __restrict__ upd,
+                                                           const double* __restrict__ c,
+                                                           const uint8_t* __restrict__ sel,
+                                                           double* __restrict__ pa, double* __restrict__ pc) {
+    __shared__ double sa[4][64], sc[4][64];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int col = blockIdx.x * 64 + lane;
+    const int r0 = blockIdx.y * rows, r1 = min(N, r0 + rows);
+    const bool on = col < W && (!sel || sel[col] != 0);
+    const bool up = on && b && upd && upd[col] != 0;
+    double ma = 0.0, mc = 0.0;
+    if (on) {
+        for (int r = r0 + wv; r < r1; r += 4) {
+            const long long i = (long long)r * W + col;
+            double v = a[i];
+            if (up) {
+                v = v + b[i];
+                a[i] = v;
+            }
+            ma = nmax(ma, fabs(v));
+            if (c) mc = nmax(mc, fabs(c[i]));
+        }
+    }
+    sa[wv][lane] = ma;
+    sc[wv][lane] = mc;
+    __syncthreads();
+    if (wv == 0 && col < W) {
+        const long long o = (long long)blockIdx.y * W + col;
+        pa[o] = nmax(nmax(sa[0][lane], sa[1][lane]), nmax(sa[2][lane], sa[3][lane]));
+        if (pc) pc[o] = nmax(nmax(sc[0][lane], sc[1][lane]), nmax(sc[2][lane], sc[3][lane]));
+    }
+}
+
+struct RefinePrm {
+    double ratio_max, ratio_singular;
+    int min_steps, max_steps;
+};
+
+// IPOPT's residual ratio |r| / (min(|x|, 1e6 |rhs|) + |rhs|) (|r| where |x| + |rhs| = 0)
+__device__ __forceinline__ double refine_ratio(double nres, double nx, double nr) {
+    return nr + nx == 0.0 ? nres : nres / (nmin(nx, 1e6 * nr) + nr);
+}
+
+// mode 0: out0 = column maxima of the partials pa; mode 1: the first residual of the solve (sel = the
+// solved columns); mode 2: after refinement step k (k counted from 1; sel = the columns that refined)
+__global__ __launch_bounds__(RD_THREADS) void k_refine_decide(int W, int nch, int mode, int k, RefinePrm o,
+                                                              const double* __restrict__ pa,
+                                                              const double* __restrict__ pc,
+                                                              const uint8_t* __restrict__ sel,
+                                                              const double* __restrict__ nr, double* __restrict__ rr,
+                                                              double* __restrict__ old, uint8_t* __restrict__ bad,
+                                                              uint8_t* __restrict__ refine, uint8_t* __restrict__ need,
+                                                              int32_t* __restrict__ list, uint8_t* __restrict__ ok) {
+    __shared__ int wcount[RD_THREADS / 64];
+    __shared__ int total;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    if (tid == 0) total = 0;
+    __syncthreads();
+    for (int base = 0; base < W; base += RD_THREADS) {
+        const int col = base + tid;
+        bool flag = false;
+        if (col < W) {
+            double nx = 0.0, nres = 0.0;
+            for (int q = 0; q < nch; ++q) {
+                nx = nmax(nx, pa[(long long)q * W + col]);
+                if (pc) nres = nmax(nres, pc[(long long)q * W + col]);
+            }
+            if (mode == 0) {
+                rr[col] = nx;
+            } else {
+                const bool s = sel[col] != 0;
+                double r = rr[col];
+                bool rf, bd;
+                if (mode == 1) {
+                    r = s ? refine_ratio(nres, nx, nr[col]) : 0.0;
+                    old[col] = r;
+                    bd = false;
+                    rf = s;
+                } else {
+                    bd = bad[col] != 0;
+                    rf = false;
+                    if (s) {
+                        r = refine_ratio(nres, nx, nr[col]);
+                        const bool quit = (r > o.ratio_max && k > o.max_steps) || (r > old[col] && k > o.min_steps);
+                        bd = bd || (quit && r > o.ratio_singular);
+                        rf = !quit;
+                        old[col] = r;
+                    }
+                }
+                rr[col] = r;
+                bad[col] = bd ? 1 : 0;
+                refine[col] = rf ? 1 : 0;
+                flag = rf && fin(r) && (k >= o.min_steps ? r > o.ratio_max : true);
+                need[col] = flag ? 1 : 0;
+                ok[col] = (fin(r) && !bd) ? 1 : 0;
+            }
+        }
+        if (mode != 0) {   // ordered compaction of the flags: wave ballots, then the waves in order
+            const unsigned long long bal = __ballot(flag);
+            if (lane == 0) wcount[wv] = __popcll(bal);
+            __syncthreads();
+            int off = total;
+            for (int w = 0; w < wv; ++w) off += wcount[w];
+            if (flag) list[1 + off + __popcll(bal & ((1ull << lane) - 1ull))] = col;
+            __syncthreads();
+            if (tid == 0) {
+                int t = total;
+                for (int w = 0; w < RD_THREADS / 64; ++w) t += wcount[w];
+                total = t;
+            }
+            __syncthreads();
+        }
+    }
+    if (mode != 0 && tid == 0) list[0] = total;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1091,6 +1221,39 @@ int ato_ipm_barrier(int32_t W, const double* prm, const double* Emu, uint8_t* mu
                        mu_act, force, act, reinterpret_cast<long long*>(status), mu, tau,
                        reinterpret_cast<long long*>(nf), upd);
     return check_launch("ato_ipm_barrier");
+}
+
+
+int ato_ipm_refine_work(int32_t N, int32_t W) {
+    if (N < 0 || W < 1) return 0;
+    const int nch = N ? (N + 63) / 64 : 1;       // row chunks of 64 (16 rows per wave)
+    return nch < 64 ? nch : 64;
+}
+
+int ato_ipm_refine_pass(int32_t N, int32_t W, double* a, const double* b, const uint8_t* upd, const double* c,
+                        const uint8_t* sel, double* part_a, double* part_c, void* stream) {
+    if (N < 0 || W < 0 || (W && (!a || !part_a || (c && !part_c) || (b && !upd))))
+        return fail(ATO_ERR_ARG, "ato_ipm_refine_pass: arguments");
+    if (W == 0) return 0;
+    const int nch = ato_ipm_refine_work(N, W);
+    const int rows = N ? (N + nch - 1) / nch : 0;
+    hipLaunchKernelGGL(k_refine_pass, dim3((W + 63) / 64, nch), dim3(RF_THREADS), 0, static_cast<hipStream_t>(stream),
+                       N, W, rows, a, b, upd, c, sel, part_a, c ? part_c : nullptr);
+    return check_launch("ato_ipm_refine_pass");
+}
+
+int ato_ipm_refine_decide(int32_t N, int32_t W, int32_t mode, int32_t k, const double* prm, const double* part_a,
+                          const double* part_c, const uint8_t* sel, const double* nr, double* rr, double* old,
+                          uint8_t* bad, uint8_t* refine, uint8_t* need, int32_t* list, uint8_t* ok, void* stream) {
+    if (N < 0 || W < 0 || mode < 0 || mode > 2 || !prm) return fail(ATO_ERR_ARG, "ato_ipm_refine_decide: arguments");
+    if (W == 0) return 0;
+    if (!part_a || !rr || (mode && (!part_c || !sel || !nr || !old || !bad || !refine || !need || !list || !ok)))
+        return fail(ATO_ERR_ARG, "ato_ipm_refine_decide: arguments");
+    const RefinePrm o{prm[0], prm[1], (int)prm[2], (int)prm[3]};
+    hipLaunchKernelGGL(k_refine_decide, dim3(1), dim3(RD_THREADS), 0, static_cast<hipStream_t>(stream), W,
+                       ato_ipm_refine_work(N, W), mode, k, o, part_a, mode ? part_c : nullptr, sel, nr, rr, old, bad,
+                       refine, need, list, ok);
+    return check_launch("ato_ipm_refine_decide");
 }
 
 }  // extern "C"

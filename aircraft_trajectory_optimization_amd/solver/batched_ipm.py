@@ -827,6 +827,8 @@ class BatchedInteriorPoint:
         max_refinement_steps, or until the ratio stops improving; last_solve_ok is False where the
         refinement stopped above residual_ratio_singular (or the ratio is not finite) '''
         o = self.o
+        if self.vk is not None:
+            return self._refine_device(rhs, x, mask, idx, H, Js, dx, dr)
         nr = rhs.abs().amax(0)
 
         def ratio(res, x_):
@@ -858,6 +860,32 @@ class BatchedInteriorPoint:
             refine = need & ~quit_
             old = torch.where(need, rr, old)
         self.last_solve_ok = torch.isfinite(rr) & ~bad
+        self.laps.lap('kkt_refine')
+        return x
+
+    def _refine_device(self, rhs, x, mask, idx, H, Js, dx, dr):
+        ''' _refine with the ratio, the decisions and the list of the refining columns in two fused kernels
+        per step (ato_ipm_refine_pass / _decide): the same tests on the same values, one host
+        synchronisation per step (the list) '''
+        vk = self.vk
+        res = self._residual(H, Js, dx, dr, x, rhs, idx).contiguous()
+        st = vk.refine_begin(rhs.contiguous(), x, res, mask.contiguous(), self.o)
+        k = 0
+        while True:
+            lst = st['list'].cpu().numpy()
+            cnt = int(lst[0])
+            if cnt == 0:
+                break
+            nidx = np.ascontiguousarray(lst[1:1 + cnt], dtype=np.int32)
+            self.laps.lap('kkt_refine')
+            self.kkt.solve(res, nidx)
+            self.laps.lap('kkt_solve')
+            self.stats['solves'] += 1
+            vk.refine_update(st, x, res)
+            res = self._residual(H, Js, dx, dr, x, rhs, nidx).contiguous()
+            k += 1
+            vk.refine_ratio(st, res, k)
+        self.last_solve_ok = st['ok']
         self.laps.lap('kkt_refine')
         return x
 

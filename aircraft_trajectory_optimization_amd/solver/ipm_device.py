@@ -211,6 +211,63 @@ class DeviceIPMKernels:
                                                   _p(out[1]), self._stream()), 'ato_ipm_filter_multi')
         return kacc, out[0], out[1]
 
+    # ------------------------------------------------------------------ iterative refinement
+    def _refine_vec(self, t, N, W, what):
+        if t.dtype != torch.float64 or t.device != self.device or t.shape != (N, W) or not t.is_contiguous():
+            raise ValueError(f'refinement {what}: expected contiguous fp64 [{N}, {W}] on {self.device}')
+        return t
+
+    def refine_begin(self, rhs, x, res, mask, o):
+        ''' the refinement state of a batch of solves after their first residual (ato_ipm_refine_pass /
+        _decide modes 0 and 1; batched_ipm.py _refine): nr = max |rhs|, rr = old = the residual ratio on
+        the solved columns mask, and the list of the columns that refine first '''
+        N, W = rhs.shape
+        for t, w in ((rhs, 'rhs'), (x, 'x'), (res, 'residual')):
+            self._refine_vec(t, N, W, w)
+        self._own(mask, torch.bool, W, 'solved-column mask')
+        nch = int(self.lib.ato_ipm_refine_work(N, W))
+        f64 = dict(dtype=torch.float64, device=self.device)
+        u8 = dict(dtype=torch.bool, device=self.device)
+        key = ('refine', o.residual_ratio_max, o.residual_ratio_singular, o.min_refinement_steps,
+               o.max_refinement_steps)
+        st = {'N': N, 'W': W, 'pa': torch.empty((nch, W), **f64), 'pc': torch.empty((nch, W), **f64),
+              'nr': torch.empty(W, **f64), 'rr': torch.empty(W, **f64), 'old': torch.empty(W, **f64),
+              'bad': torch.empty(W, **u8), 'refine': torch.empty(W, **u8), 'need': torch.empty(W, **u8),
+              'ok': torch.empty(W, **u8), 'list': torch.empty(W + 1, dtype=torch.int32, device=self.device),
+              'prm': self._host_prm(key)}
+        self._check(self.lib.ato_ipm_refine_pass(N, W, _p(rhs), None, None, None, None, _p(st['pa']), None,
+                                                 self._stream()), 'ato_ipm_refine_pass')
+        self._decide(st, 0, 0, None, st['nr'])
+        self._check(self.lib.ato_ipm_refine_pass(N, W, _p(x), None, None, _p(res), _p(mask), _p(st['pa']),
+                                                 _p(st['pc']), self._stream()), 'ato_ipm_refine_pass')
+        self._decide(st, 1, 0, mask, st['rr'])
+        return st
+
+    def _decide(self, st, mode, k, sel, rr):
+        self._check(self.lib.ato_ipm_refine_decide(st['N'], st['W'], mode, k, st['prm'].ctypes.data, _p(st['pa']),
+                                                   _p(st['pc']), _p(sel), _p(st['nr']), _p(rr), _p(st['old']),
+                                                   _p(st['bad']), _p(st['refine']), _p(st['need']), _p(st['list']),
+                                                   _p(st['ok']), self._stream()), 'ato_ipm_refine_decide')
+
+    def refine_update(self, st, x, corr):
+        ''' x += corr on the refining columns, and their max |x| '''
+        N, W = st['N'], st['W']
+        self._refine_vec(x, N, W, 'x')
+        self._refine_vec(corr, N, W, 'correction')
+        need = st['need']
+        self._check(self.lib.ato_ipm_refine_pass(N, W, _p(x), _p(corr), _p(need), None, _p(need), _p(st['pa']), None,
+                                                 self._stream()), 'ato_ipm_refine_pass')
+
+    def refine_ratio(self, st, res, k):
+        ''' after refinement step k (>= 1): the new residual ratios of the refining columns, the decisions
+        and the list of the columns that refine next '''
+        N, W = st['N'], st['W']
+        self._refine_vec(res, N, W, 'residual')
+        need = st['need']
+        self._check(self.lib.ato_ipm_refine_pass(N, W, _p(res), None, None, None, _p(need), _p(st['pc']), None,
+                                                 self._stream()), 'ato_ipm_refine_pass')
+        self._decide(st, 2, k, need, st['rr'])
+
     def perturb(self, op, pert, mu, pend, inertia=None, dw_out=None, dc_out=None, tosolve=None, fin=None, m=0):
         ''' one step of the per-column PDPerturbationHandler (ato_ipm_perturb, op 0 / 1 / 2 as in
         include/ato_ipm.h) on the handler state `pert` (batched_ipm.py BatchedPerturbation, updated in

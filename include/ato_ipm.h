@@ -161,6 +161,29 @@ int ato_ipm_status(int32_t W, const double* prm, const double* E0, const double*
  * force is cleared. prm = HOST {kappa_eps, kappa_mu, theta_mu, mu_min, tau_min}. */
 int ato_ipm_barrier(int32_t W, const double* prm, const double* Emu, uint8_t* mu_act, uint8_t* force, uint8_t* act,
                     int64_t* status, double* mu, double* tau, int64_t* nf, uint8_t* upd, void* stream);
+
+/* Iterative refinement of a batch of KKT solves (IPOPT's PDFullSpaceSolver; solver/batched_ipm.py
+ * _refine): [N][W] vectors, per-column state [W].
+ * ato_ipm_refine_work: the number of row chunks nch of the partial buffers ([nch][W] doubles each).
+ * ato_ipm_refine_pass: where sel (NULL: every column) -- a += b on the columns with upd (b NULL: no
+ *   update), then per row chunk the column maxima of |a| into part_a and of |c| into part_c (c NULL:
+ *   none). NaN propagates.
+ * ato_ipm_refine_decide (one workgroup): mode 0 -- rr = the column maxima of part_a (e.g. |rhs|);
+ *   mode 1 -- the first residual of the solve (sel = the solved columns; part_a = |x|, part_c = |r|):
+ *   rr = old = ratio |r| / (min(|x|, 1e6 nr) + nr) on sel (0 elsewhere), bad = 0, refine = sel;
+ *   mode 2 -- after refinement step k >= 1 of the columns sel: rr = old = the new ratio, a column
+ *   quits when (rr > ratio_max and k > max_steps) or (rr > old and k > min_steps), bad |= quit and
+ *   rr > ratio_singular, refine = sel and not quit. Modes 1 and 2 then set need = refine, rr finite
+ *   and (k >= min_steps ? rr > ratio_max : true), ok = rr finite and not bad, and write the columns
+ *   with need in ascending order to list[1..], their count to list[0] (list: W + 1 int32).
+ *   prm (host): ratio_max, ratio_singular, min_steps, max_steps. */
+int ato_ipm_refine_work(int32_t N, int32_t W);
+int ato_ipm_refine_pass(int32_t N, int32_t W, double* a, const double* b, const uint8_t* upd, const double* c,
+                        const uint8_t* sel, double* part_a, double* part_c, void* stream);
+int ato_ipm_refine_decide(int32_t N, int32_t W, int32_t mode, int32_t k, const double* prm, const double* part_a,
+                          const double* part_c, const uint8_t* sel, const double* nr, double* rr, double* old,
+                          uint8_t* bad, uint8_t* refine, uint8_t* need, int32_t* list, uint8_t* ok, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
