@@ -27,31 +27,58 @@ B = 1024
 CFG = dict(track='fig8', model='drone', frame='parametric', N=50, K=4, use_quat=True, global_r=True)
 
 
+class _Heartbeat:
+    ''' a line every 30 s on file descriptor 2 (seen under --capture=sys) and appended to
+    gpurun_out/heartbeat.log (seen whatever the capture mode): a runner that takes minutes of silence for
+    a hang sees the solve alive '''
+
+    def __init__(self, label):
+        self.label = label
+
+    def _beat(self):
+        import os
+        import time
+        line = f'[{self.label}] solving {time.strftime("%H:%M:%S")}\n'
+        os.write(2, line.encode())
+        try:
+            root = os.environ.get('GRAFT_REPO_ROOT', os.getcwd())
+            os.makedirs(os.path.join(root, 'gpurun_out'), exist_ok=True)
+            with open(os.path.join(root, 'gpurun_out', 'heartbeat.log'), 'a') as f:
+                f.write(line)
+        except OSError:
+            pass
+
+    def __enter__(self):
+        import threading
+        self.stop = threading.Event()
+        self.t = threading.Thread(target=lambda: [self._beat() for _ in iter(lambda: self.stop.wait(30), True)],
+                                  daemon=True)
+        self.t.start()
+        return self
+
+    def __exit__(self, *exc):
+        self.stop.set()
+        return False
+
+
 def _corridor_solve(use_dcm, progress):
-    import os
-    import threading
     import time
     from aircraft_trajectory_optimization_amd.raceline.batch_instances import corridor_batch
     from aircraft_trajectory_optimization_amd.solver.batched_ipm import device_solver
     from aircraft_trajectory_optimization_amd.solver.ipm import IPMOptions
     kw = dict(CFG, use_dcm=use_dcm)
     t0 = time.time()
-    spec, W, LBW, UBW, pst, plap = corridor_batch(B, **{k: v for k, v in kw.items() if k != 'model'})
+    with _Heartbeat('config 5 test: point-mass corridors'):
+        spec, W, LBW, UBW, pst, plap = corridor_batch(B, **{k: v for k, v in kw.items() if k != 'model'})
     print(f'point-mass corridor solves: {time.time() - t0:.1f} s', {s: pst.count(s) for s in set(pst)}, flush=True)
     assert pst.count('optimal') == B
     t0 = time.time()
     solver = device_solver(spec, B, LBW, UBW, IPMOptions(max_iter=1000))
-    # a heartbeat on file descriptor 2 (not captured by pytest's sys capture): a runner that takes
-    # minutes of silence for a hang sees the solve alive
-    stop = threading.Event()
-    beat = threading.Thread(target=lambda: [os.write(2, b'[config 5 test] solving\n') for _ in iter(
-        lambda: stop.wait(30), True)], daemon=True)
-    beat.start()
     try:
-        res = solver.solve(W, progress=progress)
-        torch.cuda.synchronize()
+        with _Heartbeat('config 5 test'):
+            res = solver.solve(W, progress=progress)
+            torch.cuda.synchronize()
     finally:
-        stop.set()
         solver.kkt.close()
         del solver
         torch.cuda.empty_cache()
@@ -121,9 +148,10 @@ def test_config5_fp32_jacobian_leg():
     from tests.helpers import kkt_certificate
     B32 = 256
     kw = dict(CFG, use_dcm=False)
-    spec, W, LBW, UBW, pst, _ = corridor_batch(B32, **{k: v for k, v in kw.items() if k != 'model'})
-    r64 = device_solver(spec, B32, LBW, UBW, IPMOptions(max_iter=1000)).solve(W)
-    r32 = device_solver(spec, B32, LBW, UBW, IPMOptions(max_iter=1000, tol=1e-6), jac32=True).solve(W)
+    with _Heartbeat('config 5 fp32 leg'):
+        spec, W, LBW, UBW, pst, _ = corridor_batch(B32, **{k: v for k, v in kw.items() if k != 'model'})
+        r64 = device_solver(spec, B32, LBW, UBW, IPMOptions(max_iter=1000)).solve(W)
+        r32 = device_solver(spec, B32, LBW, UBW, IPMOptions(max_iter=1000, tol=1e-6), jac32=True).solve(W)
     ok64 = np.array([s == 'optimal' for s in r64.status])
     ok32 = np.array([s in ('optimal', 'acceptable') for s in r32.status])
     l64, l32 = (r.x[:spec.N].sum(0).cpu().numpy() for r in (r64, r32))
@@ -156,8 +184,9 @@ def test_config5_cpc_solve():
     from aircraft_trajectory_optimization_amd.solver.ipm import IPMOptions
     from tests.helpers import kkt_certificate
     Bc = 64
-    spec, W, LBW, UBW, _ = cpc_warm_batch(Bc, use_dcm=True)
-    res = device_solver(spec, Bc, LBW, UBW, IPMOptions(max_iter=1000)).solve(W, progress=50)   # (progress: a heartbeat)
+    with _Heartbeat('config 5 CPC test'):
+        spec, W, LBW, UBW, _ = cpc_warm_batch(Bc, use_dcm=True)
+        res = device_solver(spec, Bc, LBW, UBW, IPMOptions(max_iter=1000)).solve(W)
     ok = [b for b, s in enumerate(res.status) if s in ('optimal', 'acceptable')]
     print('CPC solve:', {s: res.status.count(s) for s in set(res.status)})
     assert len(ok) >= 1

@@ -48,12 +48,33 @@ def _work(args):
             'lap': float(np.sum(r.x[:spec.N])), 'core': core}
 
 
+def _physical(cpu):
+    ''' (package, core) of a logical CPU: SMT siblings share it (None when sysfs does not say) '''
+    base = f'/sys/devices/system/cpu/cpu{cpu}/topology/'
+    try:
+        with open(base + 'physical_package_id') as f1, open(base + 'core_id') as f2:
+            return int(f1.read()), int(f2.read())
+    except (OSError, ValueError):
+        return None
+
+
 def _cores(workers):
-    ''' distinct cores of this process's affinity set for the workers (None when there are too few) '''
+    ''' distinct physical cores of this process's affinity set for the workers, one logical CPU each (SMT
+    siblings would share a core's pipelines); None when there are too few '''
     try:
         avail = sorted(os.sched_getaffinity(0))
     except (AttributeError, OSError):
         return [None] * workers
+    seen, first = set(), []
+    for c in avail:
+        key = _physical(c)
+        if key is None:
+            first.append(c)
+        elif key not in seen:
+            seen.add(key)
+            first.append(c)
+    if len(first) >= workers:
+        return first[:workers]
     return avail[:workers] if len(avail) >= workers else [None] * workers
 
 

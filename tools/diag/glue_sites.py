@@ -2,7 +2,7 @@
 DIAGNOSTIC (GPU): torch operators (= device launches, copies included) of the batched interior-point solver
 per source line, on the real config-3 workload (B cold starts, max_iter iterations), counted by a torch
 dispatch mode on the main thread (the restoration phases' worker threads run the same code and are not
-counted). Prints the top lines and the total per lockstep iteration.
+counted unless --threads). Prints the top lines and the total per lockstep iteration.
     python tools/diag/glue_sites.py --batch 512 --max-iter 60 --out gpurun_out/glue.json
 '''
 import argparse
@@ -21,6 +21,7 @@ def main():
     ap.add_argument('--max-iter', type=int, default=60)
     ap.add_argument('--top', type=int, default=60)
     ap.add_argument('--out', default=None)
+    ap.add_argument('--threads', action='store_true', help='count the restoration worker threads too')
     a = ap.parse_args()
     import torch
     from torch.utils._python_dispatch import TorchDispatchMode
@@ -29,6 +30,7 @@ def main():
     from aircraft_trajectory_optimization_amd.tracks import make_spec
     pkg = os.path.join(ROOT, 'aircraft_trajectory_optimization_amd')
     sites = collections.Counter()
+    nbytes = collections.Counter()          # bytes of the operators' inputs and outputs (a traffic estimate)
     ops = collections.defaultdict(collections.Counter)
     # operators that launch nothing on the device (views, metadata, host scalars)
     free = ('aten.view', 'aten._unsafe_view', 'aten.t.', 'aten.alias', 'aten.detach', 'aten.unsqueeze', 'aten.squeeze',
@@ -53,8 +55,22 @@ def main():
                 site = site or 'other'
                 sites[site] += 1
                 ops[site][name] += 1
+                outs = out if isinstance(out, (tuple, list)) else (out,)
+                nbytes[site] += sum(t.numel() * t.element_size() for t in list(args) + list(outs)
+                                    if torch.is_tensor(t) and t.is_cuda)
             return out
 
+    if a.threads:
+        # the restoration phases run in worker threads (dispatch modes are per thread): count there too
+        import concurrent.futures as cf
+        submit0 = cf.ThreadPoolExecutor.submit
+
+        def submit(self, fn, *args, **kwargs):
+            def run(*a_, **k_):
+                with Count():
+                    return fn(*a_, **k_)
+            return submit0(self, run, *args, **kwargs)
+        cf.ThreadPoolExecutor.submit = submit
     spec = make_spec(track='race', model='drone', frame='parametric', N=50, K=4, use_quat=True, global_r=True)
     lock = {'n': 0}
     with Count():
@@ -63,11 +79,16 @@ def main():
     torch.cuda.synchronize()
     n = max(lock['n'], 1)
     tot = sum(sites.values())
-    print(f'lockstep iterations {n}, device operators on the main thread {tot} ({tot / n:.0f} per iteration)')
+    print(f'lockstep iterations {n}, device operators ({"all threads" if a.threads else "main thread"}) {tot} '
+          f'({tot / n:.0f} per iteration)')
+    print('by launches:')
     for s, c in sites.most_common(a.top):
-        print(f'{c / n:8.1f}  {s}   {dict(ops[s].most_common(3))}')
+        print(f'{c / n:8.1f}  {nbytes[s] / n / 1e6:8.1f} MB  {s}   {dict(ops[s].most_common(3))}')
+    print('by bytes:')
+    for s, b in nbytes.most_common(a.top // 2):
+        print(f'{sites[s] / n:8.1f}  {b / n / 1e6:8.1f} MB  {s}   {dict(ops[s].most_common(3))}')
     if a.out:
-        json.dump({'lockstep': n, 'total': tot, 'sites': sites.most_common(),
+        json.dump({'lockstep': n, 'total': tot, 'sites': sites.most_common(), 'bytes': nbytes.most_common(),
                    'ops': {k: dict(v) for k, v in ops.items()}}, open(a.out, 'w'), indent=1)
 
 
