@@ -1043,6 +1043,41 @@ __global__ __launch_bounds__(RD_THREADS) void k_refine_decide(int W, int nch, in
     if (mode != 0 && tid == 0) list[0] = total;
 }
 
+
+// ------------------------------------------------------------------------------------------
+// Rows of the restoration phase's reduced KKT system (batched_ipm.py _RestorationKKT.factor): the
+// p and n variables of row i are eliminated, so the row diagonal becomes dr - 1/dp - 1/dn (the same
+// operations in the same order as the torch formulation), and their diagonals' signs add to the
+// inertia: cnt[b] = (#dp > 0 + #dn > 0, #dp < 0 + #dn < 0) over the rows (integer atomics: exact).
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_resto_rows(int m, int W, int rows, const double* __restrict__ dr,
+                                                    const double* __restrict__ dp, const double* __restrict__ dn,
+                                                    double* __restrict__ drow, int* __restrict__ cnt) {
+    __shared__ int sp[4][64], sn[4][64];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int col = blockIdx.x * 64 + lane;
+    const int r0 = blockIdx.y * rows, r1 = min(m, r0 + rows);
+    int np = 0, nn = 0;
+    if (col < W) {
+        for (int r = r0 + wv; r < r1; r += 4) {
+            const long long i = (long long)r * W + col;
+            const double a = dp[i], c = dn[i];
+            drow[i] = (dr[i] - 1.0 / a) - 1.0 / c;
+            np += (a > 0.0) + (c > 0.0);
+            nn += (a < 0.0) + (c < 0.0);
+        }
+    }
+    sp[wv][lane] = np;
+    sn[wv][lane] = nn;
+    __syncthreads();
+    if (wv == 0 && col < W) {
+        const int tp = sp[0][lane] + sp[1][lane] + sp[2][lane] + sp[3][lane];
+        const int tn = sn[0][lane] + sn[1][lane] + sn[2][lane] + sn[3][lane];
+        if (tp) atomicAdd(&cnt[2 * col + 0], tp);
+        if (tn) atomicAdd(&cnt[2 * col + 1], tn);
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -1254,6 +1289,18 @@ int ato_ipm_refine_decide(int32_t N, int32_t W, int32_t mode, int32_t k, const d
                        ato_ipm_refine_work(N, W), mode, k, o, part_a, mode ? part_c : nullptr, sel, nr, rr, old, bad,
                        refine, need, list, ok);
     return check_launch("ato_ipm_refine_decide");
+}
+
+
+int ato_ipm_resto_rows(int32_t m, int32_t W, const double* dr, const double* dp, const double* dn, double* drow,
+                       int32_t* cnt, void* stream) {
+    if (m < 0 || W < 0 || (m && W && (!dr || !dp || !dn || !drow || !cnt)))
+        return fail(ATO_ERR_ARG, "ato_ipm_resto_rows: arguments");
+    if (m == 0 || W == 0) return 0;
+    const int rows = 256;
+    hipLaunchKernelGGL(k_resto_rows, dim3((W + 63) / 64, (m + rows - 1) / rows), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), m, W, rows, dr, dp, dn, drow, cnt);
+    return check_launch("ato_ipm_resto_rows");
 }
 
 }  // extern "C"

@@ -20,6 +20,24 @@ def _p(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
 
+def resto_rows(dr, dp, dn):
+    ''' the restoration KKT's row diagonal dr - 1/dp - 1/dn ([m][W] fp64) and the signs of dp, dn per column
+    (int32 [W][2]: positive, negative counts) in one launch (ato_ipm_resto_rows) '''
+    m, W = dr.shape
+    for t in (dr, dp, dn):
+        if t.dtype != torch.float64 or t.shape != (m, W) or not t.is_cuda:
+            raise ValueError('resto_rows: expected fp64 [m, W] device tensors')
+    dr, dp, dn = dr.contiguous(), dp.contiguous(), dn.contiguous()
+    drow = torch.empty_like(dr)
+    cnt = torch.zeros((W, 2), dtype=torch.int32, device=dr.device)
+    lib = native.load()
+    rc = lib.ato_ipm_resto_rows(m, W, _p(dr), _p(dp), _p(dn), _p(drow), _p(cnt),
+                                ctypes.c_void_p(torch.cuda.current_stream(dr.device).cuda_stream))
+    if rc != 0:
+        raise RuntimeError(f'ato_ipm_resto_rows failed ({rc}): {lib.ato_last_error().decode()}')
+    return drow, cnt
+
+
 class DeviceIPMKernels:
     def __init__(self, n: int, m: int, iin: torch.Tensor, ieq: torch.Tensor, device):
         self.lib = native.load()

@@ -184,6 +184,13 @@ int ato_ipm_refine_decide(int32_t N, int32_t W, int32_t mode, int32_t k, const d
                           const double* part_c, const uint8_t* sel, const double* nr, double* rr, double* old,
                           uint8_t* bad, uint8_t* refine, uint8_t* need, int32_t* list, uint8_t* ok, void* stream);
 
+
+/* Rows of the restoration phase's reduced KKT system (solver/batched_ipm.py _RestorationKKT): drow =
+ * dr - 1/dp - 1/dn elementwise on [m][W], and cnt[b] (int32 [W][2], ADDED to: zero it first) +=
+ * (number of dp, dn > 0, number of dp, dn < 0) over the m rows of column b. */
+int ato_ipm_resto_rows(int32_t m, int32_t W, const double* dr, const double* dp, const double* dn, double* drow,
+                       int32_t* cnt, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
