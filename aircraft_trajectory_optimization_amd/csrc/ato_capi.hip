@@ -49,7 +49,7 @@ static void release(ato_handle* h) {
     (void)hipFree(h->d_units_lf);
     (void)hipFree(h->d_fpart);
     for (int32_t* d : {h->d_color, h->d_take_e, h->d_take_r, h->d_tk_ptr, h->d_tk_ent, h->d_tk_row, h->d_tkf_ptr,
-                       h->d_tkf_ent, h->d_tkf_row})
+                       h->d_tkf_ent, h->d_tkf_row, h->d_take_off})
         (void)hipFree(d);
     (void)hipFree(h->d_amask);
     (void)hipFree(h->d_dJ);
@@ -221,6 +221,18 @@ int ato_bounds(const ato_handle* h, double* lbg, double* ubg) {
     return ATO_OK;
 }
 
+// colours whose seeded passes share one launch: their scratch is held at once, within a byte budget
+// (ATO_HESS_GROUP_BYTES, default 2 GiB) -- at B = 512 on the racetrack nine colours, at restoration widths
+// all of them
+static size_t hess_group_bytes() {
+    static const size_t v = [] {
+        const char* e = std::getenv("ATO_HESS_GROUP_BYTES");
+        const long long b = e ? std::atoll(e) : (2LL << 30);
+        return (size_t)(b > 0 ? b : 0);
+    }();
+    return v;
+}
+
 static int hess_reserve(ato_handle* h, int32_t max_batch) {
     if (max_batch <= h->hess_reserved) return ATO_OK;
     // the old scratch may still be read by kernels queued on any stream: drain before freeing
@@ -229,9 +241,19 @@ static int hess_reserve(ato_handle* h, int32_t max_batch) {
     (void)hipFree(h->d_dgf);
     h->d_dJ = h->d_dgf = nullptr;
     h->hess_reserved = 0;
-    ATO_HIP(hipMalloc(&h->d_dJ, (size_t)std::max(h->L.p.nnz, 1) * max_batch * sizeof(double)));
-    ATO_HIP(hipMalloc(&h->d_dgf, (size_t)h->L.p.nw * max_batch * sizeof(double)));
+    h->hess_colors = 0;
+    const size_t per = ((size_t)std::max(h->L.p.nnz, 1) + (size_t)h->L.p.nw) * (size_t)max_batch * sizeof(double);
+    const int nc = std::max(h->HL.n_colors, 1);
+    const int g = (int)std::max<size_t>(1, std::min<size_t>((size_t)nc, hess_group_bytes() / std::max<size_t>(per, 1)));
+    ATO_HIP(hipMalloc(&h->d_dJ, (size_t)g * std::max(h->L.p.nnz, 1) * max_batch * sizeof(double)));
+    if (hipMalloc(&h->d_dgf, (size_t)g * h->L.p.nw * max_batch * sizeof(double)) != hipSuccess) {
+        (void)hipGetLastError();
+        (void)hipFree(h->d_dJ);
+        h->d_dJ = nullptr;
+        return fail(ATO_ERR_HIP, "hessian scratch: out of device memory");
+    }
     h->hess_reserved = max_batch;
+    h->hess_colors = g;
     return ATO_OK;
 }
 
@@ -341,7 +363,8 @@ static int ensure_hess_impl(ato_handle* h) {
         (rc = upload(h->HL.take_r, &h->d_take_r)) || (rc = upload(h->HL.tk_ptr, &h->d_tk_ptr)) ||
         (rc = upload(h->HL.tk_ent, &h->d_tk_ent)) || (rc = upload(h->HL.tk_row, &h->d_tk_row)) ||
         (rc = upload(h->HL.tkf_ptr, &h->d_tkf_ptr)) || (rc = upload(h->HL.tkf_ent, &h->d_tkf_ent)) ||
-        (rc = upload(h->HL.tkf_row, &h->d_tkf_row)) || (rc = upload(h->HL.amask, &h->d_amask)))
+        (rc = upload(h->HL.tkf_row, &h->d_tkf_row)) || (rc = upload(h->HL.amask, &h->d_amask)) ||
+        (rc = upload(h->HL.take_off, &h->d_take_off)))
         return rc;
     h->hess_ready = true;
     return ATO_OK;
@@ -373,7 +396,10 @@ extern "C" int ato_hess_eval(ato_handle* h, int32_t batch, int32_t layout, const
     const ato::HessDev hd{h->d_color, h->d_take_e, h->d_take_r, mk ? h->d_tk_ptr : h->d_tkf_ptr,
                           mk ? h->d_tk_ent : h->d_tkf_ent, mk ? h->d_tk_row : h->d_tkf_row,
                           mk ? h->d_amask : nullptr, h->HL.mask_words,
-                          h->HL.take_off.data(), h->HL.n_colors, h->HL.nnz()};
+                          h->HL.take_off.data(), h->HL.n_colors, h->HL.nnz(), h->d_take_off,
+                          // colours per launch at this batch: as many as the scratch holds
+                          (int)std::max<long long>(1, std::min<long long>(h->HL.n_colors,
+                              (long long)h->hess_colors * h->hess_reserved / batch))};
     hipError_t e = hipSuccess;
     ato::ProbD p = batch <= h->lf_max_batch ? h->pd_lf : h->pd;   // unit order as in ato_eval
     p.gf_sparse = 0;    // the seeded passes' grad f tangents fill a scratch buffer: every entry is written

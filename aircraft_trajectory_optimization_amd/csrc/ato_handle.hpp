@@ -39,7 +39,11 @@ struct ato_handle {
     int32_t *d_tkf_ptr = nullptr, *d_tkf_ent = nullptr, *d_tkf_row = nullptr;
     uint32_t* d_amask = nullptr;
     bool hess_mask = false;           // ATO_HESS_MASK=1: the masked colour passes (HessLayout::amask)
-    double* d_dJ = nullptr;     // [nnz][hess_reserved] Jacobian tangents of one colour
-    double* d_dgf = nullptr;    // [nw][hess_reserved] grad f tangents of one colour
+    int32_t* d_take_off = nullptr;    // device copy of HL.take_off (the colour of a take, grouped passes)
+    // seeded-pass scratch for hess_colors colours at hess_reserved instances: [colour][nnz][B] / [colour][nw][B]
+    // (a launch runs as many colours as fit at its batch: fewer, larger launches)
+    double* d_dJ = nullptr;
+    double* d_dgf = nullptr;
     int32_t hess_reserved = 0;
+    int32_t hess_colors = 0;
 };

@@ -419,15 +419,19 @@ struct DevTangentSinkMasked {
     __device__ __forceinline__ void finish() {}
 };
 
-// one seeded pass for colour c: dJ = d J / d eps, dgf = d grad f / d eps along v_c
-// (outputs interleaved [entry][B]; w in either layout)
+// seeded passes for colours c0 + z (z = blockIdx.z): dJ = d J / d eps, dgf = d grad f / d eps along v_c,
+// colour z's tangents at dJ + z sJ, dgf + z sG (outputs interleaved [entry][B]; w in either layout)
 template <class M, int UMASK, bool MASKED = false>
 __global__ __launch_bounds__(WAVE) void k_hess_dual(ProbD p, int B, int layout, const double* __restrict__ w,
-                                                   const int32_t* __restrict__ color, int c,
-                                                   const uint32_t* __restrict__ amask,
-                                                   double* __restrict__ dJ, double* __restrict__ dgf) {
+                                                   const int32_t* __restrict__ color, int c0,
+                                                   const uint32_t* __restrict__ amask, int mask_words,
+                                                   double* __restrict__ dJ, double* __restrict__ dgf, long sJ,
+                                                   long sG) {
     const int b = blockIdx.x * WAVE + threadIdx.x;
     if (b >= B) return;
+    const int c = c0 + (int)blockIdx.z;
+    dJ += (long)blockIdx.z * sJ;
+    dgf += (long)blockIdx.z * sG;
     const int32_t* ut = p.units + 4 * blockIdx.y;
     const bool il = layout == ATO_LAYOUT_INTERLEAVED;
     const ColorW<double, DevW<double>> W{DevW<double>{il ? w + b : w + (long)b * p.nw, il ? (long)B : 1L,
@@ -435,7 +439,7 @@ __global__ __launch_bounds__(WAVE) void k_hess_dual(ProbD p, int B, int layout, 
                                          color, c};
     const TangentGrad<double> go{dgf + b, (long)B};
     if constexpr (MASKED) {
-        DevTangentSinkMasked<double> s{dJ + b, (long)B, 0, amask, 0};
+        DevTangentSinkMasked<double> s{dJ + b, (long)B, 0, amask + (long)c * mask_words, 0};
         run_unit<M, Dual<double, 1>, 0, true, true, UMASK>(p, ut[0], ut[1], ut[2], W, s, go);
     } else {
         DevTangentSink<double> s{dJ + b, (long)B, 0};
@@ -443,10 +447,11 @@ __global__ __launch_bounds__(WAVE) void k_hess_dual(ProbD p, int B, int layout, 
     }
 }
 
-// Hessian entries recovered from colour c: one wave = one take for 64 instances
-// (a template only so that every translation unit may instantiate it)
+// Hessian entries recovered from colours c0 .. c1 - 1: one wave = one take for 64 instances; the take's
+// colour from the take offsets (a template only so that every translation unit may instantiate it)
 template <int UNUSED = 0>
-__global__ __launch_bounds__(WAVE) void k_hess_take(int B, int layout, int ng, int nnzh, int t0,
+__global__ __launch_bounds__(WAVE) void k_hess_take(int B, int layout, int ng, int nnzh, int t0, int c0, int c1,
+                                                   const int32_t* __restrict__ take_off,
                                                    const int32_t* __restrict__ take_e,
                                                    const int32_t* __restrict__ take_r,
                                                    const int32_t* __restrict__ tk_ptr,
@@ -454,10 +459,14 @@ __global__ __launch_bounds__(WAVE) void k_hess_take(int B, int layout, int ng, i
                                                    const int32_t* __restrict__ tk_row,
                                                    const double* __restrict__ lam, const double* __restrict__ sigma,
                                                    const double* __restrict__ dJ, const double* __restrict__ dgf,
-                                                   double* __restrict__ H) {
+                                                   long sJ, long sG, double* __restrict__ H) {
     const int b = blockIdx.x * WAVE + threadIdx.x;
     if (b >= B) return;
     const int t = t0 + blockIdx.y;
+    int c = c0;
+    while (c + 1 < c1 && take_off[c + 1] <= t) ++c;          // (uniform across the wave)
+    dJ += (long)(c - c0) * sJ;
+    dgf += (long)(c - c0) * sG;
     const int e = take_e[t], r = take_r[t];
     const bool il = layout == ATO_LAYOUT_INTERLEAVED;
     const double* lb = il ? lam + b : lam + (long)b * ng;
@@ -474,6 +483,8 @@ struct HessDev {
     int mask_words;
     const int32_t* take_off_host;   // host array [n_colors + 1]
     int n_colors, nnzh;
+    const int32_t* take_off;        // device copy
+    int group;                      // colours per launch (their scratch side by side)
 };
 
 template <class M>
@@ -558,23 +569,26 @@ template <class M>
 hipError_t launch_hess(const ProbD& p, const HessDev& hd, int B, int layout, const double* w, const double* lam,
                        const double* sigma, double* H, double* dJ, double* dgf, hipStream_t st) {
     const int chunks = (B + WAVE - 1) / WAVE;
-    for (int c = 0; c < hd.n_colors; ++c) {
+    const long sJ = (long)p.nnz * B, sG = (long)p.nw * B;
+    const int G = hd.group > 0 ? hd.group : 1;
+    for (int c0 = 0; c0 < hd.n_colors; c0 += G) {
+        const int c1 = c0 + G < hd.n_colors ? c0 + G : hd.n_colors;
         {
-            const uint32_t* am = hd.amask ? hd.amask + (long)c * hd.mask_words : nullptr;
-            const dim3 grid(chunks, p.n_units);
+            const dim3 grid(chunks, p.n_units, c1 - c0);
+            const uint32_t* am = hd.amask;
             if (p.trans == ATO_TRANS_RK4) {
-                if (am) hipLaunchKernelGGL((k_hess_dual<M, UMASK_RK4, true>), grid, dim3(WAVE), 0, st, p, B, layout, w, hd.color, c, am, dJ, dgf);
-                else hipLaunchKernelGGL((k_hess_dual<M, UMASK_RK4>), grid, dim3(WAVE), 0, st, p, B, layout, w, hd.color, c, am, dJ, dgf);
+                if (am) hipLaunchKernelGGL((k_hess_dual<M, UMASK_RK4, true>), grid, dim3(WAVE), 0, st, p, B, layout, w, hd.color, c0, am, hd.mask_words, dJ, dgf, sJ, sG);
+                else hipLaunchKernelGGL((k_hess_dual<M, UMASK_RK4>), grid, dim3(WAVE), 0, st, p, B, layout, w, hd.color, c0, am, hd.mask_words, dJ, dgf, sJ, sG);
             } else {
-                if (am) hipLaunchKernelGGL((k_hess_dual<M, UMASK_COLLOC, true>), grid, dim3(WAVE), 0, st, p, B, layout, w, hd.color, c, am, dJ, dgf);
-                else hipLaunchKernelGGL((k_hess_dual<M, UMASK_COLLOC>), grid, dim3(WAVE), 0, st, p, B, layout, w, hd.color, c, am, dJ, dgf);
+                if (am) hipLaunchKernelGGL((k_hess_dual<M, UMASK_COLLOC, true>), grid, dim3(WAVE), 0, st, p, B, layout, w, hd.color, c0, am, hd.mask_words, dJ, dgf, sJ, sG);
+                else hipLaunchKernelGGL((k_hess_dual<M, UMASK_COLLOC>), grid, dim3(WAVE), 0, st, p, B, layout, w, hd.color, c0, am, hd.mask_words, dJ, dgf, sJ, sG);
             }
         }
-        const int t0 = hd.take_off_host[c], nt = hd.take_off_host[c + 1] - t0;
+        const int t0 = hd.take_off_host[c0], nt = hd.take_off_host[c1] - t0;
         if (nt > 0)
-            hipLaunchKernelGGL(k_hess_take<0>, dim3(chunks, nt), dim3(WAVE), 0, st, B, layout, p.ng, hd.nnzh, t0,
-                               hd.take_e, hd.take_r, hd.tk_ptr, hd.tk_ent, hd.tk_row, lam, sigma,
-                               (const double*)dJ, (const double*)dgf, H);
+            hipLaunchKernelGGL(k_hess_take<0>, dim3(chunks, nt), dim3(WAVE), 0, st, B, layout, p.ng, hd.nnzh, t0, c0,
+                               c1, hd.take_off, hd.take_e, hd.take_r, hd.tk_ptr, hd.tk_ent, hd.tk_row, lam, sigma,
+                               (const double*)dJ, (const double*)dgf, sJ, sG, H);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
