@@ -1671,7 +1671,7 @@ class BatchedInteriorPoint:
                     done = self._resto_collect(j, cols, x, s, B0)
                     infl = infl & ~done[0]
             if done is None and len(inflight) < self.ASYNC_PHASES and n_wait and \
-                    (n_act == 0 or n_wait >= max(1, n_act // 8) or it % 10 == 9):
+                    (n_act == 0 or n_wait >= max(1, n_act // self.RESTO_BATCH_DIV) or it % 10 == 9):
                 R = waiting.clone()
                 # at most resto_phase_max columns per phase (the others wait for the next one): a phase in
                 # a worker thread factorises in its own storage, and the nested solve's [n + 2m, R]
@@ -2006,6 +2006,9 @@ class BatchedInteriorPoint:
 
     # restoration phases in flight at once (each: own handle, storage, stream); ATO_ASYNC_PHASES overrides
     ASYNC_PHASES = int(os.environ.get('ATO_ASYNC_PHASES', '3'))
+    # a restoration phase starts once the waiting columns are 1 / RESTO_BATCH_DIV of the stepping ones (or
+    # every tenth iteration, or when nothing else steps): fewer, wider phases against shorter waits
+    RESTO_BATCH_DIV = int(os.environ.get('ATO_RESTO_BATCH_DIV', '8'))
     ASYNC_PHASE_BYTES = 4e9         # factor storage of one phase in flight (its columns are capped to fit)
     ASYNC_MAX_BATCH = 1 << 30       # (batches above it would restore synchronously, on the main storage)
 
