@@ -106,6 +106,12 @@ constexpr int EPT = 8;                    // entries per thread and front (<= 40
 #define ATO_KKT_S16_NG 2      // row groups of the 16-wide-tile Schur update (with tile guards: 2 groups 18.46 ms,
                               // 3: 18.22, 4: 18.57; without: 2: 13.74, 3: 14.07)
 #endif
+#ifndef ATO_KKT_PRIO
+#define ATO_KKT_PRIO 0        // wave priority of the pivot search and decision (s_setprio), 0 before the Schur
+                              // update: the fronts sharing a CU issue their chain ahead of another's FMAs
+#endif
+#define KKT_PRIO_CHAIN() do { if (ATO_KKT_PRIO) __builtin_amdgcn_s_setprio(ATO_KKT_PRIO); } while (0)
+#define KKT_PRIO_UPDATE() do { if (ATO_KKT_PRIO) __builtin_amdgcn_s_setprio(0); } while (0)
 #ifndef ATO_KKT_CH
 #define ATO_KKT_CH 512      // 8 KB ring: B = 512 solve 3.28 -> 3.01 ms against 16 KB (64 KB: 11.1 ms); B = 1 0.37 -> 0.38 ms
 #endif
@@ -513,6 +519,7 @@ __global__ __launch_bounds__(FTT) __attribute__((amdgpu_waves_per_eu(W))) void k
         const int k = kc;
         double* ck = colb + (par * 2 + 0) * NP;
         double* cr = colb + (par * 2 + 1) * NP;
+        KKT_PRIO_CHAIN();
         extract_column<T, NC>(a, k, ti, tj, ck);
         lds_barrier();
         KST(1);                  // extract + barrier (waits for the slowest wave's update)
@@ -630,6 +637,7 @@ __global__ __launch_bounds__(FTT) __attribute__((amdgpu_waves_per_eu(W))) void k
         // Schur update: one rank-1 pass (1x1 pivot) or two (2x2 pivot), A -= l c^T with c the
         // pivot column (pass 0: c0, pass 1: cr)
         const int npass = type == 0 ? 1 : type == 1 ? 2 : 0;
+        KKT_PRIO_UPDATE();
         for (int pass = 0; pass < npass; ++pass) {
             const double* cc = pass == 1 ? cr : c0p;
             const double f0 = pass == 1 ? i01 : i00, f1 = pass == 1 ? i11 : i01;
@@ -868,6 +876,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void k
         const int k = kc;
         double* ck = colb + (par * 2 + 0) * NP;
         double* cr = colb + (par * 2 + 1) * NP;
+        KKT_PRIO_CHAIN();
         extract_column16<TT>(a, k, ti, tj, ck);
         lds_barrier();
         unsigned key = 0u;
@@ -970,6 +979,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void k
         loff += (long long)nlive * ncol;
         const int npass = type == 0 ? 1 : type == 1 ? 2 : 0;
         const int J0 = k >> 4;                   // tiles left of k's tile hold only eliminated positions
+        KKT_PRIO_UPDATE();
 #pragma unroll 1
         for (int pass = 0; pass < npass; ++pass) {
             const double* cc = pass == 1 ? cr : c0p;

@@ -63,6 +63,10 @@ def parse():
                     help='config 5\'s CPC gate-progress formulation (build-side, global frame, the gates as '
                          'waypoints; N rounds up to the gate phases): --track fig8 --pose dcm --cpc --dtype f32 '
                          '--batch 8192 --no-solve')
+    ap.add_argument('--jac32', action='store_true',
+                    help='config 5 solve (--track fig8): the Jacobian of every iterate from the fp32 evaluation kernel '
+                         '(g, f, grad f, the Hessian and the KKT stay fp64); use with --tol 1e-6')
+    ap.add_argument('--tol', type=float, default=1e-8, help="IPOPT's tol (1e-8, base_raceline.py defaults)")
     ap.add_argument('--cpu-seconds', type=float, default=15.0, help='budget of the CPU baselines')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-solve', action='store_true', help='evaluation kernel only')
@@ -261,17 +265,18 @@ def main():
             from aircraft_trajectory_optimization_amd.raceline.batch_instances import corridor_batch
             from aircraft_trajectory_optimization_amd.solver.batched_ipm import device_solver
             wkw = {k: v for k, v in spec_kw.items() if k not in ('model',)}
-            if args.pose == 'esp':
-                raise SystemExit('the fig-8 solve batch is the DCM pose (config 5): --pose dcm')
             spec, Wws, LBW, UBW, _, _ = corridor_batch(len(seeds), device=dev, seeds=seeds,
                                                         progress=args.progress, **wkw)
             sync()
             t0 = time.perf_counter()
-            solver = device_solver(spec, len(seeds), LBW, UBW, IPMOptions(max_iter=args.max_iter), device=dev)
+            solver = device_solver(spec, len(seeds), LBW, UBW, IPMOptions(max_iter=args.max_iter, tol=args.tol),
+                                   device=dev, jac32=args.jac32)
             res = solver.solve(Wws, on_iteration=hook, progress=args.progress)
         else:
             t0 = time.perf_counter()
-            res, solver, _ = solve_shard(spec, seeds, IPMOptions(max_iter=args.max_iter), on_iteration=hook,
+            if args.jac32:
+                raise SystemExit('--jac32 is the config-5 solve leg: --track fig8')
+            res, solver, _ = solve_shard(spec, seeds, IPMOptions(max_iter=args.max_iter, tol=args.tol), on_iteration=hook,
                                          progress=args.progress)
         sync()
         t_solve = time.perf_counter() - t0
@@ -314,11 +319,11 @@ def main():
                 opt = [i for i, st in enumerate(res.status) if st == 'optimal']
                 i0 = opt[0] if opt else 0
                 if args.track == 'fig8':
-                    s1 = device_solver(spec, 1, LBW[i0:i0 + 1], UBW[i0:i0 + 1], IPMOptions(max_iter=args.max_iter),
-                                       device=dev)
+                    s1 = device_solver(spec, 1, LBW[i0:i0 + 1], UBW[i0:i0 + 1],
+                                       IPMOptions(max_iter=args.max_iter, tol=args.tol), device=dev, jac32=args.jac32)
                     r1 = s1.solve(Wws[i0:i0 + 1])
                 else:
-                    r1, s1, _ = one(spec, [seeds[i0]], IPMOptions(max_iter=args.max_iter))
+                    r1, s1, _ = one(spec, [seeds[i0]], IPMOptions(max_iter=args.max_iter, tol=args.tol))
                 lap1 = float(r1.x[:spec.N].sum())
                 lap_err = abs(float(allrec[i0, 0]) - lap1)
                 sqp_full['lap_check_instance'] = {'seed': int(seeds[i0]), 'batched_lap_s': float(allrec[i0, 0]),
@@ -337,6 +342,8 @@ def main():
                 'scaling': 'weak',
                 'vs_baseline': None,
                 'dtype': 'f64',
+                'precision': ('fp32 Jacobian (ato_eval_f32, widened), fp64 g / f / grad f / Hessian / KKT' if args.jac32
+                              else 'fp64 throughout'),
                 'data': ('synthetic: seeded per-instance corridors, each warm-started from its own point-mass raceline '
                          '(raceline/batch_instances.py corridor_batch)' if args.track == 'fig8'
                          else 'synthetic: seeded cold-start instances (SURVEY 8(d) config 3 generator, '
@@ -344,7 +351,7 @@ def main():
                 'config': {'workload': f'{track}_parametric_{args.pose}_drone_colloc_N50_K4_'
                                        f'{"warm" if args.track == "fig8" else "cold"}_start_batched_sqp',
                            'N': 50, 'K': 4, 'nz': spec.nz, 'nu': 4, 'batch_per_gpu': B, 'global_batch': world * B,
-                           'max_iter': args.max_iter, 'layout': args.layout,
+                           'max_iter': args.max_iter, 'tol': args.tol, 'layout': args.layout,
                            'parallelism': f'instances sharded x{world}, records all-gathered'},
                 'lap_time_err_vs_casadi': None,
                 'lap_time_err_note': 'CasADi/IPOPT cannot run in this pipeline (SURVEY F8): lap-time parity with it '
