@@ -29,7 +29,7 @@ def main():
     ap.add_argument('--frame', default='parametric')
     ap.add_argument('--rk4', action='store_true')
     ap.add_argument('--ordering', default='nd', choices=['nd', 'chain'])
-    ap.add_argument('--saddle', type=int, default=1, help='1: saddle fronts for the collocation defects')
+    ap.add_argument('--saddle', type=int, default=0, help='1: saddle fronts for the collocation defects (opt-in plan; the solver default is 0, Bunch-Kaufman leaves)')
     ap.add_argument('--dr-eq', default='zero', choices=['zero', 'random'],
                     help='row diagonal of the equality rows: 0 (delta_c = 0, the interior-point default) or random')
     a = ap.parse_args()
