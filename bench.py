@@ -48,8 +48,8 @@ def parse():
     ap.add_argument('--warmup', type=int, default=5, help='untimed lockstep iterations before the window (driver: 5)')
     ap.add_argument('--batch', type=int, default=512, help='instances per GPU')
     ap.add_argument('--max-iter', type=int, default=1000, help="IPOPT's max_iter (base_raceline.py:54)")
-    ap.add_argument('--eval-steps', type=int, default=50)
-    ap.add_argument('--eval-warmup', type=int, default=10)
+    ap.add_argument('--eval-steps', type=int, default=200)
+    ap.add_argument('--eval-warmup', type=int, default=20)
     ap.add_argument('--dtype', choices=['f64', 'f32'], default='f64', help='evaluation-kernel bench dtype')
     ap.add_argument('--layout', choices=['interleaved', 'instance'], default='interleaved')
     ap.add_argument('--track', choices=['race', 'fig8', 'obstacles'], default='race',
@@ -80,8 +80,9 @@ def eval_bench(spec, W, args, dev, world):
     '''
     ato_eval over the batch (inputs resident in HBM): evals/s and the k_eval roofline. Kernel
     durations come from HIP events recorded inside the library on the evaluation stream, on
-    every stride-th step so that >= 10 launches are sampled (each recorded step adds ~10 us of
-    event gaps, tools/diag/step_gaps.py, which the other steps do not pay).
+    every stride-th step so that >= 40 launches are sampled (each recorded step adds ~10 us of
+    event gaps, tools/diag/step_gaps.py, which the other steps do not pay; with 10 samples the
+    average wandered by +-2 us against the rocprof average of the same run, r06final).
     '''
     import torch
     import torch.distributed as dist
@@ -96,7 +97,7 @@ def eval_bench(spec, W, args, dev, world):
     nw, ng, nnz = bn.sizes
     for _ in range(args.eval_warmup):
         bn.evaluate()
-    stride = max(1, args.eval_steps // 10)
+    stride = max(1, args.eval_steps // 40)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
