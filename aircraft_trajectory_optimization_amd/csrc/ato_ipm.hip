@@ -1045,6 +1045,40 @@ __global__ __launch_bounds__(RD_THREADS) void k_refine_decide(int W, int nch, in
 
 
 // ------------------------------------------------------------------------------------------
+// Scaled Jacobian and its transpose product (batched_ipm.py, the optimality check and the soft
+// restoration's primal-dual error): Js = jv * sg[row] entry by entry and jty = Js^T y, one thread per
+// (column i, instance) walking column i's entries in the structure's column order (the stable argsort
+// of the entries by column), so the sum runs in the order torch's segment_reduce adds them, from 0.
+// Products and sums are rounded one at a time (no contraction into FMAs): bit for bit the torch
+// formulation (a gather, a product, a gather, a product, a segment sum), in one pass over jv instead
+// of five over [nnz][W].
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_js_jty(int n, int W, const int32_t* __restrict__ col_ptr,
+                                                const int32_t* __restrict__ src, const int32_t* __restrict__ row,
+                                                const double* __restrict__ jv, const double* __restrict__ sg,
+                                                const double* __restrict__ y, double* __restrict__ js,
+                                                double* __restrict__ jty) {
+#pragma clang fp contract(off)
+    const int b = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int i = blockIdx.y * 4 + (threadIdx.x >> 6);          // one wave per column: uniform entry loop
+    if (i >= n || b >= W) return;
+    const int e0 = col_ptr[i], e1 = col_ptr[i + 1];
+    double acc = 0.0;
+    for (int k = e0; k < e1; ++k) {
+        const long long e = (long long)src[k] * W + b;
+        const long long r = (long long)row[k] * W + b;
+        double v = jv[e];
+        if (sg) {
+            v = v * sg[r];
+            if (js) js[e] = v;
+        }
+        const double t = v * y[r];
+        acc = acc + t;
+    }
+    jty[(long long)i * W + b] = acc;
+}
+
+// ------------------------------------------------------------------------------------------
 // Rows of the restoration phase's reduced KKT system (batched_ipm.py _RestorationKKT.factor): the
 // p and n variables of row i are eliminated, so the row diagonal becomes dr - 1/dp - 1/dn (the same
 // operations in the same order as the torch formulation), and their diagonals' signs add to the
@@ -1301,6 +1335,17 @@ int ato_ipm_resto_rows(int32_t m, int32_t W, const double* dr, const double* dp,
     hipLaunchKernelGGL(k_resto_rows, dim3((W + 63) / 64, (m + rows - 1) / rows), dim3(256), 0,
                        static_cast<hipStream_t>(stream), m, W, rows, dr, dp, dn, drow, cnt);
     return check_launch("ato_ipm_resto_rows");
+}
+
+int ato_ipm_js_jty(int32_t n, int32_t nnz, int32_t W, const int32_t* col_ptr, const int32_t* src, const int32_t* row,
+                   const double* jv, const double* sg, const double* y, double* js, double* jty, void* stream) {
+    if (n < 0 || nnz < 0 || W < 0 || (n && W && (!col_ptr || !jty || (nnz && (!src || !row || !jv || !y)))) ||
+        (js && !sg))
+        return fail(ATO_ERR_ARG, "ato_ipm_js_jty: arguments");
+    if (n == 0 || W == 0) return 0;
+    hipLaunchKernelGGL(k_js_jty, dim3((W + 63) / 64, (n + 3) / 4), dim3(256), 0, static_cast<hipStream_t>(stream),
+                       n, W, col_ptr, src, row, jv, sg, y, js, jty);
+    return check_launch("ato_ipm_js_jty");
 }
 
 }  // extern "C"

@@ -105,7 +105,7 @@ class AtoIpmBounds(ctypes.Structure):
 IPM_SYMBOLS = ('ato_ipm_work_size', 'ato_ipm_errors', 'ato_ipm_rhs', 'ato_ipm_direction', 'ato_ipm_measures',
                'ato_ipm_multipliers', 'ato_ipm_filter_accept', 'ato_ipm_kkt_diag', 'ato_ipm_perturb',
                'ato_ipm_status', 'ato_ipm_barrier', 'ato_ipm_filter_multi', 'ato_ipm_refine_work',
-               'ato_ipm_refine_pass', 'ato_ipm_refine_decide', 'ato_ipm_resto_rows')
+               'ato_ipm_refine_pass', 'ato_ipm_refine_decide', 'ato_ipm_resto_rows', 'ato_ipm_js_jty')
 
 EXPORTED_SYMBOLS = ('ato_create', 'ato_destroy', 'ato_sizes', 'ato_sparsity', 'ato_bounds',
                     'ato_reserve', 'ato_eval', 'ato_eval_f32', 'ato_hess_sparsity', 'ato_hess_eval',
@@ -179,6 +179,7 @@ def declare(lib: ctypes.CDLL, prefix: str = 'ato') -> ctypes.CDLL:
         lib.ato_ipm_refine_pass.argtypes = [ctypes.c_int32, ctypes.c_int32] + [vp] * 7 + [vp]
         lib.ato_ipm_refine_decide.argtypes = [ctypes.c_int32] * 4 + [vp] * 12 + [vp]
         lib.ato_ipm_resto_rows.argtypes = [ctypes.c_int32, ctypes.c_int32] + [vp] * 5 + [vp]
+        lib.ato_ipm_js_jty.argtypes = [ctypes.c_int32] * 3 + [vp] * 8 + [vp]
         for fn in IPM_SYMBOLS[1:]:
             getattr(lib, fn).restype = ctypes.c_int
         for fn in ('ato_create', 'ato_destroy', 'ato_sizes', 'ato_sparsity', 'ato_bounds', 'ato_reserve',

@@ -311,6 +311,8 @@ class _Laps:
 
 
 _DEBUG_HESS = os.environ.get('ATO_DEBUG_HESS_NONFINITE', '0') == '1'
+# Js and J^T y of the optimality check in one launch (ato_ipm_js_jty); 0: the torch formulation (A/B)
+_FUSED_JTY = os.environ.get('ATO_IPM_FUSED_JTY', '1') != '0'
 
 def _idx(mask: torch.Tensor) -> np.ndarray:
     return torch.nonzero(mask).reshape(-1).cpu().numpy().astype(np.int32)
@@ -344,6 +346,9 @@ def _structure(ev, dev) -> Dict[str, torch.Tensor]:
     pc = np.argsort(jc_np, kind='stable')
     d['jt_src'], d['jt_row'] = t(pc, torch.long), t(jr_np[pc], torch.long)
     d['jt_len'] = t(np.bincount(jc_np, minlength=n), torch.long)
+    # the same column order as int32 arrays for the fused kernel (ato_ipm_js_jty)
+    d['jt_ptr32'] = t(np.concatenate([[0], np.cumsum(np.bincount(jc_np, minlength=n))]), torch.int32)
+    d['jt_src32'], d['jt_row32'] = t(pc, torch.int32), t(jr_np[pc], torch.int32)
     w_row = np.concatenate([hr, hc[off]])
     w_col = np.concatenate([hc, hr[off]])
     w_src = np.concatenate([np.arange(len(hr)), off])
@@ -521,6 +526,15 @@ class BatchedInteriorPoint:
 
     def _JTy(self, Js, y):
         return self._segsum(Js[self.jt_src] * y[self.jt_row], self.jt_len, self.n_j)
+
+    def _js_jty(self, jv, y, want_js=True):
+        ''' (Js = jv * sg[jr] or None, Js^T y): one fused launch on the device (ato_ipm_js_jty, bit for bit
+        the torch formulation below, which the CPU stand-ins run) '''
+        if jv.is_cuda and _FUSED_JTY:
+            from aircraft_trajectory_optimization_amd.solver.ipm_device import js_jty
+            return js_jty(jv, self.sg, y, self.jt_ptr32, self.jt_src32, self.jt_row32, want_js)
+        Js = jv * self.sg[self.jr]
+        return (Js if want_js else None), self._JTy(Js, y)
 
     def _Wx(self, H, v):
         return self._segsum(H[self.w_src] * v[self.w_col], self.w_len, self.n_w)
@@ -1221,8 +1235,7 @@ class BatchedInteriorPoint:
                     sf, sg = self.sf, self.sg
                     self.stats['compactions'] += 1
                     laps.lap('compact')
-            Js = jv * sg[self.jr]
-            jty = self._JTy(Js, y)
+            Js, jty = self._js_jty(jv, y)
             dual_x = gf + jty - zl + zu
             if self.vk is not None:
                 E0, du, pr, co, pr_uns = self.vk.errors(self._bd(), x, s, g, self.c_rhs, sg, y, zl, zu, vl, vu,
@@ -1803,11 +1816,12 @@ class BatchedInteriorPoint:
             setattr(self, k, take(getattr(self, k)))
         return tuple(take(t) for t in tensors)
 
-    def _pd_error(self, gf, Js, g, x, s, y, zl, zu, vl, vu, mu):
+    def _pd_error(self, gf, jv, g, x, s, y, zl, zu, vl, vu, mu):
         ''' primal-dual system error per instance (solver/ipm.py pd_error): 1-norms of the dual,
-        primal and complementarity residuals over the number of their entries '''
+        primal and complementarity residuals over the number of their entries (jv: the unscaled
+        Jacobian values, scaled by sg here) '''
         a, b, c, d = self._slacks(x, s)
-        dual_x = gf + self._JTy(Js, y) - zl + zu
+        dual_x = gf + self._js_jty(jv, y, want_js=False)[1] - zl + zu
         dual_s = -y[self.iin] - vl + vu
         r = self._resid(g, s)
         tot = dual_x.abs().sum(0) + dual_s.abs().sum(0) + r.abs().sum(0)
@@ -1835,9 +1849,8 @@ class BatchedInteriorPoint:
         # CheckAcceptabilityOfTrialPoint(0): alpha test 0, never the Armijo case (and the reset heuristic)
         sat, _, _ = self._filter_test(theta, phi, zero, zero, tht, pht, F, nf, mask, torch.zeros_like(mask), frs,
                                       theta_min=torch.full_like(al, -1.0))
-        sg = self.sg
-        e_cur = self._pd_error(gf, jv * sg[self.jr], g, x, s, y, zl, zu, vl, vu, mu)
-        e_tr = self._pd_error(gft, jvt * sg[self.jr], gt, xt, st, yt, zlt, zut, vlt, vut, mu)
+        e_cur = self._pd_error(gf, jv, g, x, s, y, zl, zu, vl, vu, mu)
+        e_tr = self._pd_error(gft, jvt, gt, xt, st, yt, zlt, zut, vlt, vut, mu)
         ok = mask & (sat | (e_tr <= o.soft_resto_pderror_reduction_factor * e_cur))
         take(ok, al, xt, st, torch.ones_like(ok), dy)
         return ok, sat

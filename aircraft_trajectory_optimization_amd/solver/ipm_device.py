@@ -38,6 +38,31 @@ def resto_rows(dr, dp, dn):
     return drow, cnt
 
 
+def js_jty(jv, sg, y, col_ptr, src, row, want_js=True):
+    ''' (Js = jv * sg[row of each entry] or None, Js^T y [n][W]) in one launch (ato_ipm_js_jty): jv [nnz][W],
+    sg, y [m][W] fp64 device tensors; col_ptr [n + 1], src, row [nnz] int32 device tensors of the column order
+    (batched_ipm.py _structure: jt_ptr32 / jt_src32 / jt_row32). Bit for bit the torch formulation
+    `Js = jv * sg[jr]; segment_reduce(Js[jt_src] * y[jt_row], 'sum', jt_len)` '''
+    nnz, W = jv.shape
+    m = y.shape[0]
+    n = col_ptr.shape[0] - 1
+    for t, rows in ((jv, nnz), (sg, m), (y, m)):
+        if t.dtype != torch.float64 or t.dim() != 2 or t.shape != (rows, W) or not t.is_cuda:
+            raise ValueError(f'js_jty: expected fp64 [{rows}, {W}] device tensors, got {tuple(t.shape)} {t.dtype}')
+    for t, rows in ((col_ptr, n + 1), (src, nnz), (row, nnz)):
+        if t.dtype != torch.int32 or t.shape != (rows,) or not t.is_contiguous() or t.device != jv.device:
+            raise ValueError('js_jty: expected contiguous int32 structure arrays on the values\' device')
+    jv, sg, y = jv.contiguous(), sg.contiguous(), y.contiguous()
+    js = torch.empty_like(jv) if want_js else None
+    jty = torch.empty((n, W), dtype=torch.float64, device=jv.device)
+    lib = native.load()
+    rc = lib.ato_ipm_js_jty(n, nnz, W, _p(col_ptr), _p(src), _p(row), _p(jv), _p(sg), _p(y), _p(js), _p(jty),
+                            ctypes.c_void_p(torch.cuda.current_stream(jv.device).cuda_stream))
+    if rc != 0:
+        raise RuntimeError(f'ato_ipm_js_jty failed ({rc}): {lib.ato_last_error().decode()}')
+    return js, jty
+
+
 class DeviceIPMKernels:
     def __init__(self, n: int, m: int, iin: torch.Tensor, ieq: torch.Tensor, device):
         self.lib = native.load()

@@ -191,6 +191,16 @@ int ato_ipm_refine_decide(int32_t N, int32_t W, int32_t mode, int32_t k, const d
 int ato_ipm_resto_rows(int32_t m, int32_t W, const double* dr, const double* dp, const double* dn, double* drow,
                        int32_t* cnt, void* stream);
 
+/* The scaled Jacobian and its transpose product (solver/batched_ipm.py, the optimality check and the soft
+ * restoration's primal-dual error; replaces `Js = jv * sg[jr]` and `_JTy(Js, y)`, the sparse products IPOPT's
+ * dual infeasibility grad f + J^T y needs, ref: drone3d/raceline/base_raceline.py:752-799 via ca.nlpsol):
+ * jv [nnz][W] Jacobian values in CSR entry order, sg [m][W] row scaling (NULL: Js = jv, js must be NULL),
+ * y [m][W]; the entries of column i are src[col_ptr[i] .. col_ptr[i+1]) (entry indices, ascending within a
+ * column) with rows row[.]. Writes js [nnz][W] = jv * sg[row] (when js is not NULL) and
+ * jty [n][W] = sum over column i's entries, in that order from 0, of js * y[row] (no fused multiply-add). */
+int ato_ipm_js_jty(int32_t n, int32_t nnz, int32_t W, const int32_t* col_ptr, const int32_t* src, const int32_t* row,
+                   const double* jv, const double* sg, const double* y, double* js, double* jty, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -474,3 +474,54 @@ def test_status_and_barrier_kernels_match_torch_formulation():
     assert tstop.any() and upd.any() and (want & ~upd).any()
     for got, ref in zip([upd_k] + k, [upd, ma2, torch.zeros_like(force), a2, st2, mu2, tau2, nf2]):
         assert torch.equal(got, ref)
+
+
+def test_js_jty_matches_torch_formulation():
+    ''' ato_ipm_js_jty (batched_ipm.py _js_jty on the device): Js = jv * sg[jr] and Js^T y bit for bit as the
+    torch formulation computes them (a gather, a product, a gather, a product, segment_reduce in the stable
+    column order), on a random CSR structure with empty rows and columns, NaN / inf / signed zeros, and on
+    the racetrack NLP's own structure; also without writing Js '''
+    from aircraft_trajectory_optimization_amd.solver.ipm_device import js_jty
+    dev = torch.device('cuda', torch.cuda.current_device())
+    g = torch.Generator().manual_seed(11)
+
+    def case(m, n, row_ptr, col, W):
+        nnz = len(col)
+        jr = np.repeat(np.arange(m), np.diff(row_ptr))
+        pc = np.argsort(col, kind='stable')
+        jt_len = np.bincount(col, minlength=n)
+        ptr = torch.as_tensor(np.concatenate([[0], np.cumsum(jt_len)]), dtype=torch.int32, device=dev)
+        src = torch.as_tensor(pc, dtype=torch.int32, device=dev)
+        row = torch.as_tensor(jr[pc], dtype=torch.int32, device=dev)
+        jv = torch.randn((nnz, W), generator=g, dtype=torch.float64) * 10 ** (6 * torch.rand((nnz, W), generator=g) - 3)
+        sg = torch.rand((m, W), generator=g, dtype=torch.float64) + 1e-3
+        y = torch.randn((m, W), generator=g, dtype=torch.float64) * 1e2
+        if nnz > 4:
+            jv[1, :3] = float('nan')
+            jv[2, 4] = float('inf')
+            jv[3, 5] = -0.0
+        jvd, sgd, yd = jv.to(dev), sg.to(dev), y.to(dev)
+        js, jty = js_jty(jvd, sgd, yd, ptr, src, row)
+        # the torch formulation, on the device (batched_ipm.py _JTy / _segsum)
+        jrd = torch.as_tensor(jr, dtype=torch.long, device=dev)
+        Js = jvd * sgd[jrd]
+        ref = torch.segment_reduce(Js[torch.as_tensor(pc, device=dev)] * yd[torch.as_tensor(jr[pc], device=dev)],
+                                   'sum', lengths=torch.as_tensor(jt_len, device=dev), axis=0, unsafe=True)
+        assert torch.equal(js.isnan(), Js.isnan()) and torch.equal(js.nan_to_num(), Js.nan_to_num())
+        assert torch.equal(jty.isnan(), ref.isnan()) and torch.equal(jty.nan_to_num(), ref.nan_to_num())
+        assert torch.equal(torch.signbit(js), torch.signbit(Js))
+        none, jty2 = js_jty(jvd, sgd, yd, ptr, src, row, want_js=False)
+        assert none is None and torch.equal(jty2.nan_to_num(), ref.nan_to_num())
+
+    # random structure: rows of 0..12 entries, column indices with repeats across rows, some empty columns
+    m, n = 300, 257
+    lens = np.random.default_rng(4).integers(0, 13, size=m)
+    col = np.concatenate([np.sort(np.random.default_rng(5 + i).choice(n - 7, size=k, replace=False))
+                          for i, k in enumerate(lens)]).astype(np.int64)
+    case(m, n, np.concatenate([[0], np.cumsum(lens)]), col, 301)
+    # the racetrack NLP's Jacobian structure (config 3), narrow batch
+    from aircraft_trajectory_optimization_amd.raceline.batched import BatchedNLP
+    from aircraft_trajectory_optimization_amd.tracks import make_spec
+    bn = BatchedNLP(make_spec(track='race', N=50, K=4), 2, device=dev)
+    nw, ng, nnz = bn.sizes
+    case(ng, nw, np.asarray(bn.row_ptr), np.asarray(bn.col, dtype=np.int64), 67)

@@ -54,6 +54,10 @@ for s in $STEPS; do
                    ATO_KKT_SADDLE=1 ATO_KKT_SADDLE_TAU=$t run c3_sad_tau$t 600 python -u tools/solver_ab.py --what config3 --tag "saddle tau $t" --out "$OUT/c3_sad_tau$t.json"
                done ;;
         bench5solve) run bench5_dcm_solve 1100 python -u bench.py --track fig8 --pose dcm --batch ${B5:-8192} --max-iter ${B5_MAXIT:-150} --no-cpu-baseline --progress 20 ;;
+        jtyab) run pytest_jty 200 python -u -m pytest tests/test_gpu_ipm_kernels.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider -k js_jty
+               for v in 0 1; do
+                   ATO_IPM_FUSED_JTY=$v run solve_jty$v 600 python tools/solve_batched.py --batch 512 --max-iter 1000 --cold --no-host --out "$OUT/solve_jty$v.json"
+               done ;;
         bench5j32) run bench5_dcm_jac32 1100 python -u bench.py --track fig8 --pose dcm --batch ${B5:-8192} --max-iter ${B5_MAXIT:-150} --jac32 --tol 1e-6 --no-cpu-baseline --progress 20 ;;
         bench4) run bench4_obstacles 900 python bench.py --track obstacles --batch 512 --no-cpu-baseline ;;
         abnew) run ab_new 900 python -u tools/solver_ab.py --what ${AB_WHAT:-fig8,config3} --tag new --out "$OUT/ab_new.json" ;;
