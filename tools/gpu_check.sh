@@ -137,6 +137,8 @@ for s in $STEPS; do
         prof5) run prof5 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof5" -o run -- \
                    python bench.py --track fig8 --pose dcm --dtype f32 --batch 8192 --no-solve --no-cpu-baseline --eval-steps 30 ;;
         solvelapscold) ATO_IPM_PROFILE=1 run solvelaps_cold 600 python tools/solve_batched.py --batch 512 --max-iter 200 --cold --no-host --out "$OUT/solvelaps_cold.json" ;;
+        solveprofnd) HIP_ENABLE_DEFERRED_LOADING=0 run solveprof_cold_nodefer 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/solveprof_cold_nodefer" -o run -- \
+                   python tools/solve_batched.py --batch 512 --max-iter 200 --cold --no-host --out "$OUT/solveprof_cold_nodefer.json" ;;
         solveprofcold) run solveprof_cold 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/solveprof_cold" -o run -- \
                    python tools/solve_batched.py --batch 512 --max-iter 200 --cold --no-host --out "$OUT/solveprof_cold.json" ;;
         s16ab) i=0
